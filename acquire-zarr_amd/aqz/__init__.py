@@ -1,0 +1,397 @@
+"""Python binding of the MI355X multiscale stage (C ABI: include/aqz_gpu.h).
+
+Thin ctypes layer used by tests/ and bench.py.  The compute runs in the HIP
+library ``acquire-zarr_amd/libaqz_gpu.so``; there is no CPU fallback -- if the
+library is missing and cannot be built, importing this module raises.
+
+Mirrors the reference interfaces:
+  Dims         <- ArrayDimensions   (src/streaming/array.dimensions.hh:45)
+  Downsampler  <- zarr::Downsampler (src/streaming/downsampler.hh:12-64)
+  Stage        <- MultiscaleArray::write_frame hot path
+                  (src/streaming/multiscale.array.cpp:57-74, 291-325)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libaqz_gpu.so")
+
+UINT8, UINT16, UINT32, UINT64, INT8, INT16, INT32, INT64, FLOAT32, FLOAT64 = range(10)
+DECIMATE, MEAN, MIN, MAX = range(4)
+SPACE, CHANNEL, TIME, OTHER = range(4)
+MEM_HOST, MEM_DEVICE = 0, 1
+
+NP_DTYPES = {UINT8: np.uint8, UINT16: np.uint16, UINT32: np.uint32,
+             UINT64: np.uint64, INT8: np.int8, INT16: np.int16,
+             INT32: np.int32, INT64: np.int64, FLOAT32: np.float32,
+             FLOAT64: np.float64}
+
+STATUS = {0: "Success", 1: "InvalidArgument", 2: "Overflow", 3: "InvalidIndex",
+          4: "NotYetImplemented", 5: "InternalError", 6: "OutOfMemory",
+          9: "InvalidSettings", 12: "WriteOutOfBounds"}
+
+
+class AqzError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        super().__init__(f"{what}: {STATUS.get(status, status)} ({status})")
+        self.status = status
+
+
+class Dimension(C.Structure):
+    _fields_ = [("type", C.c_int32), ("array_size_px", C.c_uint32),
+                ("chunk_size_px", C.c_uint32),
+                ("shard_size_chunks", C.c_uint32)]
+
+
+class ArrayDescC(C.Structure):
+    _fields_ = [("dimensions", C.POINTER(Dimension)),
+                ("dimension_count", C.c_size_t),
+                ("data_type", C.c_int32), ("multiscale", C.c_int32),
+                ("downsampling_method", C.c_int32),
+                ("max_levels", C.c_uint32),
+                ("storage_dimension_order", C.POINTER(C.c_size_t)),
+                ("device", C.c_int32)]
+
+
+class StageOptionsC(C.Structure):
+    _fields_ = [("layer_slots", C.c_uint32), ("max_batch_frames", C.c_uint32),
+                ("force_levels", C.c_uint32), ("skip_level0_split", C.c_int32)]
+
+
+class LevelLayoutC(C.Structure):
+    _fields_ = [("bytes_per_chunk", C.c_uint64),
+                ("chunks_per_layer", C.c_uint32), ("layer_slots", C.c_uint32),
+                ("frames_per_layer", C.c_uint64), ("frame_bytes", C.c_uint64),
+                ("width", C.c_uint32), ("height", C.c_uint32)]
+
+
+def build_library(force: bool = False) -> str:
+    """Compile libaqz_gpu.so for gfx950 in-tree (hipcc, no GPU needed)."""
+    if force or not os.path.exists(LIB_PATH):
+        jobs = str(min(8, os.cpu_count() or 1))
+        subprocess.run(["make", "-C", PKG_DIR, "-j" + jobs], check=True,
+                       stdout=subprocess.DEVNULL)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    build_library()
+    L = C.CDLL(LIB_PATH)
+    vp, sz, i32, u32, u64 = C.c_void_p, C.c_size_t, C.c_int32, C.c_uint32, C.c_uint64
+    D = C.POINTER(Dimension)
+    sig = {
+        "aqz_version": ([], C.c_char_p),
+        "aqz_status_message": ([i32], C.c_char_p),
+        "aqz_device_count": ([C.POINTER(i32)], i32),
+        "aqz_dims_create": ([D, sz, i32, C.POINTER(sz), C.POINTER(vp)], i32),
+        "aqz_dims_destroy": ([vp], None),
+        "aqz_dims_ndims": ([vp], sz),
+        "aqz_dims_get": ([vp, sz, D], i32),
+        "aqz_dims_tile_group_offset": ([vp, u64], u32),
+        "aqz_dims_chunk_internal_offset": ([vp, u64], u64),
+        "aqz_dims_chunk_lattice_index": ([vp, u64, u32], u32),
+        "aqz_dims_transpose_frame_id": ([vp, u64], u64),
+        "aqz_dims_bytes_per_chunk": ([vp], u64),
+        "aqz_dims_number_of_chunks_in_memory": ([vp], u32),
+        "aqz_dims_frames_per_chunk_layer": ([vp], u64),
+        "aqz_dims_shard_index_for_chunk": ([vp, u32], u32),
+        "aqz_dims_shard_internal_index": ([vp, u32], u32),
+        "aqz_pyramid_levels": ([D, sz, u32, C.POINTER(u32), D, sz], i32),
+        "aqz_downsampler_create": ([C.POINTER(ArrayDescC), C.POINTER(vp)], i32),
+        "aqz_downsampler_destroy": ([vp], None),
+        "aqz_downsampler_n_levels": ([vp], u32),
+        "aqz_downsampler_level_dims": ([vp, u32, D, sz, C.POINTER(sz)], i32),
+        "aqz_downsampler_add_frame": ([vp, vp, sz, i32], i32),
+        "aqz_downsampler_take_frame": ([vp, u32, vp, sz, i32, C.POINTER(sz), C.POINTER(i32)], i32),
+        "aqz_downsampler_method_name": ([vp], C.c_char_p),
+        "aqz_downsampler_metadata_json": ([vp, C.c_char_p, sz, C.POINTER(sz)], i32),
+        "aqz_stage_create": ([C.POINTER(ArrayDescC), C.POINTER(StageOptionsC), C.POINTER(vp)], i32),
+        "aqz_stage_destroy": ([vp], None),
+        "aqz_stage_n_levels": ([vp], u32),
+        "aqz_stage_level_dims": ([vp, u32, D, sz, C.POINTER(sz)], i32),
+        "aqz_stage_level_layout": ([vp, u32, C.POINTER(LevelLayoutC)], i32),
+        "aqz_stage_set_stream": ([vp, vp], i32),
+        "aqz_stage_append": ([vp, vp, u64, i32], i32),
+        "aqz_stage_synchronize": ([vp], i32),
+        "aqz_stage_frames_written": ([vp, u32], u64),
+        "aqz_stage_copy_layer": ([vp, u32, u64, vp, sz, vp, sz, i32], i32),
+        "aqz_stage_device_layer": ([vp, u32, u64, C.POINTER(vp), C.POINTER(vp)], i32),
+        "aqz_stage_finalize": ([vp], i32),
+        "aqz_stage_enable_kernel_timing": ([vp, i32], i32),
+        "aqz_stage_kernel_timing": ([vp, C.POINTER(C.c_double), C.POINTER(u64)], i32),
+        "aqz_stage_dominant_kernel": ([vp], C.c_char_p),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _check(status: int, what: str) -> None:
+    if status != 0:
+        raise AqzError(status, what)
+
+
+def device_count() -> int:
+    n = C.c_int32(0)
+    _check(lib().aqz_device_count(C.byref(n)), "aqz_device_count")
+    return n.value
+
+
+def _dims_c(dims):
+    arr = (Dimension * len(dims))()
+    for i, d in enumerate(dims):
+        arr[i] = Dimension(*d)
+    return arr
+
+
+def _tuples(arr, n):
+    return [(arr[i].type, arr[i].array_size_px, arr[i].chunk_size_px,
+             arr[i].shard_size_chunks) for i in range(n)]
+
+
+class Dims:
+    """ArrayDimensions on the host restatement in libaqz_gpu (no GPU)."""
+
+    def __init__(self, dims, dtype, storage_order=None):
+        self._keep = _dims_c(dims)
+        order = None
+        if storage_order is not None:
+            order = (C.c_size_t * len(storage_order))(*storage_order)
+        h = C.c_void_p()
+        _check(lib().aqz_dims_create(self._keep, len(dims), dtype, order,
+                                     C.byref(h)), "aqz_dims_create")
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.aqz_dims_destroy(self.h)
+            self.h = None
+
+    def ndims(self):
+        return lib().aqz_dims_ndims(self.h)
+
+    def dims(self):
+        out = []
+        for i in range(self.ndims()):
+            d = Dimension()
+            _check(lib().aqz_dims_get(self.h, i, C.byref(d)), "aqz_dims_get")
+            out.append((d.type, d.array_size_px, d.chunk_size_px, d.shard_size_chunks))
+        return out
+
+    def tile_group_offset(self, fid):
+        return lib().aqz_dims_tile_group_offset(self.h, fid)
+
+    def chunk_internal_offset(self, fid):
+        return lib().aqz_dims_chunk_internal_offset(self.h, fid)
+
+    def chunk_lattice_index(self, fid, dim):
+        return lib().aqz_dims_chunk_lattice_index(self.h, fid, dim)
+
+    def transpose_frame_id(self, fid):
+        return lib().aqz_dims_transpose_frame_id(self.h, fid)
+
+    def bytes_per_chunk(self):
+        return lib().aqz_dims_bytes_per_chunk(self.h)
+
+    def number_of_chunks_in_memory(self):
+        return lib().aqz_dims_number_of_chunks_in_memory(self.h)
+
+    def frames_per_chunk_layer(self):
+        return lib().aqz_dims_frames_per_chunk_layer(self.h)
+
+    def shard_index_for_chunk(self, c):
+        return lib().aqz_dims_shard_index_for_chunk(self.h, c)
+
+    def shard_internal_index(self, c):
+        return lib().aqz_dims_shard_internal_index(self.h, c)
+
+
+def pyramid_levels(dims, max_levels=0):
+    """Level dims per Downsampler::make_writer_configurations_ (no GPU)."""
+    d = _dims_c(dims)
+    n = C.c_uint32(0)
+    _check(lib().aqz_pyramid_levels(d, len(dims), max_levels, C.byref(n), None, 0),
+           "aqz_pyramid_levels")
+    nd = max(3, len(dims))
+    out = (Dimension * (n.value * nd))()
+    _check(lib().aqz_pyramid_levels(d, len(dims), max_levels, C.byref(n), out,
+                                    n.value * nd), "aqz_pyramid_levels")
+    return [_tuples(out[l * nd:(l + 1) * nd], nd) for l in range(n.value)]
+
+
+def _desc(dims, dtype, method, max_levels, multiscale, storage_order, device):
+    keep = [_dims_c(dims)]
+    order = None
+    if storage_order is not None:
+        order = (C.c_size_t * len(storage_order))(*storage_order)
+        keep.append(order)
+    d = ArrayDescC(keep[0], len(dims), dtype, 1 if multiscale else 0, method,
+                   max_levels, order, device)
+    return d, keep
+
+
+def _ptr(buf):
+    """(pointer, mem kind) for numpy arrays / torch tensors / raw ints."""
+    if isinstance(buf, np.ndarray):
+        assert buf.flags.c_contiguous
+        return buf.ctypes.data, MEM_HOST
+    if hasattr(buf, "data_ptr"):
+        assert buf.is_contiguous()
+        return buf.data_ptr(), (MEM_DEVICE if buf.is_cuda else MEM_HOST)
+    raise TypeError(type(buf))
+
+
+class Downsampler:
+    """zarr::Downsampler on the GPU: add_frame / take_frame."""
+
+    def __init__(self, dims, dtype, method, max_levels=0, storage_order=None,
+                 device=0):
+        self.dtype = dtype
+        d, self._keep = _desc(dims, dtype, method, max_levels, True,
+                              storage_order, device)
+        h = C.c_void_p()
+        _check(lib().aqz_downsampler_create(C.byref(d), C.byref(h)),
+               "aqz_downsampler_create")
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.aqz_downsampler_destroy(self.h)
+            self.h = None
+
+    def n_levels(self):
+        return lib().aqz_downsampler_n_levels(self.h)
+
+    def level_dims(self, level):
+        out = (Dimension * 16)()
+        n = C.c_size_t(0)
+        _check(lib().aqz_downsampler_level_dims(self.h, level, out, 16, C.byref(n)),
+               "level_dims")
+        return _tuples(out, n.value)
+
+    def add_frame(self, frame):
+        p, mem = _ptr(frame)
+        nbytes = frame.nbytes if isinstance(frame, np.ndarray) else \
+            frame.numel() * frame.element_size()
+        _check(lib().aqz_downsampler_add_frame(self.h, p, nbytes, mem), "add_frame")
+
+    def take_frame(self, level):
+        d = self.level_dims(level) if level < self.n_levels() else None
+        if d is None:
+            return None
+        out = np.empty((d[-2][1], d[-1][1]), dtype=NP_DTYPES[self.dtype])
+        nb = C.c_size_t(0)
+        found = C.c_int32(0)
+        _check(lib().aqz_downsampler_take_frame(self.h, level, out.ctypes.data,
+                                                out.nbytes, MEM_HOST,
+                                                C.byref(nb), C.byref(found)),
+               "take_frame")
+        return out if found.value else None
+
+    def method_name(self):
+        return lib().aqz_downsampler_method_name(self.h).decode()
+
+    def metadata_json(self):
+        n = C.c_size_t(0)
+        _check(lib().aqz_downsampler_metadata_json(self.h, None, 0, C.byref(n)), "meta")
+        buf = C.create_string_buffer(n.value + 1)
+        _check(lib().aqz_downsampler_metadata_json(self.h, buf, n.value + 1, C.byref(n)),
+               "meta")
+        return buf.value.decode()
+
+
+class Stage:
+    """Device-resident multiscale stage: tile split + pyramid of every level."""
+
+    def __init__(self, dims, dtype, method, max_levels=0, multiscale=True,
+                 storage_order=None, device=0, layer_slots=0,
+                 max_batch_frames=0, force_levels=0, skip_level0_split=False):
+        self.dtype = dtype
+        d, self._keep = _desc(dims, dtype, method, max_levels, multiscale,
+                              storage_order, device)
+        o = StageOptionsC(layer_slots, max_batch_frames, force_levels,
+                          1 if skip_level0_split else 0)
+        h = C.c_void_p()
+        _check(lib().aqz_stage_create(C.byref(d), C.byref(o), C.byref(h)),
+               "aqz_stage_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.aqz_stage_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def n_levels(self):
+        return lib().aqz_stage_n_levels(self.h)
+
+    def level_dims(self, level):
+        out = (Dimension * 16)()
+        n = C.c_size_t(0)
+        _check(lib().aqz_stage_level_dims(self.h, level, out, 16, C.byref(n)),
+               "level_dims")
+        return _tuples(out, n.value)
+
+    def layout(self, level):
+        l = LevelLayoutC()
+        _check(lib().aqz_stage_level_layout(self.h, level, C.byref(l)), "layout")
+        return {f: getattr(l, f) for f, _ in LevelLayoutC._fields_}
+
+    def set_stream(self, stream_ptr):
+        _check(lib().aqz_stage_set_stream(self.h, stream_ptr), "set_stream")
+
+    def append(self, frames, n_frames=None):
+        p, mem = _ptr(frames)
+        if n_frames is None:
+            n_frames = frames.shape[0] if frames.ndim == 3 else 1
+        _check(lib().aqz_stage_append(self.h, p, n_frames, mem), "append")
+
+    def append_ptr(self, ptr, n_frames, mem=MEM_DEVICE):
+        _check(lib().aqz_stage_append(self.h, ptr, n_frames, mem), "append")
+
+    def synchronize(self):
+        _check(lib().aqz_stage_synchronize(self.h), "synchronize")
+
+    def frames_written(self, level):
+        return lib().aqz_stage_frames_written(self.h, level)
+
+    def copy_layer(self, level, layer):
+        lay = self.layout(level)
+        nbytes = lay["bytes_per_chunk"] * lay["chunks_per_layer"]
+        out = np.empty(nbytes, dtype=np.uint8)
+        flags = np.empty(lay["chunks_per_layer"], dtype=np.uint8)
+        _check(lib().aqz_stage_copy_layer(self.h, level, layer, out.ctypes.data,
+                                          nbytes, flags.ctypes.data, flags.size,
+                                          MEM_HOST), "copy_layer")
+        return out, flags
+
+    def finalize(self):
+        _check(lib().aqz_stage_finalize(self.h), "finalize")
+
+    def enable_kernel_timing(self, on=True):
+        _check(lib().aqz_stage_enable_kernel_timing(self.h, 1 if on else 0), "timing")
+
+    def kernel_timing(self):
+        ms = C.c_double(0)
+        n = C.c_uint64(0)
+        _check(lib().aqz_stage_kernel_timing(self.h, C.byref(ms), C.byref(n)), "timing")
+        return ms.value, n.value
+
+    def dominant_kernel(self):
+        return lib().aqz_stage_dominant_kernel(self.h).decode()

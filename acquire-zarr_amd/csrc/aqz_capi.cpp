@@ -1,0 +1,520 @@
+// aqz_capi.cpp -- extern "C" boundary (include/aqz_gpu.h).  No exception or
+// HIP error crosses it: everything maps to a ZarrStatusCode value.
+#include "aqz_gpu.h"
+
+#include "aqz_engine.hh"
+
+#include <cstring>
+#include <new>
+
+using namespace aqz;
+
+struct aqz_dims
+{
+    std::unique_ptr<ArrayDimensions> ad;
+};
+struct aqz_downsampler
+{
+    std::unique_ptr<GpuDownsampler> ds;
+    int32_t sticky = AQZ_STATUS_SUCCESS;
+};
+struct aqz_stage
+{
+    std::unique_ptr<Stage> st;
+    int32_t sticky = AQZ_STATUS_SUCCESS;
+};
+
+namespace {
+
+template<typename F>
+aqz_status
+guard(F&& f)
+{
+    try {
+        f();
+        return AQZ_STATUS_SUCCESS;
+    } catch (const Error& e) {
+        return e.status;
+    } catch (const std::bad_alloc&) {
+        return AQZ_STATUS_OUT_OF_MEMORY;
+    } catch (...) {
+        return AQZ_STATUS_INTERNAL_ERROR;
+    }
+}
+
+// Device/internal errors are sticky on an object, like ZarrStream_s::error_.
+template<typename O, typename F>
+aqz_status
+guard_sticky(O* o, F&& f)
+{
+    if (!o)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    if (o->sticky != AQZ_STATUS_SUCCESS)
+        return o->sticky;
+    const aqz_status s = guard(std::forward<F>(f));
+    if (s == AQZ_STATUS_INTERNAL_ERROR || s == AQZ_STATUS_OUT_OF_MEMORY)
+        o->sticky = s;
+    return s;
+}
+
+std::vector<Dim>
+to_dims(const aqz_dimension* d, size_t n)
+{
+    if (!d && n)
+        throw Error(AQZ_STATUS_INVALID_ARGUMENT, "null dimensions");
+    std::vector<Dim> v(n);
+    for (size_t i = 0; i < n; ++i)
+        v[i] = Dim{ d[i].type, d[i].array_size_px, d[i].chunk_size_px,
+                    d[i].shard_size_chunks };
+    return v;
+}
+
+ArrayDesc
+to_desc(const aqz_array_desc* d)
+{
+    if (!d)
+        throw Error(AQZ_STATUS_INVALID_ARGUMENT, "null desc");
+    ArrayDesc a;
+    a.dims = to_dims(d->dimensions, d->dimension_count);
+    a.dtype = d->data_type;
+    a.multiscale = d->multiscale != 0;
+    a.method = d->downsampling_method;
+    a.max_levels = d->max_levels;
+    if (d->storage_dimension_order)
+        a.storage_order.assign(d->storage_dimension_order,
+                               d->storage_dimension_order + d->dimension_count);
+    a.device = d->device;
+    if (a.dtype < 0 || a.dtype >= AQZ_DTYPE_COUNT)
+        throw Error(AQZ_STATUS_INVALID_ARGUMENT, "Invalid data type");
+    return a;
+}
+
+void
+put_dims(const std::vector<Dim>& v, aqz_dimension* out, size_t cap,
+         size_t* ndims)
+{
+    if (ndims)
+        *ndims = v.size();
+    if (out) {
+        if (cap < v.size())
+            throw Error(AQZ_STATUS_OVERFLOW, "output too small");
+        for (size_t i = 0; i < v.size(); ++i)
+            out[i] = aqz_dimension{ v[i].type, v[i].array_size_px,
+                                    v[i].chunk_size_px,
+                                    v[i].shard_size_chunks };
+    }
+}
+
+} // namespace
+
+extern "C" {
+
+const char*
+aqz_version(void)
+{
+    return "0.1.0";
+}
+
+const char*
+aqz_status_message(aqz_status s)
+{
+    // same strings as Zarr_get_status_message (src/streaming/acquire.zarr.cpp)
+    switch (s) {
+        case 0: return "Success";
+        case 1: return "Invalid argument";
+        case 2: return "Buffer overflow";
+        case 3: return "Invalid index";
+        case 4: return "Not yet implemented";
+        case 5: return "Internal error";
+        case 6: return "Out of memory";
+        case 7: return "I/O error";
+        case 8: return "Error compressing";
+        case 9: return "Invalid settings";
+        case 10: return "Refusing to overwrite existing data";
+        case 11: return "Data partially written";
+        case 12: return "Attempted write beyond array boundary";
+        case 13: return "Array key not found";
+        default: return "Unknown error";
+    }
+}
+
+aqz_status
+aqz_device_count(int32_t* count)
+{
+    if (!count)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        n = 0;
+    }
+    *count = n;
+    return AQZ_STATUS_SUCCESS;
+}
+
+// ---- dims ----------------------------------------------------------------
+aqz_status
+aqz_dims_create(const aqz_dimension* dims, size_t ndims, int32_t data_type,
+                const size_t* storage_order, aqz_dims** out)
+{
+    if (!out)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    *out = nullptr;
+    return guard([&] {
+        std::vector<size_t> ord;
+        if (storage_order)
+            ord.assign(storage_order, storage_order + ndims);
+        auto* d = new aqz_dims;
+        try {
+            d->ad = std::make_unique<ArrayDimensions>(to_dims(dims, ndims),
+                                                      data_type, ord);
+        } catch (...) {
+            delete d;
+            throw;
+        }
+        *out = d;
+    });
+}
+
+void
+aqz_dims_destroy(aqz_dims* d)
+{
+    delete d;
+}
+
+size_t
+aqz_dims_ndims(const aqz_dims* d)
+{
+    return d ? d->ad->ndims() : 0;
+}
+
+aqz_status
+aqz_dims_get(const aqz_dims* d, size_t i, aqz_dimension* out)
+{
+    if (!d || !out || i >= d->ad->ndims())
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    const Dim& x = d->ad->at(i);
+    *out = aqz_dimension{ x.type, x.array_size_px, x.chunk_size_px,
+                          x.shard_size_chunks };
+    return AQZ_STATUS_SUCCESS;
+}
+
+uint32_t
+aqz_dims_tile_group_offset(const aqz_dims* d, uint64_t fid)
+{
+    return d->ad->tile_group_offset(fid);
+}
+
+uint64_t
+aqz_dims_chunk_internal_offset(const aqz_dims* d, uint64_t fid)
+{
+    return d->ad->chunk_internal_offset(fid);
+}
+
+uint32_t
+aqz_dims_chunk_lattice_index(const aqz_dims* d, uint64_t fid, uint32_t dim)
+{
+    try {
+        return d->ad->chunk_lattice_index(fid, dim);
+    } catch (...) {
+        return UINT32_MAX;
+    }
+}
+
+uint64_t
+aqz_dims_transpose_frame_id(const aqz_dims* d, uint64_t fid)
+{
+    try {
+        return d->ad->transpose_frame_id(fid);
+    } catch (...) {
+        return UINT64_MAX;
+    }
+}
+
+uint64_t
+aqz_dims_bytes_per_chunk(const aqz_dims* d)
+{
+    return d->ad->bytes_per_chunk();
+}
+
+uint32_t
+aqz_dims_number_of_chunks_in_memory(const aqz_dims* d)
+{
+    return d->ad->number_of_chunks_in_memory();
+}
+
+uint64_t
+aqz_dims_frames_per_chunk_layer(const aqz_dims* d)
+{
+    return d->ad->frames_per_chunk_layer();
+}
+
+uint32_t
+aqz_dims_shard_index_for_chunk(const aqz_dims* d, uint32_t c)
+{
+    try {
+        return d->ad->shard_index_for_chunk(c);
+    } catch (...) {
+        return UINT32_MAX;
+    }
+}
+
+uint32_t
+aqz_dims_shard_internal_index(const aqz_dims* d, uint32_t c)
+{
+    try {
+        return d->ad->shard_internal_index(c);
+    } catch (...) {
+        return UINT32_MAX;
+    }
+}
+
+aqz_status
+aqz_pyramid_levels(const aqz_dimension* dims, size_t ndims, uint32_t max_levels,
+                   uint32_t* n_levels, aqz_dimension* out_dims, size_t out_cap)
+{
+    return guard([&] {
+        auto v = to_dims(dims, ndims);
+        if (v.size() == 2)
+            v.insert(v.begin(), Dim{ kOther, 1, 1, 1 });
+        const auto levels = make_pyramid_levels(v, max_levels);
+        if (n_levels)
+            *n_levels = uint32_t(levels.size());
+        if (out_dims) {
+            if (out_cap < levels.size() * v.size())
+                throw Error(AQZ_STATUS_OVERFLOW, "output too small");
+            size_t j = 0;
+            for (const auto& l : levels)
+                for (const auto& x : l)
+                    out_dims[j++] = aqz_dimension{ x.type, x.array_size_px,
+                                                   x.chunk_size_px,
+                                                   x.shard_size_chunks };
+        }
+    });
+}
+
+// ---- downsampler -------------------------------------------------------------
+aqz_status
+aqz_downsampler_create(const aqz_array_desc* desc, aqz_downsampler** out)
+{
+    if (!out)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    *out = nullptr;
+    return guard([&] {
+        const ArrayDesc a = to_desc(desc);
+        auto* d = new aqz_downsampler;
+        try {
+            d->ds = std::make_unique<GpuDownsampler>(a);
+        } catch (...) {
+            delete d;
+            throw;
+        }
+        *out = d;
+    });
+}
+
+void
+aqz_downsampler_destroy(aqz_downsampler* ds)
+{
+    try {
+        delete ds;
+    } catch (...) {
+    }
+}
+
+uint32_t
+aqz_downsampler_n_levels(const aqz_downsampler* ds)
+{
+    return ds ? ds->ds->n_levels() : 0;
+}
+
+aqz_status
+aqz_downsampler_level_dims(const aqz_downsampler* ds, uint32_t level,
+                           aqz_dimension* out, size_t cap, size_t* ndims)
+{
+    if (!ds)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard([&] { put_dims(ds->ds->level_dims(level), out, cap, ndims); });
+}
+
+aqz_status
+aqz_downsampler_add_frame(aqz_downsampler* ds, const void* frame, size_t nbytes,
+                          int32_t mem)
+{
+    return guard_sticky(ds, [&] { ds->ds->add_frame(frame, nbytes, mem); });
+}
+
+aqz_status
+aqz_downsampler_take_frame(aqz_downsampler* ds, uint32_t level, void* dst,
+                           size_t cap, int32_t mem, size_t* nbytes,
+                           int32_t* found)
+{
+    return guard_sticky(ds, [&] {
+        const bool f = ds->ds->take_frame(level, dst, cap, mem, nbytes);
+        if (found)
+            *found = f ? 1 : 0;
+    });
+}
+
+const char*
+aqz_downsampler_method_name(const aqz_downsampler* ds)
+{
+    return ds ? ds->ds->method_name() : "";
+}
+
+aqz_status
+aqz_downsampler_metadata_json(const aqz_downsampler* ds, char* buf, size_t cap,
+                              size_t* len)
+{
+    if (!ds)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard([&] {
+        const std::string s = ds->ds->metadata_json();
+        if (len)
+            *len = s.size();
+        if (buf) {
+            if (cap < s.size() + 1)
+                throw Error(AQZ_STATUS_OVERFLOW, "buffer too small");
+            std::memcpy(buf, s.c_str(), s.size() + 1);
+        }
+    });
+}
+
+// ---- stage ---------------------------------------------------------------------
+aqz_status
+aqz_stage_create(const aqz_array_desc* desc, const aqz_stage_options* opt,
+                 aqz_stage** out)
+{
+    if (!out)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    *out = nullptr;
+    return guard([&] {
+        const ArrayDesc a = to_desc(desc);
+        StageOptions o;
+        if (opt) {
+            o.layer_slots = opt->layer_slots;
+            o.max_batch_frames = opt->max_batch_frames;
+            o.force_levels = opt->force_levels;
+            o.skip_level0_split = opt->skip_level0_split != 0;
+        }
+        auto* s = new aqz_stage;
+        try {
+            s->st = std::make_unique<Stage>(a, o);
+        } catch (...) {
+            delete s;
+            throw;
+        }
+        *out = s;
+    });
+}
+
+void
+aqz_stage_destroy(aqz_stage* st)
+{
+    try {
+        delete st;
+    } catch (...) {
+    }
+}
+
+uint32_t
+aqz_stage_n_levels(const aqz_stage* st)
+{
+    return st ? st->st->n_levels() : 0;
+}
+
+aqz_status
+aqz_stage_level_dims(const aqz_stage* st, uint32_t level, aqz_dimension* out,
+                     size_t cap, size_t* ndims)
+{
+    if (!st)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard([&] { put_dims(st->st->level_dims(level), out, cap, ndims); });
+}
+
+aqz_status
+aqz_stage_level_layout(const aqz_stage* st, uint32_t level,
+                       aqz_level_layout* out)
+{
+    if (!st || !out)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard([&] {
+        const LevelLayout l = st->st->layout(level);
+        *out = aqz_level_layout{ l.bytes_per_chunk, l.chunks_per_layer,
+                                 l.layer_slots,     l.frames_per_layer,
+                                 l.frame_bytes,     l.width,
+                                 l.height };
+    });
+}
+
+aqz_status
+aqz_stage_set_stream(aqz_stage* st, void* stream)
+{
+    return guard_sticky(
+      st, [&] { st->st->set_stream(static_cast<hipStream_t>(stream)); });
+}
+
+aqz_status
+aqz_stage_append(aqz_stage* st, const void* frames, uint64_t n_frames,
+                 int32_t mem)
+{
+    return guard_sticky(st, [&] { st->st->append(frames, n_frames, mem); });
+}
+
+aqz_status
+aqz_stage_synchronize(aqz_stage* st)
+{
+    return guard_sticky(st, [&] { st->st->synchronize(); });
+}
+
+uint64_t
+aqz_stage_frames_written(const aqz_stage* st, uint32_t level)
+{
+    if (!st || level >= st->st->n_levels())
+        return 0;
+    return st->st->frames_written(level);
+}
+
+aqz_status
+aqz_stage_copy_layer(aqz_stage* st, uint32_t level, uint64_t layer, void* dst,
+                     size_t cap, uint8_t* has_data, size_t has_data_cap,
+                     int32_t mem)
+{
+    return guard_sticky(st, [&] {
+        st->st->copy_layer(level, layer, dst, cap, has_data, has_data_cap, mem);
+    });
+}
+
+aqz_status
+aqz_stage_device_layer(aqz_stage* st, uint32_t level, uint64_t layer,
+                       void** chunks, uint32_t** has_data)
+{
+    return guard_sticky(
+      st, [&] { st->st->device_layer(level, layer, chunks, has_data); });
+}
+
+aqz_status
+aqz_stage_finalize(aqz_stage* st)
+{
+    return guard_sticky(st, [&] { st->st->finalize(); });
+}
+
+aqz_status
+aqz_stage_enable_kernel_timing(aqz_stage* st, int32_t enable)
+{
+    return guard_sticky(st, [&] { st->st->enable_timing(enable != 0); });
+}
+
+aqz_status
+aqz_stage_kernel_timing(aqz_stage* st, double* total_ms, uint64_t* launches)
+{
+    return guard_sticky(st, [&] { st->st->timing(total_ms, launches); });
+}
+
+const char*
+aqz_stage_dominant_kernel(const aqz_stage* st)
+{
+    return st ? st->st->dominant_kernel() : "";
+}
+
+} // extern "C"

@@ -1,0 +1,962 @@
+// aqz_engine.cpp -- see aqz_engine.hh.  Citations are to
+// /root/reference/src/streaming/.
+#include "aqz_engine.hh"
+
+#include <algorithm>
+#include <cstring>
+
+namespace aqz {
+
+
+constexpr int kMemDevice = 1;
+
+void
+hip_check(hipError_t e, const char* what)
+{
+    if (e != hipSuccess) {
+        (void)hipGetLastError(); // clear
+        throw Error(e == hipErrorOutOfMemory ? 6 : 5,
+                    std::string(what) + ": " + hipGetErrorString(e));
+    }
+}
+
+DevBuf::~DevBuf()
+{
+    if (p)
+        (void)hipFree(p);
+}
+
+DevBuf::DevBuf(DevBuf&& o) noexcept
+  : p(o.p)
+  , n(o.n)
+{
+    o.p = nullptr;
+    o.n = 0;
+}
+
+DevBuf&
+DevBuf::operator=(DevBuf&& o) noexcept
+{
+    if (this != &o) {
+        if (p)
+            (void)hipFree(p);
+        p = o.p;
+        n = o.n;
+        o.p = nullptr;
+        o.n = 0;
+    }
+    return *this;
+}
+
+void
+DevBuf::alloc(size_t bytes)
+{
+    if (p && n >= bytes)
+        return;
+    if (p)
+        (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    if (bytes == 0)
+        return;
+    void* q = nullptr;
+    hip_check(hipMalloc(&q, bytes), "hipMalloc");
+    p = static_cast<uint8_t*>(q);
+    n = bytes;
+}
+
+PinnedBuf::~PinnedBuf()
+{
+    if (p)
+        (void)hipHostFree(p);
+}
+
+void
+PinnedBuf::alloc(size_t bytes)
+{
+    if (p && n >= bytes)
+        return;
+    if (p)
+        (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+    if (bytes == 0)
+        return;
+    void* q = nullptr;
+    hip_check(hipHostMalloc(&q, bytes, hipHostMallocDefault), "hipHostMalloc");
+    p = static_cast<uint8_t*>(q);
+    n = bytes;
+}
+
+static hipMemcpyKind
+kind_from(int src_mem, int dst_mem)
+{
+    if (src_mem == kMemDevice)
+        return dst_mem == kMemDevice ? hipMemcpyDeviceToDevice
+                                     : hipMemcpyDeviceToHost;
+    return dst_mem == kMemDevice ? hipMemcpyHostToDevice : hipMemcpyHostToHost;
+}
+
+static bool
+method_valid(int32_t m)
+{
+    return m >= 0 && m < 4;
+}
+
+// ===========================================================================
+// Stage
+// ===========================================================================
+Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
+  : desc_(desc)
+  , opt_(opt)
+{
+    bpp_ = bytes_of_type(desc.dtype);
+    if (desc.multiscale && !method_valid(desc.method))
+        throw Error(1, "Invalid downsampling method");
+    if (opt_.layer_slots == 0)
+        opt_.layer_slots = 2;
+    if (opt_.max_batch_frames == 0)
+        opt_.max_batch_frames = 64;
+
+    auto base = std::make_unique<ArrayDimensions>(desc.dims, desc.dtype,
+                                                  desc.storage_order);
+    if (base->needs_xy_transposition())
+        throw Error(4, "XY-transposed storage order is not implemented on "
+                       "the GPU stage");
+    std::vector<std::vector<Dim>> levels;
+    if (desc.multiscale)
+        levels = make_pyramid_levels(base->dims(), desc.max_levels,
+                                     opt_.force_levels);
+    else
+        levels = { base->dims() };
+
+    hip_check(hipSetDevice(desc.device), "hipSetDevice");
+    hip_check(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking),
+              "hipStreamCreate");
+    stream_ = own_stream_;
+
+    const size_t n = base->ndims();
+    const uint32_t B = opt_.max_batch_frames;
+    lv_.resize(levels.size());
+    for (size_t k = 0; k < levels.size(); ++k) {
+        StageLevel& L = lv_[k];
+        L.dims = levels[k];
+        if (k == 0)
+            L.ad = std::move(base);
+        else
+            L.ad = std::make_unique<ArrayDimensions>(L.dims, desc.dtype);
+        L.W = L.dims[n - 1].array_size_px;
+        L.H = L.dims[n - 2].array_size_px;
+        L.planes = L.dims[n - 3].array_size_px;
+        if (k > 0)
+            L.xy_shrinks = L.W < lv_[k - 1].W || L.H < lv_[k - 1].H;
+        L.tw = L.dims[n - 1].chunk_size_px;
+        L.th = L.dims[n - 2].chunk_size_px;
+        L.ntx = parts_along(L.W, L.tw);
+        L.nty = parts_along(L.H, L.th);
+        L.bpc = L.ad->bytes_per_chunk();
+        L.n_chunks = L.ad->number_of_chunks_in_memory();
+        const uint64_t F = L.ad->frames_per_chunk_layer();
+        if (F == 0 || F > 0x7fffffffull)
+            throw Error(9, "unsupported frames per chunk layer");
+        L.F = uint32_t(F);
+        L.slot_bytes = L.bpc * L.n_chunks;
+        L.n_slots = std::max<uint32_t>(opt_.layer_slots,
+                                       (B - 1 + L.F - 1) / L.F + 1);
+        L.needs_zero = (L.W % L.tw) != 0 || (L.H % L.th) != 0;
+        for (size_t i = 1; i + 2 < n; ++i)
+            L.needs_zero |= (L.dims[i].array_size_px % L.dims[i].chunk_size_px) != 0;
+        L.slot_layer.assign(L.n_slots, -1);
+
+        if (!(k == 0 && opt_.skip_level0_split)) {
+            L.ring.alloc(L.slot_bytes * L.n_slots);
+            L.flags.alloc(size_t(L.n_chunks) * L.n_slots * 4);
+            hip_check(hipMemsetAsync(L.flags.p, 0, L.flags.n, stream_),
+                      "hipMemsetAsync");
+        }
+        // per-frame chunk addressing table (periodic in frames_per_layer)
+        L.h_tab_off.resize(L.F);
+        L.h_tab_grp.resize(L.F);
+        for (uint32_t fl = 0; fl < L.F; ++fl) {
+            const uint64_t sf = L.ad->transpose_frame_id(fl);
+            const uint32_t grp = L.ad->tile_group_offset(sf);
+            L.h_tab_grp[fl] = grp;
+            L.h_tab_off[fl] = uint64_t(grp) * L.bpc + L.ad->chunk_internal_offset(sf);
+        }
+        L.tab_off.alloc(size_t(L.F) * 8);
+        L.tab_grp.alloc(size_t(L.F) * 4);
+        hip_check(hipMemcpy(L.tab_off.p, L.h_tab_off.data(), size_t(L.F) * 8,
+                            hipMemcpyHostToDevice),
+                  "hipMemcpy");
+        hip_check(hipMemcpy(L.tab_grp.p, L.h_tab_grp.data(), size_t(L.F) * 4,
+                            hipMemcpyHostToDevice),
+                  "hipMemcpy");
+    }
+
+    // 2-D fast path: z never shrinks and XY shrinks at every level, so every
+    // input frame emits exactly one frame per level (downsampler.cpp:358-399)
+    fused_2d_ = true;
+    for (size_t k = 1; k < lv_.size(); ++k)
+        fused_2d_ &= !(lv_[k].planes < lv_[k - 1].planes) && lv_[k].xy_shrinks;
+    n_fused_ = fused_2d_ ? std::min<uint32_t>(n_levels() - 1, kMaxFused) : 0;
+    rh_log2_ = std::max<uint32_t>(4, n_fused_);
+
+    const Dim& d0 = lv_[0].dims[0];
+    if (d0.array_size_px > 0) {
+        max_frames_ = 1;
+        for (size_t i = 0; i + 2 < n; ++i)
+            max_frames_ *= lv_[0].dims[i].array_size_px;
+    }
+    pend_.resize(lv_.size());
+    for (auto& e : stage_ev_)
+        hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming),
+                  "hipEventCreate");
+    for (auto& L : lv_)
+        hip_check(hipEventCreateWithFlags(&L.ops_ev, hipEventDisableTiming),
+                  "hipEventCreate");
+    hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+}
+
+Stage::~Stage()
+{
+    if (stream_)
+        (void)hipStreamSynchronize(stream_);
+    for (auto& e : stage_ev_)
+        if (e)
+            (void)hipEventDestroy(e);
+    for (auto& L : lv_)
+        if (L.ops_ev)
+            (void)hipEventDestroy(L.ops_ev);
+    for (auto& pr : ev_pairs_) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
+    if (own_stream_)
+        (void)hipStreamDestroy(own_stream_);
+}
+
+const std::vector<Dim>&
+Stage::level_dims(uint32_t level) const
+{
+    if (level >= lv_.size())
+        throw Error(3, "level out of range");
+    return lv_[level].dims;
+}
+
+LevelLayout
+Stage::layout(uint32_t level) const
+{
+    if (level >= lv_.size())
+        throw Error(3, "level out of range");
+    const StageLevel& L = lv_[level];
+    return LevelLayout{ L.bpc,   L.n_chunks,
+                        L.n_slots, L.F,
+                        uint64_t(L.W) * L.H * bpp_, L.W,
+                        L.H };
+}
+
+void
+Stage::set_stream(hipStream_t s)
+{
+    hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    stream_ = s ? s : own_stream_;
+}
+
+uint64_t
+Stage::frames_written(uint32_t level) const
+{
+    if (level >= lv_.size())
+        throw Error(3, "level out of range");
+    return lv_[level].frames_written;
+}
+
+void
+Stage::synchronize()
+{
+    hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+}
+
+void
+Stage::append(const void* frames, uint64_t n_frames, int mem)
+{
+    if (n_frames == 0)
+        return;
+    if (!frames)
+        throw Error(1, "null frames");
+    const uint64_t fbytes = uint64_t(lv_[0].W) * lv_[0].H * bpp_;
+    uint64_t n_ok = n_frames;
+    if (max_frames_ > 0) {
+        const uint64_t room = max_frames_ - std::min(max_frames_, lv_[0].frames_written);
+        n_ok = std::min(n_ok, room);
+    }
+    const auto* src = static_cast<const uint8_t*>(frames);
+    const uint32_t B = opt_.max_batch_frames;
+    for (uint64_t done = 0; done < n_ok;) {
+        const uint32_t b = uint32_t(std::min<uint64_t>(B, n_ok - done));
+        const uint8_t* p = src + done * fbytes;
+        if (mem == kMemDevice) {
+            run_batch(p, b);
+        } else {
+            // pinned double buffer: the copy of batch i+1 overlaps batch i
+            const int j = stage_idx_;
+            stage_idx_ ^= 1;
+            h_stage_[j].alloc(size_t(B) * fbytes);
+            d_stage_[j].alloc(size_t(B) * fbytes);
+            hip_check(hipEventSynchronize(stage_ev_[j]), "hipEventSynchronize");
+            std::memcpy(h_stage_[j].p, p, size_t(b) * fbytes);
+            hip_check(hipMemcpyAsync(d_stage_[j].p, h_stage_[j].p,
+                                     size_t(b) * fbytes, hipMemcpyHostToDevice,
+                                     stream_),
+                      "hipMemcpyAsync");
+            hip_check(hipEventRecord(stage_ev_[j], stream_), "hipEventRecord");
+            run_batch(d_stage_[j].p, b);
+        }
+        done += b;
+    }
+    if (n_ok < n_frames)
+        throw Error(12, "append beyond the array's bounded extent");
+}
+
+void
+Stage::run_batch(const uint8_t* dsrc, uint32_t n)
+{
+    if (fused_2d_)
+        run_fused(dsrc, n);
+    else
+        run_generic(dsrc, n);
+}
+
+void
+Stage::enter_layer(StageLevel& L, uint64_t layer)
+{
+    const uint32_t slot = uint32_t(layer % L.n_slots);
+    if (L.slot_layer[slot] == int64_t(layer))
+        return;
+    // a fresh chunk layer: has_data cleared; zeroed like Chunk's ctor
+    // (chunk.cpp:8-15) wherever tiles do not cover every byte
+    hip_check(hipMemsetAsync(L.flags.p + size_t(slot) * L.n_chunks * 4, 0,
+                             size_t(L.n_chunks) * 4, stream_),
+              "hipMemsetAsync");
+    if (L.needs_zero)
+        hip_check(hipMemsetAsync(L.ring.p + slot * L.slot_bytes, 0,
+                                 L.slot_bytes, stream_),
+                  "hipMemsetAsync");
+    L.slot_layer[slot] = int64_t(layer);
+}
+
+void
+Stage::enter_layers(StageLevel& L, uint64_t first_fid, uint64_t n)
+{
+    if (n == 0 || !L.ring.p)
+        return;
+    for (uint64_t layer = first_fid / L.F; layer <= (first_fid + n - 1) / L.F;
+         ++layer)
+        enter_layer(L, layer);
+}
+
+LevelGeom
+Stage::geom(StageLevel& L, uint64_t fid0, bool tiles, uint8_t* scratch) const
+{
+    LevelGeom g{};
+    g.W = L.W;
+    g.H = L.H;
+    g.tw = L.tw;
+    g.th = L.th;
+    g.ntx = L.ntx;
+    g.dtw = make_fastdiv(L.tw);
+    g.dth = make_fastdiv(L.th);
+    g.bpc = L.bpc;
+    g.slot_bytes = L.slot_bytes;
+    g.n_chunks = L.n_chunks;
+    g.n_slots = L.n_slots;
+    g.frames_per_layer = L.F;
+    g.fid0_mod = uint32_t(fid0 % L.F);
+    g.slot0 = uint32_t((fid0 / L.F) % L.n_slots);
+    g.base = (tiles && L.ring.p) ? L.ring.p : nullptr;
+    g.flags = reinterpret_cast<uint32_t*>(L.flags.p);
+    g.tab_off = reinterpret_cast<const uint64_t*>(L.tab_off.p);
+    g.tab_grp = reinterpret_cast<const uint32_t*>(L.tab_grp.p);
+    g.scratch = scratch;
+    return g;
+}
+
+void
+Stage::tile_addr(const StageLevel& L, uint64_t fid, uint64_t* off,
+                 uint32_t* flag_off) const
+{
+    const uint64_t slot = (fid / L.F) % L.n_slots;
+    *off = slot * L.slot_bytes + L.h_tab_off[fid % L.F];
+    *flag_off = uint32_t(slot * L.n_chunks + L.h_tab_grp[fid % L.F]);
+}
+
+void
+Stage::run_fused(const uint8_t* dsrc, uint32_t n)
+{
+    const uint32_t nl = n_levels();
+    const bool tail = nl - 1 > n_fused_;
+    const uint64_t fb0 = uint64_t(lv_[0].W) * lv_[0].H * bpp_;
+    for (uint32_t k = 0; k < nl; ++k)
+        enter_layers(lv_[k], lv_[k].frames_written, n);
+
+    FusedParams p{};
+    p.src = dsrc;
+    p.src_stride = fb0;
+    p.n_frames = n;
+    p.n_fused = n_fused_;
+    p.rh_log2 = rh_log2_;
+    const uint32_t RW = uint32_t(512 / bpp_);
+    p.nbx = parts_along(lv_[0].W, RW);
+    p.nby = parts_along(lv_[0].H, 1u << rh_log2_);
+    p.vec_rows = ((fb0 / lv_[0].H) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(dsrc) % 16 == 0)
+                   ? 1
+                   : 0;
+    for (uint32_t k = 0; k <= n_fused_; ++k) {
+        uint8_t* scr = nullptr;
+        if (tail && k == n_fused_) {
+            lv_[k].scratch.alloc(size_t(opt_.max_batch_frames) * lv_[k].W *
+                                 lv_[k].H * bpp_);
+            scr = lv_[k].scratch.p;
+        }
+        p.lv[k] = geom(lv_[k], lv_[k].frames_written, true, scr);
+    }
+
+    std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
+    if (timing_) {
+        if (ev_used_ == ev_pairs_.size()) {
+            hipEvent_t a, b;
+            hip_check(hipEventCreate(&a), "hipEventCreate");
+            hip_check(hipEventCreate(&b), "hipEventCreate");
+            ev_pairs_.emplace_back(a, b);
+        }
+        ev = &ev_pairs_[ev_used_++];
+        hip_check(hipEventRecord(ev->first, stream_), "hipEventRecord");
+    }
+    hip_check(launch_fused_pyramid(desc_.dtype, desc_.method, p, stream_),
+              "fused_pyramid launch");
+    if (ev)
+        hip_check(hipEventRecord(ev->second, stream_), "hipEventRecord");
+
+    // levels deeper than the fused depth: one generic step per level
+    for (uint32_t k = n_fused_ + 1; k < nl; ++k) {
+        StageLevel& L = lv_[k];
+        StageLevel& P = lv_[k - 1];
+        const bool more = k + 1 < nl;
+        if (more)
+            L.scratch.alloc(size_t(opt_.max_batch_frames) * L.W * L.H * bpp_);
+        hip_check(hipEventSynchronize(L.ops_ev), "hipEventSynchronize");
+        L.h_ops.alloc(size_t(opt_.max_batch_frames + 1) * sizeof(LevelOp));
+        L.d_ops.alloc(size_t(opt_.max_batch_frames + 1) * sizeof(LevelOp));
+        auto* ops = reinterpret_cast<LevelOp*>(L.h_ops.p);
+        const uint64_t pfb = uint64_t(P.W) * P.H * bpp_;
+        const uint64_t lfb = uint64_t(L.W) * L.H * bpp_;
+        for (uint32_t f = 0; f < n; ++f) {
+            LevelOp& o = ops[f];
+            o = LevelOp{};
+            o.a = P.scratch.p + f * pfb;
+            o.a_scale = L.xy_shrinks ? 1 : 0;
+            o.scratch_out = more ? L.scratch.p + f * lfb : nullptr;
+            tile_addr(L, L.frames_written + f, &o.tile_off, &o.flag_off);
+            o.has_tile = 1;
+        }
+        hip_check(hipMemcpyAsync(L.d_ops.p, ops, size_t(n) * sizeof(LevelOp),
+                                 hipMemcpyHostToDevice, stream_),
+                  "hipMemcpyAsync");
+        hip_check(hipEventRecord(L.ops_ev, stream_), "hipEventRecord");
+        LevelParams lp{};
+        lp.Wp = P.W;
+        lp.Hp = P.H;
+        lp.g = geom(L, L.frames_written, true, nullptr);
+        lp.ops = reinterpret_cast<const LevelOp*>(L.d_ops.p);
+        lp.n_ops = n;
+        hip_check(launch_level(desc_.dtype, desc_.method, lp, stream_),
+                  "level launch");
+    }
+    for (uint32_t k = 0; k < nl; ++k) {
+        lv_[k].frames_written += n;
+        lv_[k].level_frame_count += n;
+    }
+}
+
+const uint8_t*
+Stage::frame_ptr(uint32_t level, uint32_t index, const uint8_t* dsrc) const
+{
+    const StageLevel& L = lv_[level];
+    const uint64_t fb = uint64_t(L.W) * L.H * bpp_;
+    if (level == 0)
+        return dsrc + index * fb;
+    return L.scratch.p + index * fb;
+}
+
+void
+Stage::run_generic(const uint8_t* dsrc, uint32_t n)
+{
+    const uint32_t nl = n_levels();
+    const size_t nd = lv_[0].dims.size();
+    (void)nd;
+    // level 0 tile split: the fused kernel with no pyramid levels
+    if (!opt_.skip_level0_split) {
+        StageLevel& L0 = lv_[0];
+        enter_layers(L0, L0.frames_written, n);
+        FusedParams p{};
+        p.src = dsrc;
+        p.src_stride = uint64_t(L0.W) * L0.H * bpp_;
+        p.n_frames = n;
+        p.n_fused = 0;
+        p.rh_log2 = 4;
+        p.nbx = parts_along(L0.W, uint32_t(512 / bpp_));
+        p.nby = parts_along(L0.H, 16);
+        p.vec_rows = ((uint64_t(L0.W) * bpp_) % 16 == 0 &&
+                      reinterpret_cast<uintptr_t>(dsrc) % 16 == 0)
+                       ? 1
+                       : 0;
+        p.lv[0] = geom(L0, L0.frames_written, true, nullptr);
+        hip_check(launch_fused_pyramid(desc_.dtype, desc_.method, p, stream_),
+                  "level-0 split launch");
+    }
+    lv_[0].frames_written += n;
+
+    // Host simulation of the cascade (downsampler.cpp:306-401) -> ops/level.
+    struct HostOp
+    {
+        int a_kind; // 0 frame of level k-1 in batch, 1 carried partial
+        uint32_t a_index;
+        bool a_scale;
+        int has_b;
+        uint32_t b_index;
+        bool b_scale;
+        int out; // 0 scratch slot, 1 partial store
+        uint32_t out_index;
+        uint64_t fid;
+    };
+    std::vector<std::vector<HostOp>> ops(nl);
+    std::vector<uint32_t> nout(nl, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        ++lv_[0].level_frame_count;
+        uint32_t cur = i; // index of the current frame at level k-1
+        for (uint32_t k = 1; k < nl; ++k) {
+            StageLevel& L = lv_[k];
+            StageLevel& P = lv_[k - 1];
+            bool average = L.planes < P.planes;
+            if (P.planes % 2 != 0 && P.level_frame_count % P.planes == 0)
+                average = false;
+            const bool xy = L.xy_shrinks;
+            Pending& pd = pend_[k];
+            if (average) {
+                if (pd.has) {
+                    HostOp o{};
+                    o.a_kind = pd.kind;
+                    o.a_index = pd.index;
+                    o.a_scale = pd.kind == 0 ? pd.scale : false;
+                    o.has_b = 1;
+                    o.b_index = cur;
+                    o.b_scale = xy;
+                    o.out = 0;
+                    o.out_index = nout[k]++;
+                    o.fid = L.frames_written++;
+                    ops[k].push_back(o);
+                    ++L.level_frame_count;
+                    pd.has = false;
+                    cur = o.out_index;
+                } else {
+                    pd.has = true;
+                    pd.kind = 0;
+                    pd.index = cur;
+                    pd.scale = xy;
+                    break;
+                }
+            } else {
+                HostOp o{};
+                o.a_kind = 0;
+                o.a_index = cur;
+                o.a_scale = xy;
+                o.has_b = 0;
+                o.out = 0;
+                o.out_index = nout[k]++;
+                o.fid = L.frames_written++;
+                ops[k].push_back(o);
+                ++L.level_frame_count;
+                cur = o.out_index;
+            }
+        }
+    }
+    // an unpaired plane produced in this batch is carried in a partial buffer
+    std::vector<int> store_into(nl, -1);
+    for (uint32_t k = 1; k < nl; ++k) {
+        Pending& pd = pend_[k];
+        if (pd.has && pd.kind == 0) {
+            const int dst = lv_[k].carried == 0 ? 1 : 0;
+            HostOp o{};
+            o.a_kind = 0;
+            o.a_index = pd.index;
+            o.a_scale = pd.scale;
+            o.out = 1;
+            o.out_index = uint32_t(dst);
+            ops[k].push_back(o);
+            store_into[k] = dst;
+        }
+    }
+
+    // Execute level by level.
+    for (uint32_t k = 1; k < nl; ++k) {
+        StageLevel& L = lv_[k];
+        StageLevel& P = lv_[k - 1];
+        if (ops[k].empty())
+            continue;
+        const uint64_t lfb = uint64_t(L.W) * L.H * bpp_;
+        const bool more = k + 1 < nl;
+        if (more && nout[k] > 0)
+            L.scratch.alloc(size_t(opt_.max_batch_frames) * lfb);
+        if (store_into[k] >= 0)
+            L.partial[store_into[k]].alloc(lfb);
+        const size_t nops = ops[k].size();
+        hip_check(hipEventSynchronize(L.ops_ev), "hipEventSynchronize");
+        L.h_ops.alloc(size_t(opt_.max_batch_frames + 1) * sizeof(LevelOp));
+        L.d_ops.alloc(size_t(opt_.max_batch_frames + 1) * sizeof(LevelOp));
+        auto* dops = reinterpret_cast<LevelOp*>(L.h_ops.p);
+        for (size_t j = 0; j < nops; ++j) {
+            const HostOp& h = ops[k][j];
+            LevelOp& o = dops[j];
+            o = LevelOp{};
+            o.a = h.a_kind == 0 ? frame_ptr(k - 1, h.a_index, dsrc)
+                                : L.partial[L.carried].p;
+            o.a_scale = h.a_scale ? 1 : 0;
+            o.b = h.has_b ? frame_ptr(k - 1, h.b_index, dsrc) : nullptr;
+            o.b_scale = h.b_scale ? 1 : 0;
+            if (h.out == 0) {
+                o.scratch_out = more ? L.scratch.p + h.out_index * lfb : nullptr;
+                if (L.ring.p) {
+                    enter_layer(L, h.fid / L.F);
+                    tile_addr(L, h.fid, &o.tile_off, &o.flag_off);
+                    o.has_tile = 1;
+                }
+            } else {
+                o.scratch_out = L.partial[h.out_index].p;
+            }
+        }
+        (void)P;
+        hip_check(hipMemcpyAsync(L.d_ops.p, dops, nops * sizeof(LevelOp),
+                                 hipMemcpyHostToDevice, stream_),
+                  "hipMemcpyAsync");
+        hip_check(hipEventRecord(L.ops_ev, stream_), "hipEventRecord");
+        LevelParams lp{};
+        lp.Wp = P.W;
+        lp.Hp = P.H;
+        lp.g = geom(L, 0, true, nullptr);
+        lp.ops = reinterpret_cast<const LevelOp*>(L.d_ops.p);
+        lp.n_ops = uint32_t(nops);
+        hip_check(launch_level(desc_.dtype, desc_.method, lp, stream_),
+                  "level launch");
+    }
+    for (uint32_t k = 1; k < nl; ++k) {
+        if (store_into[k] >= 0) {
+            lv_[k].carried = store_into[k];
+            pend_[k].kind = 1;
+        }
+    }
+}
+
+void
+Stage::copy_layer(uint32_t level, uint64_t layer, void* dst, size_t cap,
+                  uint8_t* has_data, size_t has_data_cap, int mem)
+{
+    if (level >= lv_.size())
+        throw Error(3, "level out of range");
+    StageLevel& L = lv_[level];
+    if (!L.ring.p)
+        throw Error(1, "level 0 split disabled for this stage");
+    const uint32_t slot = uint32_t(layer % L.n_slots);
+    if (L.slot_layer[slot] != int64_t(layer))
+        throw Error(3, "chunk layer not resident");
+    if (dst && cap < L.slot_bytes)
+        throw Error(2, "destination too small for a chunk layer");
+    synchronize();
+    if (dst)
+        hip_check(hipMemcpy(dst, L.ring.p + slot * L.slot_bytes, L.slot_bytes,
+                            kind_from(kMemDevice, mem)),
+                  "hipMemcpy");
+    if (has_data) {
+        if (has_data_cap < L.n_chunks)
+            throw Error(2, "has_data too small");
+        std::vector<uint32_t> f(L.n_chunks);
+        hip_check(hipMemcpy(f.data(), L.flags.p + size_t(slot) * L.n_chunks * 4,
+                            size_t(L.n_chunks) * 4, hipMemcpyDeviceToHost),
+                  "hipMemcpy");
+        for (uint32_t c = 0; c < L.n_chunks; ++c)
+            has_data[c] = f[c] ? 1 : 0;
+    }
+}
+
+void
+Stage::device_layer(uint32_t level, uint64_t layer, void** chunks,
+                    uint32_t** flags)
+{
+    if (level >= lv_.size())
+        throw Error(3, "level out of range");
+    StageLevel& L = lv_[level];
+    const uint32_t slot = uint32_t(layer % L.n_slots);
+    if (!L.ring.p || L.slot_layer[slot] != int64_t(layer))
+        throw Error(3, "chunk layer not resident");
+    if (chunks)
+        *chunks = L.ring.p + slot * L.slot_bytes;
+    if (flags)
+        *flags = reinterpret_cast<uint32_t*>(L.flags.p) + size_t(slot) * L.n_chunks;
+}
+
+void
+Stage::finalize()
+{
+    for (auto& L : lv_) {
+        if (!L.ring.p || L.needs_zero)
+            continue; // zeroed whole on entry
+        const uint64_t fw = L.frames_written;
+        if (fw % L.F == 0)
+            continue;
+        const uint64_t end = (fw / L.F + 1) * L.F;
+        for (uint64_t fid = fw; fid < end; ++fid) {
+            uint64_t off;
+            uint32_t fo;
+            tile_addr(L, fid, &off, &fo);
+            hip_check(launch_zero_frame_tiles(L.ring.p + off, L.bpc,
+                                              L.ntx * L.nty,
+                                              uint32_t(uint64_t(L.tw) * L.th * bpp_),
+                                              stream_),
+                      "zero launch");
+        }
+    }
+    synchronize();
+}
+
+void
+Stage::enable_timing(bool on)
+{
+    synchronize();
+    timing_ = on;
+    ev_used_ = 0;
+    timed_ms_ = 0;
+    timed_launches_ = 0;
+}
+
+void
+Stage::timing(double* total_ms, uint64_t* launches)
+{
+    synchronize();
+    for (size_t i = 0; i < ev_used_; ++i) {
+        float ms = 0;
+        hip_check(hipEventElapsedTime(&ms, ev_pairs_[i].first,
+                                      ev_pairs_[i].second),
+                  "hipEventElapsedTime");
+        timed_ms_ += ms;
+        ++timed_launches_;
+    }
+    ev_used_ = 0;
+    if (total_ms)
+        *total_ms = timed_ms_;
+    if (launches)
+        *launches = timed_launches_;
+}
+
+const char*
+Stage::dominant_kernel() const
+{
+    return fused_2d_ ? "fused_pyramid" : "level_kernel";
+}
+
+// ===========================================================================
+// GpuDownsampler
+// ===========================================================================
+GpuDownsampler::GpuDownsampler(const ArrayDesc& desc)
+  : dtype_(desc.dtype)
+  , method_(desc.method)
+  , device_(desc.device)
+{
+    bpp_ = bytes_of_type(desc.dtype); // throws on invalid dtype
+    if (!method_valid(desc.method))
+        throw Error(1, "Invalid downsampling method: " +
+                         std::to_string(desc.method));
+    ArrayDimensions ad(desc.dims, desc.dtype, desc.storage_order);
+    levels_ = make_pyramid_levels(ad.dims(), desc.max_levels);
+    const size_t n = ad.ndims();
+    lv_.resize(levels_.size());
+    for (size_t k = 0; k < levels_.size(); ++k) {
+        Lv& L = lv_[k];
+        L.W = levels_[k][n - 1].array_size_px;
+        L.H = levels_[k][n - 2].array_size_px;
+        L.planes = levels_[k][n - 3].array_size_px;
+        L.xy_shrinks = k > 0 && (L.W < lv_[k - 1].W || L.H < lv_[k - 1].H);
+    }
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking),
+              "hipStreamCreate");
+}
+
+GpuDownsampler::~GpuDownsampler()
+{
+    if (stream_) {
+        (void)hipStreamSynchronize(stream_);
+        (void)hipStreamDestroy(stream_);
+    }
+}
+
+const std::vector<Dim>&
+GpuDownsampler::level_dims(uint32_t level) const
+{
+    if (level >= levels_.size())
+        throw Error(3, "level out of range");
+    return levels_[level];
+}
+
+void
+GpuDownsampler::add_frame(const void* frame, size_t nbytes, int mem)
+{
+    // downsampler.cpp:306-401
+    const uint64_t fb0 = uint64_t(lv_[0].W) * lv_[0].H * bpp_;
+    if (!frame || nbytes < fb0)
+        throw Error(1, "Expecting at least " + std::to_string(fb0) + " bytes");
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    input_.alloc(fb0);
+    hip_check(hipMemcpyAsync(input_.p, frame, fb0, kind_from(mem, kMemDevice),
+                             stream_),
+              "hipMemcpyAsync");
+    ++lv_[0].count;
+
+    // Plan this frame's cascade on the host, then run one launch per level.
+    std::vector<LevelOp> ops;
+    std::vector<uint32_t> op_level;
+    const uint8_t* cur = input_.p;
+    for (uint32_t k = 1; k < lv_.size(); ++k) {
+        Lv& L = lv_[k];
+        Lv& P = lv_[k - 1];
+        const uint64_t lfb = uint64_t(L.W) * L.H * bpp_;
+        L.cur.alloc(lfb);
+        L.pending.alloc(lfb);
+        L.partial.alloc(lfb);
+        bool average = L.planes < P.planes;
+        if (P.planes % 2 != 0 && P.count % P.planes == 0)
+            average = false;
+        LevelOp o{};
+        if (average && !L.has_partial) {
+            // partial_scaled_frames_.emplace + break (:386-389)
+            o.a = cur;
+            o.a_scale = L.xy_shrinks;
+            o.scratch_out = L.partial.p;
+            ops.push_back(o);
+            op_level.push_back(k);
+            L.has_partial = true;
+            break;
+        }
+        if (average) {
+            o.a = L.partial.p; // earlier plane, already XY-scaled
+            o.b = cur;
+            o.b_scale = L.xy_shrinks;
+            L.has_partial = false;
+        } else {
+            o.a = cur;
+            o.a_scale = L.xy_shrinks;
+        }
+        o.scratch_out = L.cur.p;
+        ops.push_back(o);
+        op_level.push_back(k);
+        // emplace_downsampled_frame_ (:599-605): a waiting frame is kept,
+        // the count advances regardless
+        ++L.count;
+        if (!L.has_pending) {
+            std::swap(L.cur, L.pending);
+            L.has_pending = true;
+            cur = L.pending.p;
+        } else {
+            cur = L.cur.p;
+        }
+    }
+    if (!ops.empty()) {
+        d_op_.alloc(ops.size() * sizeof(LevelOp));
+        hip_check(hipMemcpyAsync(d_op_.p, ops.data(), ops.size() * sizeof(LevelOp),
+                                 hipMemcpyHostToDevice, stream_),
+                  "hipMemcpyAsync");
+        for (size_t j = 0; j < ops.size(); ++j) {
+            const uint32_t k = op_level[j];
+            LevelParams lp{};
+            lp.Wp = lv_[k - 1].W;
+            lp.Hp = lv_[k - 1].H;
+            lp.g.W = lv_[k].W;
+            lp.g.H = lv_[k].H;
+            lp.ops = reinterpret_cast<const LevelOp*>(d_op_.p) + j;
+            lp.n_ops = 1;
+            hip_check(launch_level(dtype_, method_, lp, stream_),
+                      "level launch");
+        }
+    }
+    hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+}
+
+bool
+GpuDownsampler::take_frame(uint32_t level, void* dst, size_t cap, int mem,
+                           size_t* nbytes)
+{
+    // downsampler.cpp:403-414
+    if (level == 0 || level >= lv_.size() || !lv_[level].has_pending)
+        return false;
+    Lv& L = lv_[level];
+    const size_t fb = size_t(L.W) * L.H * bpp_;
+    if (nbytes)
+        *nbytes = fb;
+    if (dst) {
+        if (cap < fb)
+            throw Error(2, "destination too small");
+        hip_check(hipMemcpy(dst, L.pending.p, fb, kind_from(kMemDevice, mem)),
+                  "hipMemcpy");
+    }
+    L.has_pending = false;
+    return true;
+}
+
+const char*
+GpuDownsampler::method_name() const
+{
+    // downsampler.cpp:422-438
+    switch (method_) {
+        case 0:
+            return "decimate";
+        case 1:
+            return "local_mean";
+        case 2:
+            return "local_min";
+        default:
+            return "local_max";
+    }
+}
+
+std::string
+GpuDownsampler::metadata_json() const
+{
+    // downsampler.cpp:440-485, serialised with sorted keys as nlohmann does
+    switch (method_) {
+        case 1:
+            return "{\"description\":\"The fields in the metadata describe how "
+                   "to reproduce this multiscaling in scikit-image. The method "
+                   "and its parameters are given here.\",\"kwargs\":{\"cval\":"
+                   "\"0\",\"factors\":\"(2, 2)\"},\"method\":\"skimage."
+                   "transform.downscale_local_mean\",\"version\":\"0.25.2\"}";
+        case 0:
+            return "{\"args\":[\"(slice(0, None, 2), slice(0, None, 2))\"],"
+                   "\"description\":\"Subsampling by taking every 2nd "
+                   "pixel/voxel (top-left corner of each 2x2 block). "
+                   "Equivalent to numpy array slicing with stride 2.\","
+                   "\"method\":\"np.ndarray.__getitem__\",\"version\":"
+                   "\"2.2.6\"}";
+        case 2:
+            return "{\"description\":\"Minimum pooling over 2x2 blocks. "
+                   "Equivalent to reshaping into blocks and taking numpy.min "
+                   "along block dimensions.\",\"kwargs\":{\"func\":\"np.min\"},"
+                   "\"method\":\"skimage.measure.block_reduce\",\"version\":"
+                   "\"0.25.2\"}";
+        default:
+            return "{\"description\":\"Maximum pooling over 2x2 blocks. "
+                   "Equivalent to reshaping into blocks and taking numpy.max "
+                   "along block dimensions.\",\"kwargs\":{\"func\":\"np.max\"},"
+                   "\"method\":\"skimage.measure.block_reduce\",\"version\":"
+                   "\"0.25.2\"}";
+    }
+}
+
+} // namespace aqz

@@ -1,0 +1,220 @@
+// aqz_engine.hh -- host engine of the MI355X multiscale stage.
+//
+//   Stage          <- the hot path of zarr::MultiscaleArray::write_frame
+//                     (src/streaming/multiscale.array.cpp:57-74, 291-325):
+//                     level-0 tile split + Downsampler::add_frame + tile split
+//                     of every level, batched and device-resident.
+//   GpuDownsampler <- zarr::Downsampler (src/streaming/downsampler.hh:12-64),
+//                     same add_frame/take_frame contract.
+#pragma once
+
+#include "aqz_geometry.hh"
+#include "aqz_params.hh"
+
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace aqz {
+
+hipError_t launch_fused_pyramid(int dtype, int method, const FusedParams& p,
+                                hipStream_t stream);
+hipError_t launch_level(int dtype, int method, const LevelParams& p,
+                        hipStream_t stream);
+hipError_t launch_zero_frame_tiles(uint8_t* fb, uint64_t bpc,
+                                   uint32_t n_tiles, uint32_t tile_bytes,
+                                   hipStream_t stream);
+
+void hip_check(hipError_t e, const char* what);
+
+// Owning device allocation.
+struct DevBuf
+{
+    uint8_t* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    explicit DevBuf(size_t bytes) { alloc(bytes); }
+    ~DevBuf();
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept;
+    DevBuf& operator=(DevBuf&& o) noexcept;
+    void alloc(size_t bytes);
+};
+
+// Owning pinned host allocation.
+struct PinnedBuf
+{
+    uint8_t* p = nullptr;
+    size_t n = 0;
+    PinnedBuf() = default;
+    ~PinnedBuf();
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    PinnedBuf(PinnedBuf&& o) noexcept
+      : p(o.p)
+      , n(o.n)
+    {
+        o.p = nullptr;
+        o.n = 0;
+    }
+    void alloc(size_t bytes);
+};
+
+struct ArrayDesc
+{
+    std::vector<Dim> dims; // acquisition order
+    int32_t dtype = 0;
+    bool multiscale = true;
+    int32_t method = 0;
+    uint32_t max_levels = 0;
+    std::vector<size_t> storage_order;
+    int32_t device = 0;
+};
+
+struct StageOptions
+{
+    uint32_t layer_slots = 2;
+    uint32_t max_batch_frames = 64;
+    uint32_t force_levels = 0;
+    bool skip_level0_split = false;
+};
+
+struct LevelLayout
+{
+    uint64_t bytes_per_chunk;
+    uint32_t chunks_per_layer;
+    uint32_t layer_slots;
+    uint64_t frames_per_layer;
+    uint64_t frame_bytes;
+    uint32_t width, height;
+};
+
+// Per-level device state shared by Stage.
+struct StageLevel
+{
+    std::vector<Dim> dims;                 // storage order
+    std::unique_ptr<ArrayDimensions> ad;   // chunk lattice of this level
+    uint32_t W = 0, H = 0, planes = 0;
+    bool xy_shrinks = false;               // vs previous level
+    uint64_t bpc = 0, slot_bytes = 0;
+    uint32_t n_chunks = 0, n_slots = 0, F = 0;
+    uint32_t tw = 0, th = 0, ntx = 0, nty = 0;
+    bool needs_zero = false;               // any chunk padding
+    DevBuf ring, flags, tab_off, tab_grp;
+    std::vector<uint64_t> h_tab_off;
+    std::vector<uint32_t> h_tab_grp;
+    std::vector<int64_t> slot_layer;       // layer resident in each slot
+    uint64_t frames_written = 0;           // Array::frames_written_
+    uint32_t level_frame_count = 0;        // Downsampler::level_frame_count_
+    DevBuf scratch;                        // row-major frames of a batch
+    DevBuf partial[2];                     // carried z partial planes
+    int carried = -1;                      // partial[carried] holds one
+    DevBuf d_ops;
+    PinnedBuf h_ops;
+    hipEvent_t ops_ev = nullptr;
+};
+
+class Stage
+{
+  public:
+    Stage(const ArrayDesc& desc, const StageOptions& opt);
+    ~Stage();
+
+    uint32_t n_levels() const { return uint32_t(lv_.size()); }
+    const std::vector<Dim>& level_dims(uint32_t level) const;
+    LevelLayout layout(uint32_t level) const;
+    void set_stream(hipStream_t s);
+    void append(const void* frames, uint64_t n_frames, int mem);
+    void synchronize();
+    uint64_t frames_written(uint32_t level) const;
+    void copy_layer(uint32_t level, uint64_t layer, void* dst, size_t cap,
+                    uint8_t* has_data, size_t has_data_cap, int mem);
+    void device_layer(uint32_t level, uint64_t layer, void** chunks,
+                      uint32_t** flags);
+    void finalize();
+    void enable_timing(bool on);
+    void timing(double* total_ms, uint64_t* launches);
+    const char* dominant_kernel() const;
+
+  private:
+    struct Pending
+    {
+        bool has = false;
+        int kind = 0; // 0: level k-1 frame in batch, 1: carried partial
+        uint32_t index = 0;
+        bool scale = false;
+    };
+
+    void run_batch(const uint8_t* dsrc, uint32_t n);
+    void run_fused(const uint8_t* dsrc, uint32_t n);
+    void run_generic(const uint8_t* dsrc, uint32_t n);
+    void enter_layers(StageLevel& L, uint64_t first_fid, uint64_t n);
+    void enter_layer(StageLevel& L, uint64_t layer);
+    LevelGeom geom(StageLevel& L, uint64_t fid0, bool tiles,
+                   uint8_t* scratch) const;
+    void tile_addr(const StageLevel& L, uint64_t fid, uint64_t* off,
+                   uint32_t* flag_off) const;
+    const uint8_t* frame_ptr(uint32_t level, uint32_t index,
+                             const uint8_t* dsrc) const;
+
+    ArrayDesc desc_;
+    StageOptions opt_;
+    size_t bpp_;
+    std::vector<StageLevel> lv_;
+    bool fused_2d_ = true;
+    uint32_t n_fused_ = 0;
+    uint32_t rh_log2_ = 4;
+    uint64_t max_frames_ = 0; // 0 = unbounded
+    hipStream_t own_stream_ = nullptr;
+    hipStream_t stream_ = nullptr;
+    // host-source staging: pinned double buffer -> device double buffer
+    PinnedBuf h_stage_[2];
+    DevBuf d_stage_[2];
+    hipEvent_t stage_ev_[2] = { nullptr, nullptr };
+    int stage_idx_ = 0;
+    std::vector<Pending> pend_;
+    // kernel timing
+    bool timing_ = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pairs_;
+    size_t ev_used_ = 0;
+    double timed_ms_ = 0;
+    uint64_t timed_launches_ = 0;
+};
+
+class GpuDownsampler
+{
+  public:
+    explicit GpuDownsampler(const ArrayDesc& desc);
+    ~GpuDownsampler();
+
+    uint32_t n_levels() const { return uint32_t(levels_.size()); }
+    const std::vector<Dim>& level_dims(uint32_t level) const;
+    void add_frame(const void* frame, size_t nbytes, int mem);
+    bool take_frame(uint32_t level, void* dst, size_t cap, int mem,
+                    size_t* nbytes);
+    const char* method_name() const;
+    std::string metadata_json() const;
+
+  private:
+    struct Lv
+    {
+        uint32_t W, H, planes;
+        bool xy_shrinks;
+        DevBuf cur, pending, partial;
+        bool has_pending = false, has_partial = false;
+        uint32_t count = 0;
+    };
+    int32_t dtype_, method_;
+    size_t bpp_;
+    std::vector<std::vector<Dim>> levels_;
+    std::vector<Lv> lv_;
+    DevBuf input_;
+    DevBuf d_op_;
+    hipStream_t stream_ = nullptr;
+    int32_t device_;
+};
+
+} // namespace aqz

@@ -1,0 +1,82 @@
+// aqz_params.hh -- plain structs shared by the host engine and the HIP
+// kernels (passed by value as kernel arguments).
+#pragma once
+
+#include <cstdint>
+
+namespace aqz {
+
+// n / d for n < 2^31 as (umulhi(n, m) + n) >> s; d >= 1.
+struct FastDiv
+{
+    uint32_t d, m, s;
+};
+
+inline FastDiv
+make_fastdiv(uint32_t d)
+{
+    uint32_t s = 0;
+    while ((uint64_t(1) << s) < d)
+        ++s;
+    const uint64_t m =
+      ((uint64_t(1) << 32) * ((uint64_t(1) << s) - d)) / d + 1;
+    return FastDiv{ d, static_cast<uint32_t>(m), s };
+}
+
+// Geometry + output plumbing of one pyramid level for one launch.
+struct LevelGeom
+{
+    uint32_t W, H;          // level pixel dims
+    uint32_t tw, th, ntx;   // chunk tile dims, tiles along x
+    FastDiv dtw, dth;
+    uint64_t bpc;           // bytes per chunk
+    uint64_t slot_bytes;    // bytes per resident chunk layer
+    uint32_t n_chunks;      // chunks per layer
+    uint32_t n_slots;       // resident layers (ring)
+    uint32_t frames_per_layer;
+    uint32_t fid0_mod;      // (level frame id of batch frame 0) % frames_per_layer
+    uint32_t slot0;         // ring slot of the layer holding batch frame 0
+    uint8_t* base;          // chunk-layer ring (nullptr: no tile output)
+    uint32_t* flags;        // has_data, [n_slots * n_chunks]
+    const uint64_t* tab_off; // [frames_per_layer]: group*bpc + internal offset
+    const uint32_t* tab_grp; // [frames_per_layer]: tile_group_offset
+    uint8_t* scratch;       // row-major frames (nullptr: none), stride W*H
+};
+
+constexpr int kMaxFused = 6;
+
+struct FusedParams
+{
+    const uint8_t* src;      // level-0 frames, row-major
+    uint64_t src_stride;     // bytes between frames
+    uint32_t n_frames;
+    uint32_t n_fused;        // levels 1..n_fused computed here (<= kMaxFused)
+    uint32_t rh_log2;        // region height = 1 << rh_log2 (>= 4)
+    uint32_t nbx, nby;       // regions per frame along x / y
+    uint32_t vec_rows;       // 1: every row start is 16-B aligned
+    LevelGeom lv[kMaxFused + 1];
+};
+
+// One output frame (or partial plane) of the generic level kernel.  Pixel
+// value = R2(A, B) if b != nullptr else A, where A/B are the 2x2 reduction
+// of a/b when *_scale, else a/b itself (Downsampler::add_frame's
+// next_level_frame and average2_fun_, downsampler.cpp:341-389).
+struct LevelOp
+{
+    const uint8_t* a;       // earlier plane (or the only one)
+    const uint8_t* b;       // later plane, or nullptr
+    uint8_t* scratch_out;   // row-major destination or nullptr
+    uint64_t tile_off;      // byte offset of this frame in the layer ring
+    uint32_t flag_off;      // flag index of this frame's chunk group
+    uint32_t a_scale, b_scale, has_tile;
+};
+
+struct LevelParams
+{
+    uint32_t Wp, Hp;         // source (level k-1) dims
+    LevelGeom g;             // level k
+    const LevelOp* ops;
+    uint32_t n_ops;
+};
+
+} // namespace aqz

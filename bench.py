@@ -1,0 +1,257 @@
+#!/usr/bin/env python3
+"""Benchmark: input GB/s of the device-resident multiscale stage.
+
+One "step" = one launch batch of frames through the whole hot path of
+MultiscaleArray::write_frame: level-0 chunk-tile split + pyramid + tile split
+of every level into device-resident chunk layers (+ has_data flags).  Frames
+are synthetic, already resident in HBM (a >= 2 GiB ring, well past the 256 MiB
+Infinity Cache).  With --gpus N (torch.distributed.run, one rank per GPU)
+every rank runs its own independent stream (weak scaling, no collective on
+the data path; only the barrier and the max-over-ranks of the timed region).
+
+Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement".
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "acquire-zarr_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+SPACE, CHANNEL, TIME = 0, 1, 2
+U8, U16, F32 = 0, 1, 8
+MEAN = 1
+BPP = {U8: 1, U16: 2, F32: 4}
+
+CONFIGS = {
+    # BASELINE.json configs[1] -- the metric's config.  The reference level
+    # rule (downsampler.cpp:512-541) stops at 4 levels for 256-px chunks;
+    # force_levels keeps halving to the requested 5 (L4 = 128 px, one
+    # partial 256x256 chunk), pixel values unchanged.
+    "c2": dict(workload="uint16 2048x2048 frames, 5-level pyramid (2048..128 px), "
+                        "256x256 chunks (t-chunk 64), mean, level-0 split + pyramid + "
+                        "tile split of all levels, device-resident",
+               dims=[(TIME, 0, 64, 1), (SPACE, 2048, 256, 1), (SPACE, 2048, 256, 1)],
+               dtype=U16, method=MEAN, force_levels=5, batch=64, ring=256),
+    # same, reference level rule (4 levels)
+    "c2-ref4": dict(workload="uint16 2048x2048 frames, 4-level pyramid (reference rule "
+                             "at 256-px chunks), t-chunk 64, mean, device-resident",
+                    dims=[(TIME, 0, 64, 1), (SPACE, 2048, 256, 1), (SPACE, 2048, 256, 1)],
+                    dtype=U16, method=MEAN, force_levels=0, batch=64, ring=256),
+    "c3": dict(workload="uint8 4096x4096 frames, 6-level pyramid, 128x128 chunks, mean, "
+                        "device-resident",
+               dims=[(TIME, 0, 32, 1), (SPACE, 4096, 128, 1), (SPACE, 4096, 128, 1)],
+               dtype=U8, method=MEAN, force_levels=0, batch=32, ring=160),
+    "c5": dict(workload="float32 8192x8192 frames, 7-level pyramid, 128x128 chunks, mean, "
+                        "device-resident (one camera stream per GPU)",
+               dims=[(TIME, 0, 4, 1), (SPACE, 8192, 128, 1), (SPACE, 8192, 128, 1)],
+               dtype=F32, method=MEAN, force_levels=0, batch=4, ring=12),
+}
+
+
+def level_sizes(stage):
+    out = []
+    for l in range(stage.n_levels()):
+        d = stage.level_dims(l)
+        out.append((d[-2][1], d[-1][1]))
+    return out
+
+
+def fill_ring(torch, ring, dtype, seed):
+    g = torch.Generator(device=ring.device)
+    g.manual_seed(seed)
+    if dtype == U16:
+        ring.view(torch.int16).random_(-32768, 32767, generator=g)
+    elif dtype == U8:
+        ring.view(torch.uint8).random_(0, 256, generator=g)
+    else:
+        ring.view(torch.float32).uniform_(0.0, 65535.0, generator=g)
+
+
+def cpu_baseline(cfg, seconds):
+    """The reference's CPU path timed on this host's cores (rank 0 only):
+    the compiled reference (oracle/_ref) when present, else the C port.
+    Single thread (Downsampler::add_frame runs on the one frame-consumer
+    thread, zarr.stream.cpp:1683-1684)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_bindings as ob
+    dims = list(cfg["dims"])
+    dt, m = cfg["dtype"], cfg["method"]
+    h, w = dims[-2][1], dims[-1][1]
+    # The CPU reference cannot produce the forced 5th level at 256-px chunks;
+    # its 5-level pyramid for these frames is the 128-px-chunk configuration
+    # (identical pixels).
+    if cfg.get("force_levels"):
+        dims[-1] = (SPACE, w, 128, 1)
+        dims[-2] = (SPACE, h, 128, 1)
+    dims[0] = (TIME, 0, 1, 1)
+    frames = ob.synthetic_frames(dt, 4, h, w, 99)
+    kind = "reference" if ob.ref_available() else "port"
+    ds = ob.OracleDownsampler(dims, dt, m, 0, use_ref=(kind == "reference"))
+    L = ds.n_levels()
+    ldims = [ds.level_dims(l) for l in range(L)]
+    if kind == "reference":
+        R = ob.ref()
+        R.ref_split_create.argtypes = [C.POINTER(ob.Dim), C.c_int, C.c_int]
+        R.ref_split_create.restype = C.c_void_p
+        R.ref_split_write.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p]
+        R.ref_split_write.restype = C.c_size_t
+        R.ref_split_destroy.argtypes = [C.c_void_p]
+        keep = [ob.dims_array(d) for d in ldims]
+        sp = [R.ref_split_create(keep[l], len(ldims[l]), dt) for l in range(L)]
+
+        def split(l, img):
+            R.ref_split_write(sp[l], 0, img.ctypes.data)
+    else:
+        od = [ob.OracleDims(d, dt) for d in ldims]
+        lay = [od[l].new_layer() for l in range(L)]
+
+        def split(l, img):
+            od[l].write_frame_to_chunks(0, img, *lay[l])
+
+    outs = [np.empty((ld[-2][1], ld[-1][1]), dtype=ob.NP_DTYPES[dt]) for ld in ldims]
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        fr = frames[n % len(frames)]
+        split(0, fr)
+        ds.add_frame(fr)
+        for l in range(1, L):
+            img = ds.take_frame(l)
+            if img is not None:
+                split(l, img)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 3:
+            break
+    if kind == "reference":
+        for s in sp:
+            R.ref_split_destroy(s)
+    gbs = n * frames[0].nbytes / el / 1e9
+    return {"value": round(gbs, 4), "unit": "GB/s", "cores": 1, "kind": kind,
+            "sample": f"{n} frames of {h}x{w} {ob.DTYPE_NAMES[dt]} ({el:.1f} s): "
+                      f"Downsampler::add_frame+take_frame ({L} levels) + tile split of "
+                      f"every level, single thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pyramid-only", action="store_true",
+                    help="skip the level-0 tile split (downsample levels only)")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    import aqz
+    cfg = CONFIGS[args.config]
+    dt = cfg["dtype"]
+    B = cfg["batch"]
+    st = aqz.Stage(cfg["dims"], dt, cfg["method"], force_levels=cfg["force_levels"],
+                   max_batch_frames=B, layer_slots=2, device=dev.index,
+                   skip_level0_split=args.pyramid_only)
+    stream = torch.cuda.current_stream(dev)
+    st.set_stream(stream.cuda_stream)
+    sizes = level_sizes(st)
+    H, W = sizes[0]
+    bpp = BPP[dt]
+    fbytes = H * W * bpp
+    ring_frames = cfg["ring"]
+    ring = torch.empty(ring_frames * fbytes, dtype=torch.uint8, device=dev)
+    fill_ring(torch, ring, dt, 1234 + rank)
+    nb = ring_frames // B
+    base = ring.data_ptr()
+
+    def step(s):
+        st.append_ptr(base + (s % nb) * B * fbytes, B)
+
+    for s in range(args.warmup):
+        step(s)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    st.enable_kernel_timing(True)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(args.warmup + s)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kms, launches = st.kernel_timing()
+
+    in_bytes = fbytes
+    out_bytes = sum(h * w * bpp for (h, w) in sizes[1:])
+    l0_split = 0 if args.pyramid_only else fbytes
+    alg_per_launch = B * (in_bytes + l0_split + out_bytes)
+    avg_ms = kms / max(1, launches)
+    achieved = alg_per_launch / (avg_ms * 1e-3) / 1e9 if launches else 0.0
+    value = world * args.steps * B * fbytes / elapsed / 1e9
+
+    result = {
+        "metric": "input GB/s, device-resident multiscale downsample, uint16 frames @1/2/4/8 GPU",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": {U8: "u8", U16: "u16", F32: "f32"}[dt],
+        "data": "synthetic (device-resident random frames, per-rank seed)",
+        "config": {"workload": cfg["workload"] + (" [pyramid only: no level-0 split]"
+                                                  if args.pyramid_only else ""),
+                   "frames_per_step_per_gpu": B, "levels": len(sizes),
+                   "level_sizes": [f"{h}x{w}" for (h, w) in sizes],
+                   "parallelism": f"{world} independent per-GPU streams, no collective"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None,
+                     "kernel": st.dominant_kernel(),
+                     "kernel_avg_ms": round(avg_ms, 5),
+                     "alg_bytes_per_launch": alg_per_launch},
+        "input_rate_frac_of_peak": round(value / world / HBM_PEAK_GBS, 4),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    st.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

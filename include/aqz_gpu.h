@@ -1,0 +1,266 @@
+/*
+ * aqz_gpu.h -- C ABI of the MI355X-native multiscale-pyramid + chunk-tile
+ * stage for acquire-zarr.
+ *
+ * Plain C, plain pointers and sizes.  Every call returns a status code with
+ * the numeric values of ZarrStatusCode (reference include/zarr.types.h:13-31)
+ * and never lets a C++ exception or a HIP error cross the boundary (a HIP
+ * error maps to AQZ_STATUS_INTERNAL_ERROR and is sticky on the object, like
+ * ZarrStream_s::error_, reference src/streaming/zarr.stream.cpp:1442-1449).
+ *
+ * Objects are not thread-safe: like the reference Downsampler / Array they
+ * are driven from one consumer thread (reference zarr.stream.cpp:1683-1684).
+ *
+ * Which reference interface each entry point replaces is noted per function
+ * (paths relative to /root/reference).
+ */
+#ifndef AQZ_GPU_H
+#define AQZ_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (== ZarrStatusCode, include/zarr.types.h:13-31) ---- */
+typedef int32_t aqz_status;
+#define AQZ_STATUS_SUCCESS 0
+#define AQZ_STATUS_INVALID_ARGUMENT 1
+#define AQZ_STATUS_OVERFLOW 2
+#define AQZ_STATUS_INVALID_INDEX 3
+#define AQZ_STATUS_NOT_YET_IMPLEMENTED 4
+#define AQZ_STATUS_INTERNAL_ERROR 5
+#define AQZ_STATUS_OUT_OF_MEMORY 6
+#define AQZ_STATUS_INVALID_SETTINGS 9
+#define AQZ_STATUS_WRITE_OUT_OF_BOUNDS 12
+
+/* ---- enums: numeric values of ZarrDataType (zarr.types.h:49-62),
+ *      ZarrDimensionType (:81-88), ZarrDownsamplingMethod (:90-97) ------- */
+enum
+{
+    AQZ_DTYPE_UINT8 = 0,
+    AQZ_DTYPE_UINT16,
+    AQZ_DTYPE_UINT32,
+    AQZ_DTYPE_UINT64,
+    AQZ_DTYPE_INT8,
+    AQZ_DTYPE_INT16,
+    AQZ_DTYPE_INT32,
+    AQZ_DTYPE_INT64,
+    AQZ_DTYPE_FLOAT32,
+    AQZ_DTYPE_FLOAT64,
+    AQZ_DTYPE_COUNT
+};
+enum
+{
+    AQZ_DIM_SPACE = 0,
+    AQZ_DIM_CHANNEL,
+    AQZ_DIM_TIME,
+    AQZ_DIM_OTHER
+};
+enum
+{
+    AQZ_METHOD_DECIMATE = 0,
+    AQZ_METHOD_MEAN,
+    AQZ_METHOD_MIN,
+    AQZ_METHOD_MAX,
+    AQZ_METHOD_COUNT
+};
+
+/* where a frame pointer lives */
+enum
+{
+    AQZ_MEM_HOST = 0,   /* pageable or pinned host memory (H2D copy) */
+    AQZ_MEM_DEVICE = 1  /* already resident in this device's HBM */
+};
+
+/* The pixel-geometry subset of ZarrDimensionProperties
+ * (zarr.types.h:120-133): name/unit/scale do not affect the data path. */
+typedef struct
+{
+    int32_t type;               /* AQZ_DIM_* */
+    uint32_t array_size_px;     /* 0 = unbounded (append dimension only) */
+    uint32_t chunk_size_px;
+    uint32_t shard_size_chunks;
+} aqz_dimension;
+
+/* Mirrors the array part of ZarrArraySettings (zarr.types.h:157-169). */
+typedef struct
+{
+    const aqz_dimension* dimensions; /* acquisition order, slowest first */
+    size_t dimension_count;          /* >= 2; last two are Space (y, x) */
+    int32_t data_type;               /* AQZ_DTYPE_* */
+    int32_t multiscale;              /* bool */
+    int32_t downsampling_method;     /* AQZ_METHOD_* */
+    uint32_t max_levels;             /* 0 = no limit */
+    const size_t* storage_dimension_order; /* NULL = acquisition order */
+    int32_t device;                  /* HIP device ordinal */
+} aqz_array_desc;
+
+const char* aqz_version(void);
+const char* aqz_status_message(aqz_status status);
+/* Number of HIP devices visible (0 when no GPU). */
+aqz_status aqz_device_count(int32_t* count);
+
+/* ======================================================================
+ * Host index math -- ArrayDimensions (src/streaming/array.dimensions.hh:45)
+ * Pure host C++; usable without a GPU.
+ * ==================================================================== */
+typedef struct aqz_dims aqz_dims;
+
+/* ArrayDimensions::ArrayDimensions (array.dimensions.cpp:137-189), including
+ * the 2-D phantom-dimension prepend and storage_dimension_order. */
+aqz_status aqz_dims_create(const aqz_dimension* dims, size_t ndims,
+                           int32_t data_type, const size_t* storage_order,
+                           aqz_dims** out);
+void aqz_dims_destroy(aqz_dims* d);
+size_t aqz_dims_ndims(const aqz_dims* d);
+/* storage-order dimension i */
+aqz_status aqz_dims_get(const aqz_dims* d, size_t i, aqz_dimension* out);
+/* array.dimensions.cpp:264-282 */
+uint32_t aqz_dims_tile_group_offset(const aqz_dims* d, uint64_t frame_id);
+/* array.dimensions.cpp:284-314 */
+uint64_t aqz_dims_chunk_internal_offset(const aqz_dims* d, uint64_t frame_id);
+/* array.dimensions.cpp:232-262 */
+uint32_t aqz_dims_chunk_lattice_index(const aqz_dims* d, uint64_t frame_id,
+                                      uint32_t dim_index);
+/* array.dimensions.cpp:602-620 */
+uint64_t aqz_dims_transpose_frame_id(const aqz_dims* d, uint64_t frame_id);
+uint64_t aqz_dims_bytes_per_chunk(const aqz_dims* d);
+uint32_t aqz_dims_number_of_chunks_in_memory(const aqz_dims* d);
+uint64_t aqz_dims_frames_per_chunk_layer(const aqz_dims* d);
+/* array.dimensions.cpp:393-548 */
+uint32_t aqz_dims_shard_index_for_chunk(const aqz_dims* d, uint32_t chunk);
+uint32_t aqz_dims_shard_internal_index(const aqz_dims* d, uint32_t chunk);
+
+/* Level geometry of the pyramid: Downsampler::make_writer_configurations_
+ * (src/streaming/downsampler.cpp:494-597).  dims in storage order; writes the
+ * number of levels (including level 0) and, if out_dims != NULL, the dims of
+ * every level (n_levels * ndims entries, ndims after the 2-D prepend). */
+aqz_status aqz_pyramid_levels(const aqz_dimension* dims, size_t ndims,
+                              uint32_t max_levels, uint32_t* n_levels,
+                              aqz_dimension* out_dims, size_t out_cap);
+
+/* ======================================================================
+ * Downsampler -- drop-in for zarr::Downsampler (src/streaming/downsampler.hh:
+ * 12-64): same level geometry, same add/take contract, same cascade state
+ * machine (downsampler.cpp:306-414), pixels computed on the GPU.
+ * ==================================================================== */
+typedef struct aqz_downsampler aqz_downsampler;
+
+/* Downsampler::Downsampler(config, method) (downsampler.cpp:249-304).
+ * Invalid dtype/method -> AQZ_STATUS_INVALID_ARGUMENT (the reference throws). */
+aqz_status aqz_downsampler_create(const aqz_array_desc* desc,
+                                  aqz_downsampler** out);
+void aqz_downsampler_destroy(aqz_downsampler* ds);
+/* writer_configurations().size() */
+uint32_t aqz_downsampler_n_levels(const aqz_downsampler* ds);
+/* writer_configurations().at(level)->dimensions (storage order) */
+aqz_status aqz_downsampler_level_dims(const aqz_downsampler* ds,
+                                      uint32_t level, aqz_dimension* out,
+                                      size_t cap, size_t* ndims);
+/* Downsampler::add_frame (downsampler.cpp:306-401).  frame is level-0 pixels,
+ * nbytes >= width*height*bpp, mem = AQZ_MEM_HOST or AQZ_MEM_DEVICE. */
+aqz_status aqz_downsampler_add_frame(aqz_downsampler* ds, const void* frame,
+                                     size_t nbytes, int32_t mem);
+/* Downsampler::take_frame (downsampler.cpp:403-414): *found = 0 if no frame
+ * waits at `level`; otherwise copies it to dst (mem says where dst is). */
+aqz_status aqz_downsampler_take_frame(aqz_downsampler* ds, uint32_t level,
+                                      void* dst, size_t cap, int32_t mem,
+                                      size_t* nbytes, int32_t* found);
+/* Downsampler::downsampling_method (downsampler.cpp:422-438):
+ * "decimate" | "local_mean" | "local_min" | "local_max" */
+const char* aqz_downsampler_method_name(const aqz_downsampler* ds);
+/* Downsampler::get_metadata (downsampler.cpp:440-485) as JSON text. */
+aqz_status aqz_downsampler_metadata_json(const aqz_downsampler* ds, char* buf,
+                                         size_t cap, size_t* len);
+
+/* ======================================================================
+ * Stage -- the device-resident hot path of MultiscaleArray::write_frame
+ * (src/streaming/multiscale.array.cpp:57-74, 291-325): level-0 tile split
+ * (Array::write_frame_to_chunks_, array.cpp:507-622) + pyramid
+ * (Downsampler::add_frame) + tile split of every level, written straight
+ * into device-resident chunk layers with per-chunk has_data flags
+ * (Chunk::write_tile_rows, chunk.cpp:17-58).
+ *
+ * A "chunk layer" of a level = number_of_chunks_in_memory chunks of
+ * bytes_per_chunk bytes, chunk c at c*bytes_per_chunk (the reference's
+ * Array::chunks_ vector, array.cpp:575-583), covering frames_per_chunk_layer
+ * consecutive frames of that level.  The stage keeps `layer_slots` layers
+ * per level resident in HBM as a ring.
+ * ==================================================================== */
+typedef struct aqz_stage aqz_stage;
+
+typedef struct
+{
+    uint32_t layer_slots;      /* resident chunk layers per level (>=1; 0 = 2) */
+    uint32_t max_batch_frames; /* frames per internal launch (0 = 64) */
+    uint32_t force_levels;     /* 0 = reference level rule.  >0: extension
+                                  used only by bench.py for the BASELINE
+                                  "5-level @ 256-px chunks" config: keep
+                                  halving XY until this many levels exist. */
+    int32_t skip_level0_split; /* 1 = do not tile-split level 0 (pyramid
+                                  only); default 0 = full stage */
+} aqz_stage_options;
+
+typedef struct
+{
+    uint64_t bytes_per_chunk;
+    uint32_t chunks_per_layer;
+    uint32_t layer_slots;
+    uint64_t frames_per_layer;
+    uint64_t frame_bytes;      /* width*height*bpp of this level */
+    uint32_t width, height;
+} aqz_level_layout;
+
+aqz_status aqz_stage_create(const aqz_array_desc* desc,
+                            const aqz_stage_options* opt, aqz_stage** out);
+void aqz_stage_destroy(aqz_stage* st);
+uint32_t aqz_stage_n_levels(const aqz_stage* st);
+aqz_status aqz_stage_level_dims(const aqz_stage* st, uint32_t level,
+                                aqz_dimension* out, size_t cap, size_t* ndims);
+aqz_status aqz_stage_level_layout(const aqz_stage* st, uint32_t level,
+                                  aqz_level_layout* out);
+/* Run the stage on the HIP stream `stream` (a hipStream_t; NULL = the
+ * stage's own stream).  All later work is enqueued there. */
+aqz_status aqz_stage_set_stream(aqz_stage* st, void* stream);
+/* Append n_frames full level-0 frames (contiguous, frame after frame).
+ * Equivalent to n_frames calls of MultiscaleArray::write_frame.  Device
+ * sources are consumed asynchronously (do not modify them until the next
+ * aqz_stage_synchronize); host sources are copied before return. */
+aqz_status aqz_stage_append(aqz_stage* st, const void* frames,
+                            uint64_t n_frames, int32_t mem);
+aqz_status aqz_stage_synchronize(aqz_stage* st);
+/* frames written so far to `level` (Array::frames_written_) */
+uint64_t aqz_stage_frames_written(const aqz_stage* st, uint32_t level);
+/* Copy chunk layer `layer` of `level` (must still be resident) to dst
+ * (bytes_per_chunk*chunks_per_layer bytes) and its has_data flags (one byte
+ * per chunk).  Synchronizes. mem = where dst lives. */
+aqz_status aqz_stage_copy_layer(aqz_stage* st, uint32_t level, uint64_t layer,
+                                void* dst, size_t cap, uint8_t* has_data,
+                                size_t has_data_cap, int32_t mem);
+/* Device pointers of a resident layer (for device-side consumers). */
+aqz_status aqz_stage_device_layer(aqz_stage* st, uint32_t level,
+                                  uint64_t layer, void** chunks,
+                                  uint32_t** has_data);
+/* Zero the not-yet-written frames of every level's last partial layer so
+ * it can be flushed (the reference's lazily zeroed chunks, chunk.cpp:8-15).
+ * The unpaired trailing z plane is dropped, as in the reference. */
+aqz_status aqz_stage_finalize(aqz_stage* st);
+
+/* ---- instrumentation (bench) ---------------------------------------- */
+/* Time every launch of the dominant (fused pyramid) kernel with HIP events
+ * recorded on the stream it is launched on. */
+aqz_status aqz_stage_enable_kernel_timing(aqz_stage* st, int32_t enable);
+/* Sum of those kernels' durations (ms) and their count since enabling;
+ * synchronizes. */
+aqz_status aqz_stage_kernel_timing(aqz_stage* st, double* total_ms,
+                                   uint64_t* launches);
+/* Name of the dominant kernel symbol (for matching rocprof output). */
+const char* aqz_stage_dominant_kernel(const aqz_stage* st);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AQZ_GPU_H */

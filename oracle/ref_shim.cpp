@@ -244,4 +244,68 @@ ref_write_frame_to_chunks(void* h, int dtype, uint64_t fid, const void* frame,
     return written;
 }
 
+// ---- persistent-chunk tile split (CPU baseline timing) -------------------
+// Array::write_frame_to_chunks_ (array.cpp:537-619) restated over the
+// reference's own ArrayDimensions + zarr::Chunk objects that persist across
+// frames of a chunk layer, as in the reference Array (chunks_ vector).
+struct RefSplit
+{
+    std::unique_ptr<ArrayDimensions> dims;
+    std::vector<std::unique_ptr<zarr::Chunk>> chunks;
+    size_t bpp;
+};
+
+void*
+ref_split_create(const or_dim* dims, int ndims, int dtype)
+{
+    try {
+        auto* s = new RefSplit;
+        s->dims = std::make_unique<ArrayDimensions>(
+          to_dims(dims, ndims), static_cast<ZarrDataType>(dtype));
+        s->bpp = zarr::bytes_of_type(static_cast<ZarrDataType>(dtype));
+        s->chunks.resize(s->dims->number_of_chunks_in_memory());
+        return s;
+    } catch (...) {
+        return nullptr;
+    }
+}
+
+void
+ref_split_destroy(void* h)
+{
+    delete static_cast<RefSplit*>(h);
+}
+
+size_t
+ref_split_write(void* h, uint64_t fid, const void* frame)
+{
+    auto* s = static_cast<RefSplit*>(h);
+    auto* dims = s->dims.get();
+    const size_t bpp = s->bpp;
+    const uint32_t W = dims->width_dim().array_size_px;
+    const uint32_t tw = dims->width_dim().chunk_size_px;
+    const uint32_t H = dims->height_dim().array_size_px;
+    const uint32_t th = dims->height_dim().chunk_size_px;
+    const uint32_t ntx = (W + tw - 1) / tw, nty = (H + th - 1) / th;
+    const uint32_t group = dims->tile_group_offset(fid);
+    const uint64_t internal = dims->chunk_internal_offset(fid);
+    const auto* src = static_cast<const uint8_t*>(frame);
+    size_t written = 0;
+    for (uint32_t t = 0; t < ntx * nty; ++t) {
+        auto& chunk = s->chunks[t + group];
+        if (!chunk)
+            chunk = std::make_unique<zarr::Chunk>(dims->bytes_per_chunk(), bpp);
+        const uint32_t row0 = (t / ntx) * th;
+        const uint32_t n_rows = std::min(th, H - row0);
+        const uint32_t col0 = (t % ntx) * tw;
+        const uint32_t rw = std::min(col0 + tw, W) - col0;
+        chunk->write_tile_rows(internal,
+                               src + bpp * (static_cast<size_t>(row0) * W + col0),
+                               static_cast<size_t>(W) * bpp, rw * bpp, tw * bpp,
+                               n_rows);
+        written += static_cast<size_t>(rw) * bpp * n_rows;
+    }
+    return written;
+}
+
 } // extern "C"

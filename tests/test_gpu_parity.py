@@ -1,0 +1,274 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Every test here runs the MI355X kernels via include/aqz_gpu.h and compares
+with the oracle restatement (oracle/aqz_oracle.c), which the CPU suite pins
+to the compiled reference and to tests/golden/.  Bar: bit-exact for integer
+dtypes; floats bit-exact on every non-NaN value with NaN positions equal.
+"""
+import numpy as np
+import pytest
+
+from helpers import (assert_same_pixels, expected_stage_layers, oracle_cascade,
+                     with_specials)
+from oracle_bindings import (CHANNEL, DECIMATE, DTYPE_NAMES, F32, F64, I8,
+                             I16, I32, I64, MAX, MEAN, METHOD_NAMES, MIN, SPACE,
+                             TIME, U8, U16, U32, U64, NP_DTYPES, synthetic_frames)
+
+pytestmark = pytest.mark.gpu
+
+ALL_DTYPES = [U8, U16, U32, U64, I8, I16, I32, I64, F32, F64]
+ALL_METHODS = [DECIMATE, MEAN, MIN, MAX]
+SHAPES = [(2, 2), (3, 3), (5, 7), (11, 11), (37, 29), (64, 48), (130, 67)]
+
+
+def _frames(dtype, n, h, w, seed, specials=True):
+    fr = synthetic_frames(dtype, n, h, w, seed)
+    if specials:
+        fr = with_specials(fr, dtype, seed + 7)
+    return fr
+
+
+# ---------------------------------------------------------------------------
+# Downsampler mirror (zarr::Downsampler add_frame / take_frame)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype", ALL_DTYPES, ids=lambda d: DTYPE_NAMES[d])
+@pytest.mark.parametrize("method", ALL_METHODS, ids=lambda m: METHOD_NAMES[m])
+def test_downsampler_2d_all_dtypes_methods(gpu, dtype, method):
+    for si, (h, w) in enumerate(SHAPES):
+        dims = [(TIME, 0, 1, 1), (SPACE, h, 2, 1), (SPACE, w, 2, 1)]
+        frames = _frames(dtype, 2, h, w, 100 * si + dtype * 7 + method)
+        _, exp = oracle_cascade(dims, dtype, method, frames)
+        ds = gpu.Downsampler(dims, dtype, method)
+        for i, fr in enumerate(frames):
+            ds.add_frame(fr)
+            for l in range(1, ds.n_levels()):
+                got = ds.take_frame(l)
+                assert (got is None) == (l not in exp[i]), (h, w, i, l)
+                if got is not None:
+                    assert_same_pixels(got, exp[i][l], dtype, f"{h}x{w} f{i} L{l}")
+
+
+@pytest.mark.parametrize("dtype", [U8, U16, I32, F32, F64], ids=lambda d: DTYPE_NAMES[d])
+@pytest.mark.parametrize("method", ALL_METHODS, ids=lambda m: METHOD_NAMES[m])
+def test_downsampler_3d_odd_z_cascade(gpu, dtype, method):
+    # z Space with odd plane counts at several levels, two channels, two
+    # timepoints: exercises pairing, odd pass-through and the break.
+    for (z, cz, h, w, ch) in [(5, 1, 16, 16, 4), (15, 3, 48, 64, 16), (9, 2, 21, 13, 3)]:
+        dims = [(TIME, 0, 1, 1), (CHANNEL, 2, 1, 1), (SPACE, z, cz, 1),
+                (SPACE, h, ch, 1), (SPACE, w, ch, 1)]
+        frames = _frames(dtype, 2 * 2 * z, h, w, z * 31 + method)
+        _, exp = oracle_cascade(dims, dtype, method, frames)
+        ds = gpu.Downsampler(dims, dtype, method)
+        for i, fr in enumerate(frames):
+            ds.add_frame(fr)
+            for l in range(1, ds.n_levels()):
+                got = ds.take_frame(l)
+                assert (got is None) == (l not in exp[i]), (z, i, l)
+                if got is not None:
+                    assert_same_pixels(got, exp[i][l], dtype, f"z{z} f{i} L{l}")
+
+
+def test_downsampler_reference_known_answers(gpu):
+    """tests/unit-tests/downsampler.cpp known answers, on the GPU."""
+    # test_basic_downsampling (:25-74): 10x10 of 100 -> 5x5 of 100
+    ds = gpu.Downsampler([(TIME, 0, 5, 1), (SPACE, 10, 5, 1), (SPACE, 10, 5, 1)], U8, MEAN)
+    assert ds.n_levels() == 2
+    ds.add_frame(np.full((10, 10), 100, np.uint8))
+    out = ds.take_frame(1)
+    assert out.shape == (5, 5) and (out == 100).all()
+    assert ds.take_frame(1) is None
+    # test_3d_downsampling (:76-152): 100,200,300,400 -> L1 150, L2 250
+    dims = [(TIME, 0, 5, 1), (CHANNEL, 3, 1, 3), (SPACE, 20, 5, 1),
+            (SPACE, 20, 5, 1), (SPACE, 20, 5, 1)]
+    ds = gpu.Downsampler(dims, U16, MEAN)
+    ds.add_frame(np.full((20, 20), 100, np.uint16))
+    assert ds.take_frame(1) is None
+    ds.add_frame(np.full((20, 20), 200, np.uint16))
+    l1 = ds.take_frame(1)
+    assert l1.shape == (10, 10) and (l1 == 150).all()
+    assert ds.take_frame(2) is None
+    ds.add_frame(np.full((20, 20), 300, np.uint16))
+    assert ds.take_frame(1) is None and ds.take_frame(2) is None
+    ds.add_frame(np.full((20, 20), 400, np.uint16))
+    l2 = ds.take_frame(2)
+    assert l2.shape == (5, 5) and (l2 == 250).all()
+    # test_min_max_downsampling (:447-528): [100 200; 150 250] blocks
+    img = np.zeros((10, 10), np.uint8)
+    img[0::2, 0::2], img[0::2, 1::2], img[1::2, 0::2], img[1::2, 1::2] = 100, 200, 150, 250
+    for m, v in [(MEAN, 175), (MIN, 100), (MAX, 250)]:
+        ds = gpu.Downsampler([(TIME, 0, 5, 1), (SPACE, 10, 5, 1), (SPACE, 10, 5, 1)], U8, m)
+        ds.add_frame(img)
+        assert (ds.take_frame(1) == v).all()
+    # test_edge_cases (:411-445): 11x11 -> 6x6
+    ds = gpu.Downsampler([(TIME, 0, 5, 1), (SPACE, 11, 5, 1), (SPACE, 11, 5, 1)], U8, MEAN)
+    ds.add_frame(np.full((11, 11), 100, np.uint8))
+    assert ds.take_frame(1).shape == (6, 6)
+    # test_odd_z_multi_tc_no_bleed (downsampler-odd-z.cpp:19-86)
+    dims = [(TIME, 0, 1, 1), (CHANNEL, 2, 1, 2), (SPACE, 3, 1, 1),
+            (SPACE, 8, 4, 1), (SPACE, 8, 4, 1)]
+    ds = gpu.Downsampler(dims, U16, MEAN)
+    seen = []
+    for t in range(2):
+        for v in (100, 200):
+            for z in range(3):
+                ds.add_frame(np.full((8, 8), v, np.uint16))
+                o = ds.take_frame(1)
+                if o is not None:
+                    assert (o == o.flat[0]).all()
+                    seen.append(int(o.flat[0]))
+    assert seen == [100, 100, 200, 200, 100, 100, 200, 200]
+    assert ds.take_frame(1) is None
+    # check_downsample (downsampler-odd-z.cpp:88-132): Z=15 chunk 3
+    dims = [(TIME, 0, 1, 1), (SPACE, 15, 3, 1), (SPACE, 48, 16, 1), (SPACE, 64, 16, 1)]
+    ds = gpu.Downsampler(dims, U8, MEAN)
+    assert ds.level_dims(1)[1][1] == 8
+    for val in (63, 127, 255):
+        n = 0
+        for i in range(15):
+            ds.add_frame(np.full((48, 64), val, np.uint8))
+            if i % 2 == 1:
+                o = ds.take_frame(1)
+                assert o is not None and (o == val).all()
+                n += 1
+        assert n == 7
+        o = ds.take_frame(1)
+        assert o is not None and (o == val).all()
+
+
+def test_downsampler_metadata_and_errors(gpu):
+    import aqz
+    dims = [(TIME, 0, 5, 1), (SPACE, 10, 5, 1), (SPACE, 10, 5, 1)]
+    names = {DECIMATE: "decimate", MEAN: "local_mean", MIN: "local_min", MAX: "local_max"}
+    for m, n in names.items():
+        ds = gpu.Downsampler(dims, U16, m)
+        assert ds.method_name() == n
+        assert "skimage" in ds.metadata_json() or "np.ndarray" in ds.metadata_json()
+    with pytest.raises(aqz.AqzError) as e:
+        gpu.Downsampler(dims, U16, 4)
+    assert e.value.status == 1
+    with pytest.raises(aqz.AqzError):
+        gpu.Downsampler(dims, 10, MEAN)
+    ds = gpu.Downsampler(dims, U16, MEAN)
+    with pytest.raises(aqz.AqzError):
+        ds.add_frame(np.zeros((5, 5), np.uint16))  # too few bytes
+
+
+# ---------------------------------------------------------------------------
+# Stage: level-0 tile split + pyramid + tile split of every level
+# ---------------------------------------------------------------------------
+def _run_stage(gpu, dims, dtype, method, frames, max_levels=0, batch=0, chunks=None):
+    # keep every chunk layer of the run resident so all can be checked
+    f0 = dims[0][2]
+    for d in dims[1:-2]:
+        f0 *= d[1]
+    slots = -(-len(frames) // f0) + 2
+    st = gpu.Stage(dims, dtype, method, max_levels=max_levels,
+                   max_batch_frames=batch, layer_slots=slots)
+    if chunks is None:
+        st.append(frames)
+    else:
+        i = 0
+        for c in chunks:
+            st.append(np.ascontiguousarray(frames[i:i + c]))
+            i += c
+    st.finalize()
+    return st
+
+
+def _check_stage(gpu, dims, dtype, method, frames, **kw):
+    exp, fw, ldims = expected_stage_layers(dims, dtype, method, frames,
+                                           kw.get("max_levels", 0))
+    st = _run_stage(gpu, dims, dtype, method, frames, **kw)
+    assert st.n_levels() == len(ldims)
+    for l in range(st.n_levels()):
+        assert [tuple(x) for x in st.level_dims(l)] == [tuple(x) for x in ldims[l]]
+        assert st.frames_written(l) == fw[l], (l, st.frames_written(l), fw[l])
+    for (l, layer), (buf, flags) in sorted(exp.items()):
+        got, gflags = st.copy_layer(l, layer)
+        assert_same_pixels(got, buf, dtype, f"L{l} layer{layer}")
+        assert (gflags == flags).all(), f"has_data L{l} layer{layer}: {gflags} vs {flags}"
+    st.close()
+
+
+@pytest.mark.parametrize("dtype", ALL_DTYPES, ids=lambda d: DTYPE_NAMES[d])
+def test_stage_2d_tile_split_and_pyramid(gpu, dtype):
+    for method in ALL_METHODS:
+        for (h, w, cy, cx, ct) in [(64, 48, 16, 16, 2), (37, 29, 5, 7, 3),
+                                    (130, 67, 32, 8, 1), (11, 11, 4, 4, 5)]:
+            dims = [(TIME, 0, ct, 1), (SPACE, h, cy, 1), (SPACE, w, cx, 1)]
+            frames = _frames(dtype, 7, h, w, h * w + method)
+            _check_stage(gpu, dims, dtype, method, frames, batch=3)
+
+
+@pytest.mark.parametrize("method", ALL_METHODS, ids=lambda m: METHOD_NAMES[m])
+def test_stage_2d_channels_zero_frames_and_batches(gpu, method):
+    # intermediate non-space dim (c), ragged chunks, all-zero frames (has_data)
+    dims = [(TIME, 0, 2, 1), (CHANNEL, 3, 2, 1), (SPACE, 100, 32, 1), (SPACE, 90, 32, 1)]
+    frames = _frames(U16, 13, 100, 90, 5 + method)
+    frames[2] = 0
+    frames[7] = 0
+    _check_stage(gpu, dims, U16, method, frames, batch=4, chunks=[1, 5, 7])
+
+
+@pytest.mark.parametrize("method", ALL_METHODS, ids=lambda m: METHOD_NAMES[m])
+def test_stage_3d_generic_path(gpu, method):
+    # the C example config (examples/stream-raw-multiscale-to-filesystem.c):
+    # t 10/5, c 8/4, z 6/2 (Space), y 48/16, x 64/16
+    dims = [(TIME, 10, 5, 2), (CHANNEL, 8, 4, 2), (SPACE, 6, 2, 1),
+            (SPACE, 48, 16, 1), (SPACE, 64, 16, 2)]
+    frames = _frames(U16, 10 * 8 * 6, 48, 64, 77 + method, specials=False)
+    _check_stage(gpu, dims, U16, method, frames, batch=7)
+    # odd z with several z levels, batches that split pairs
+    dims = [(TIME, 0, 1, 1), (SPACE, 11, 2, 1), (SPACE, 40, 8, 1), (SPACE, 33, 8, 1)]
+    frames = _frames(F32, 33, 40, 33, 9 + method)
+    _check_stage(gpu, dims, F32, method, frames, batch=5, chunks=[3, 11, 19])
+
+
+def test_stage_deep_pyramid_tail_levels(gpu):
+    # more levels than the fused kernel cascades (tail levels, generic kernel)
+    dims = [(TIME, 0, 1, 1), (SPACE, 1000, 4, 1), (SPACE, 700, 4, 1)]
+    frames = _frames(U8, 3, 1000, 700, 3)
+    _check_stage(gpu, dims, U8, MEAN, frames, batch=2)
+
+
+def test_stage_max_levels_and_bounds(gpu):
+    import aqz
+    dims = [(TIME, 4, 2, 1), (SPACE, 64, 8, 1), (SPACE, 64, 8, 1)]
+    frames = _frames(U16, 4, 64, 64, 1)
+    _check_stage(gpu, dims, U16, MAX, frames, max_levels=2)
+    st = gpu.Stage(dims, U16, MAX)
+    st.append(frames)
+    with pytest.raises(aqz.AqzError) as e:
+        st.append(frames[:1])
+    assert e.value.status == 12
+
+
+@pytest.mark.parametrize("cfg", ["c1", "c2", "c3", "c5"])
+def test_stage_baseline_configs(gpu, cfg):
+    """BASELINE.json configs at full frame size (few frames), vs the oracle."""
+    if cfg == "c1":
+        dims, dt, m, n = [(TIME, 0, 4, 1), (SPACE, 512, 128, 1), (SPACE, 512, 128, 1)], U16, DECIMATE, 6
+    elif cfg == "c2":
+        dims, dt, m, n = [(TIME, 0, 4, 1), (SPACE, 2048, 128, 1), (SPACE, 2048, 128, 1)], U16, MEAN, 5
+    elif cfg == "c3":
+        dims, dt, m, n = [(TIME, 0, 2, 1), (SPACE, 4096, 128, 1), (SPACE, 4096, 128, 1)], U8, MEAN, 3
+    else:
+        dims, dt, m, n = [(TIME, 0, 1, 1), (SPACE, 8192, 128, 1), (SPACE, 8192, 128, 1)], F32, MEAN, 1
+    h, w = dims[-2][1], dims[-1][1]
+    frames = synthetic_frames(dt, n, h, w, 2024)
+    _check_stage(gpu, dims, dt, m, frames, batch=2)
+
+
+def test_stage_device_resident_input(gpu):
+    import torch
+    dims = [(TIME, 0, 2, 1), (SPACE, 256, 64, 1), (SPACE, 256, 64, 1)]
+    frames = _frames(U16, 6, 256, 256, 4, specials=False)
+    exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
+    t = torch.from_numpy(frames.view(np.int16)).cuda()
+    st = gpu.Stage(dims, U16, MEAN, layer_slots=8)
+    st.append(t)
+    st.finalize()
+    for (l, layer), (buf, flags) in exp.items():
+        got, gflags = st.copy_layer(l, layer)
+        assert_same_pixels(got, buf, U16, f"L{l}")
+        assert (gflags == flags).all()
