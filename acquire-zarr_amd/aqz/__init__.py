@@ -82,11 +82,30 @@ def build_library(force: bool = False) -> str:
 _lib = None
 
 
+def _preload_hip_runtime():
+    """One HIP runtime per process.  PyTorch ships its own libamdhip64
+    (soname libamdhip64.so.7) and finds it by path; if this library bound
+    /opt/rocm's copy first, a later torch CUDA init would start a second
+    runtime and fail.  Loading torch's copy first makes our NEEDED
+    libamdhip64.so.7 resolve to it, and torch later re-uses it (same file)."""
+    try:
+        import importlib.util
+        spec = importlib.util.find_spec("torch")
+        if spec is None or not spec.submodule_search_locations:
+            return
+        p = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+        if os.path.exists(p):
+            C.CDLL(p, mode=C.RTLD_GLOBAL)
+    except OSError:
+        pass
+
+
 def lib():
     global _lib
     if _lib is not None:
         return _lib
     build_library()
+    _preload_hip_runtime()
     L = C.CDLL(LIB_PATH)
     vp, sz, i32, u32, u64 = C.c_void_p, C.c_size_t, C.c_int32, C.c_uint32, C.c_uint64
     D = C.POINTER(Dimension)
