@@ -396,6 +396,7 @@ aqz_stage_create(const aqz_array_desc* desc, const aqz_stage_options* opt,
             o.max_batch_frames = opt->max_batch_frames;
             o.force_levels = opt->force_levels;
             o.skip_level0_split = opt->skip_level0_split != 0;
+            o.blocks_per_cu = opt->blocks_per_cu;
         }
         auto* s = new aqz_stage;
         try {

@@ -3,6 +3,7 @@
 #include "aqz_engine.hh"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace aqz {
@@ -117,6 +118,7 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         opt_.layer_slots = 2;
     if (opt_.max_batch_frames == 0)
         opt_.max_batch_frames = 64;
+    opt_blocks_per_cu_ = opt_.blocks_per_cu;
 
     auto base = std::make_unique<ArrayDimensions>(desc.dims, desc.dtype,
                                                   desc.storage_order);
@@ -199,7 +201,14 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
     for (size_t k = 1; k < lv_.size(); ++k)
         fused_2d_ &= !(lv_[k].planes < lv_[k - 1].planes) && lv_[k].xy_shrinks;
     n_fused_ = fused_2d_ ? std::min<uint32_t>(n_levels() - 1, kMaxFused) : 0;
-    rh_log2_ = std::max<uint32_t>(4, n_fused_);
+    // 64-row regions whenever LDS-cascaded levels (>= 3) exist: amortises
+    // the per-region barriers of the cascade over 32 KiB of input
+    rh_log2_ = n_fused_ >= 3 ? 6 : 4;
+    if (const char* ev = std::getenv("AQZ_REGION_ROWS_LOG2")) { // tuning knob
+        const uint32_t v = uint32_t(std::atoi(ev));
+        if (v >= std::max<uint32_t>(4, n_fused_) && (1u << v) <= uint32_t(kMaxRegionRows))
+            rh_log2_ = v;
+    }
 
     const Dim& d0 = lv_[0].dims[0];
     if (d0.array_size_px > 0) {
@@ -214,6 +223,9 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
     for (auto& L : lv_)
         hip_check(hipEventCreateWithFlags(&L.ops_ev, hipEventDisableTiming),
                   "hipEventCreate");
+    for (auto& ev : refs_ev_)
+        hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming),
+                  "hipEventCreate");
     hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
 
@@ -227,6 +239,9 @@ Stage::~Stage()
     for (auto& L : lv_)
         if (L.ops_ev)
             (void)hipEventDestroy(L.ops_ev);
+    for (auto& ev : refs_ev_)
+        if (ev)
+            (void)hipEventDestroy(ev);
     for (auto& pr : ev_pairs_) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -389,37 +404,100 @@ Stage::tile_addr(const StageLevel& L, uint64_t fid, uint64_t* off,
     *flag_off = uint32_t(slot * L.n_chunks + L.h_tab_grp[fid % L.F]);
 }
 
+const FrameRef*
+Stage::upload_refs(const std::vector<FrameRef>& refs)
+{
+    // pinned double buffer -> one device table (stream-ordered reuse)
+    const size_t cap = size_t(kMaxFused + 1) * opt_.max_batch_frames;
+    if (refs.size() > cap)
+        throw Error(5, "frame table overflow");
+    const int j = refs_idx_;
+    refs_idx_ ^= 1;
+    hip_check(hipEventSynchronize(refs_ev_[j]), "hipEventSynchronize");
+    h_refs_[j].alloc(cap * sizeof(FrameRef));
+    d_refs_.alloc(cap * sizeof(FrameRef));
+    std::memcpy(h_refs_[j].p, refs.data(), refs.size() * sizeof(FrameRef));
+    hip_check(hipMemcpyAsync(d_refs_.p, h_refs_[j].p,
+                             refs.size() * sizeof(FrameRef),
+                             hipMemcpyHostToDevice, stream_),
+              "hipMemcpyAsync");
+    hip_check(hipEventRecord(refs_ev_[j], stream_), "hipEventRecord");
+    return reinterpret_cast<const FrameRef*>(d_refs_.p);
+}
+
+FusedParams
+Stage::fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
+                    uint32_t rh_log2, bool tail)
+{
+    const StageLevel& L0 = lv_[0];
+    FusedParams p{};
+    p.src = dsrc;
+    p.src_stride = uint64_t(L0.W) * L0.H * bpp_;
+    p.n_frames = n;
+    p.n_fused = n_fused;
+    p.rh_log2 = rh_log2;
+    const uint32_t RW = uint32_t(512 / bpp_);
+    p.nbx = parts_along(L0.W, RW);
+    p.nby = parts_along(L0.H, 1u << rh_log2);
+    p.vec_rows = ((uint64_t(L0.W) * bpp_) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(dsrc) % 16 == 0)
+                   ? 1
+                   : 0;
+    p.fast_ok = (p.vec_rows && L0.th % (1u << rh_log2) == 0 &&
+                 L0.tw % uint32_t(16 / bpp_) == 0 && !(tail && n_fused <= 2))
+                  ? 1
+                  : 0;
+    p.blocks_per_cu = opt_blocks_per_cu_;
+    p.nbx_in = p.fast_ok ? L0.W / RW : 0;
+    p.nby_in = p.fast_ok ? L0.H >> rh_log2 : 0;
+    p.d_nreg_in = make_fastdiv(std::max<uint32_t>(1, p.nbx_in * p.nby_in));
+    p.d_nbx_in = make_fastdiv(std::max<uint32_t>(1, p.nbx_in));
+    p.tw = L0.tw;
+    p.th = L0.th;
+    p.dtw = make_fastdiv(L0.tw);
+    p.dth = make_fastdiv(L0.th);
+    p.bpc = L0.bpc;
+    std::vector<FrameRef> refs(size_t(n_fused + 1) * n);
+    for (uint32_t k = 0; k <= n_fused; ++k) {
+        StageLevel& L = lv_[k];
+        if (L.bpc != p.bpc || L.tw != p.tw || L.th != p.th)
+            throw Error(5, "chunk shape differs between levels");
+        p.W[k] = L.W;
+        p.H[k] = L.H;
+        p.ntx[k] = L.ntx;
+        for (uint32_t f = 0; f < n; ++f) {
+            FrameRef& r = refs[size_t(k) * n + f];
+            if (L.ring.p) {
+                uint64_t off;
+                uint32_t fo;
+                tile_addr(L, L.frames_written + f, &off, &fo);
+                r.tiles = L.ring.p + off;
+                r.flags = reinterpret_cast<uint32_t*>(L.flags.p) + fo;
+            } else {
+                r.tiles = nullptr;
+                r.flags = nullptr;
+            }
+        }
+    }
+    if (tail) {
+        StageLevel& L = lv_[n_fused];
+        L.scratch.alloc(size_t(opt_.max_batch_frames) * L.W * L.H * bpp_);
+        p.scratch = L.scratch.p;
+        p.scratch_level = n_fused;
+    }
+    p.refs = upload_refs(refs);
+    return p;
+}
+
 void
 Stage::run_fused(const uint8_t* dsrc, uint32_t n)
 {
     const uint32_t nl = n_levels();
     const bool tail = nl - 1 > n_fused_;
-    const uint64_t fb0 = uint64_t(lv_[0].W) * lv_[0].H * bpp_;
     for (uint32_t k = 0; k < nl; ++k)
         enter_layers(lv_[k], lv_[k].frames_written, n);
 
-    FusedParams p{};
-    p.src = dsrc;
-    p.src_stride = fb0;
-    p.n_frames = n;
-    p.n_fused = n_fused_;
-    p.rh_log2 = rh_log2_;
-    const uint32_t RW = uint32_t(512 / bpp_);
-    p.nbx = parts_along(lv_[0].W, RW);
-    p.nby = parts_along(lv_[0].H, 1u << rh_log2_);
-    p.vec_rows = ((fb0 / lv_[0].H) % 16 == 0 &&
-                  reinterpret_cast<uintptr_t>(dsrc) % 16 == 0)
-                   ? 1
-                   : 0;
-    for (uint32_t k = 0; k <= n_fused_; ++k) {
-        uint8_t* scr = nullptr;
-        if (tail && k == n_fused_) {
-            lv_[k].scratch.alloc(size_t(opt_.max_batch_frames) * lv_[k].W *
-                                 lv_[k].H * bpp_);
-            scr = lv_[k].scratch.p;
-        }
-        p.lv[k] = geom(lv_[k], lv_[k].frames_written, true, scr);
-    }
+    const FusedParams p = fused_params(dsrc, n, n_fused_, rh_log2_, tail);
 
     std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
     if (timing_) {
@@ -496,21 +574,8 @@ Stage::run_generic(const uint8_t* dsrc, uint32_t n)
     (void)nd;
     // level 0 tile split: the fused kernel with no pyramid levels
     if (!opt_.skip_level0_split) {
-        StageLevel& L0 = lv_[0];
-        enter_layers(L0, L0.frames_written, n);
-        FusedParams p{};
-        p.src = dsrc;
-        p.src_stride = uint64_t(L0.W) * L0.H * bpp_;
-        p.n_frames = n;
-        p.n_fused = 0;
-        p.rh_log2 = 4;
-        p.nbx = parts_along(L0.W, uint32_t(512 / bpp_));
-        p.nby = parts_along(L0.H, 16);
-        p.vec_rows = ((uint64_t(L0.W) * bpp_) % 16 == 0 &&
-                      reinterpret_cast<uintptr_t>(dsrc) % 16 == 0)
-                       ? 1
-                       : 0;
-        p.lv[0] = geom(L0, L0.frames_written, true, nullptr);
+        enter_layers(lv_[0], lv_[0].frames_written, n);
+        const FusedParams p = fused_params(dsrc, n, 0, 4, false);
         hip_check(launch_fused_pyramid(desc_.dtype, desc_.method, p, stream_),
                   "level-0 split launch");
     }

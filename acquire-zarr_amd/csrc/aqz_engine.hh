@@ -80,6 +80,7 @@ struct StageOptions
     uint32_t max_batch_frames = 64;
     uint32_t force_levels = 0;
     bool skip_level0_split = false;
+    uint32_t blocks_per_cu = 0;
 };
 
 struct LevelLayout
@@ -149,6 +150,9 @@ class Stage
     };
 
     void run_batch(const uint8_t* dsrc, uint32_t n);
+    const FrameRef* upload_refs(const std::vector<FrameRef>& refs);
+    FusedParams fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
+                             uint32_t rh_log2, bool tail);
     void run_fused(const uint8_t* dsrc, uint32_t n);
     void run_generic(const uint8_t* dsrc, uint32_t n);
     void enter_layers(StageLevel& L, uint64_t first_fid, uint64_t n);
@@ -175,6 +179,12 @@ class Stage
     DevBuf d_stage_[2];
     hipEvent_t stage_ev_[2] = { nullptr, nullptr };
     int stage_idx_ = 0;
+    // per-batch (level, frame) -> chunk-layer addresses for the fused kernel
+    DevBuf d_refs_;
+    PinnedBuf h_refs_[2];
+    hipEvent_t refs_ev_[2] = { nullptr, nullptr };
+    int refs_idx_ = 0;
+    uint32_t opt_blocks_per_cu_ = 0; // 0 = occupancy
     std::vector<Pending> pend_;
     // kernel timing
     bool timing_ = false;

@@ -1,25 +1,27 @@
 // aqz_kernels.hip -- CDNA4 (gfx950) kernels of the multiscale stage.
 //
-// fused_pyramid<T,M>: one workgroup (256 threads = 4 waves) per level-0
-//   region of RH x RW pixels (RW = 512 bytes of row, RH = 16..64 rows).
-//   Each thread streams two 16-byte row vectors per pass (coalesced: 32
-//   lanes cover one 512-B row segment), stores them straight into the
-//   level-0 chunk tiles (Array::write_frame_to_chunks_, array.cpp:507-622),
-//   reduces them 2x2 in registers to level 1 (scale_image, downsampler.cpp:
-//   139-206), stores level 1 into its tiles and into LDS; levels 2..F are then
-//   cascaded inside LDS with the per-level rounding and edge replication of
-//   the chained CPU path.  has_data (chunk.cpp:41-56) is a per-chunk flag set
-//   from a wave ballot.  HBM traffic = read input once + write every level once.
+// fused_pyramid<T,M> (interior regions) / fused_pyramid_edge<T,M> (edges):
+//   a region is RH rows x 512 bytes of row of one level-0 frame.  256 threads
+//   (4 waves); every thread streams two 16-byte row vectors per 16-row pass
+//   (32 lanes cover one 512-B row segment: fully coalesced), stores them
+//   straight into the level-0 chunk tiles (Array::write_frame_to_chunks_,
+//   array.cpp:507-622), reduces them 2x2 in registers to level 1
+//   (scale_image, downsampler.cpp:139-206), meets the row below through a
+//   cross-lane swap for level 2, and cascades levels 3..F inside LDS with the
+//   per-level rounding and edge replication of the chained CPU path.
+//   has_data (chunk.cpp:41-56) is one word per chunk, set after a wave
+//   ballot.  HBM traffic = read the input once + write every level once.
+//   The interior kernel is persistent (grid = resident workgroups) and
+//   prefetches the next pass's rows while it stores the current one.
 //
 // level_kernel<T,M>: the generic one-level step used for 2x2x2 pyramids
 //   (z pairs, average_two_frames, downsampler.cpp:208-246, 358-389), for
-//   levels beyond the fused depth, and for levels whose XY does not shrink.
+//   levels deeper than the fused cascade, and for levels whose XY does not
+//   shrink.
 #include <hip/hip_runtime.h>
 
 #include "aqz_params.hh"
 #include "aqz_reduce.hh"
-
-#include <cstring>
 
 namespace aqz {
 namespace {
@@ -92,6 +94,17 @@ store_vec(uint8_t* p, const T* v)
     *reinterpret_cast<V*>(p) = raw;
 }
 
+template<typename T, int N>
+__device__ __forceinline__ bool
+any_nonzero(const T* v)
+{
+    bool nz = false;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        nz |= nonzero_bits(v[i]);
+    return nz;
+}
+
 // Collects has_data per chunk for one thread; flushes with a wave-level
 // de-duplication (most lanes of a wave hit the same chunk).
 struct FlagAcc
@@ -135,45 +148,43 @@ struct FlagAcc
     }
 };
 
-// Base of frame `f` (batch-relative) of a level inside the layer ring.
-__device__ __forceinline__ void
-frame_base(const LevelGeom& g, uint32_t f, uint8_t*& fb, uint32_t*& fl)
+// chunk tiling of one level
+struct Tiles
 {
-    const uint32_t q = g.fid0_mod + f;
-    const uint32_t ld = q / g.frames_per_layer;
-    const uint32_t fm = q - ld * g.frames_per_layer;
-    const uint32_t slot = (g.slot0 + ld) % g.n_slots;
-    fb = g.base + uint64_t(slot) * g.slot_bytes + g.tab_off[fm];
-    fl = g.flags + uint64_t(slot) * g.n_chunks + g.tab_grp[fm];
+    uint32_t tw, th, ntx;
+    FastDiv dtw, dth;
+    uint64_t bpc;
+};
+
+__device__ __forceinline__ Tiles
+tiles_of(const FusedParams& p, int k)
+{
+    return Tiles{ p.tw, p.th, p.ntx[k], p.dtw, p.dth, p.bpc };
+}
+
+__device__ __forceinline__ Tiles
+tiles_of(const LevelGeom& g)
+{
+    return Tiles{ g.tw, g.th, g.ntx, g.dtw, g.dth, g.bpc };
 }
 
 // Store a run of N pixels of row Y starting at column X into the chunk tiles
-// (nvalid <= N pixels are inside the level).
+// of one frame (nvalid <= N pixels are inside the level).
 template<typename T, int N>
 __device__ __forceinline__ void
-put_tile(const LevelGeom& g,
-         uint8_t* fb,
-         uint32_t* fl,
-         uint32_t Y,
-         uint32_t X,
-         const T* v,
-         int nvalid,
-         FlagAcc& acc)
+put_tile(const Tiles& g, uint8_t* fb, uint32_t* fl, uint32_t Y, uint32_t X,
+         const T* v, int nvalid, FlagAcc& acc)
 {
     const uint32_t ty = fdiv(Y, g.dth);
     const uint32_t ry = Y - ty * g.th;
     const uint32_t tx = fdiv(X, g.dtw);
     const uint32_t rx = X - tx * g.tw;
     if (nvalid == N && rx + N <= g.tw && (g.tw % N) == 0) {
-        bool nz = false;
-#pragma unroll
-        for (int i = 0; i < N; ++i)
-            nz |= nonzero_bits(v[i]);
         const uint32_t chunk = ty * g.ntx + tx;
         store_vec<T, N>(fb + uint64_t(chunk) * g.bpc +
                           uint64_t(ry * g.tw + rx) * sizeof(T),
                         v);
-        acc.note(fl + chunk, nz);
+        acc.note(fl + chunk, any_nonzero<T, N>(v));
     } else {
         for (int i = 0; i < nvalid; ++i) {
             const uint32_t xi = X + i;
@@ -191,34 +202,27 @@ put_tile(const LevelGeom& g,
 // One cascaded level K (2..6) inside LDS: prev (pitch RW >> (K-1)) -> cur.
 template<typename T, int M, int K, uint32_t RW>
 __device__ __forceinline__ void
-deep_level(const FusedParams& p,
-           uint32_t f,
-           uint32_t y0,
-           uint32_t x0,
-           const T* prev,
-           T* cur)
+deep_level(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
+           const T* prev, T* cur)
 {
-    const LevelGeom& g = p.lv[K];
-    const LevelGeom& gp = p.lv[K - 1];
     constexpr uint32_t lw = RW >> K;
     constexpr uint32_t pw = RW >> (K - 1);
+    const uint32_t Wk = p.W[K], Hk = p.H[K];
     const uint32_t lh = (1u << p.rh_log2) >> K;
     const uint32_t yk0 = y0 >> K, xk0 = x0 >> K;
-    const uint32_t yp0 = y0 >> (K - 1), xp0 = x0 >> (K - 1);
     // last valid local row/col of the previous level inside this region
-    const uint32_t pxmax = gp.W - 1 - xp0;
-    const uint32_t pymax = gp.H - 1 - yp0;
-    uint8_t* fb = nullptr;
-    uint32_t* fl = nullptr;
-    if (g.base)
-        frame_base(g, f, fb, fl);
-    T* scr = g.scratch ? reinterpret_cast<T*>(g.scratch) + uint64_t(f) * g.W * g.H
-                       : nullptr;
+    const uint32_t pxmax = p.W[K - 1] - 1 - (x0 >> (K - 1));
+    const uint32_t pymax = p.H[K - 1] - 1 - (y0 >> (K - 1));
+    const FrameRef ref = p.refs[K * p.n_frames + f];
+    const Tiles tg = tiles_of(p, K);
+    T* scr = (p.scratch_level == uint32_t(K))
+               ? reinterpret_cast<T*>(p.scratch) + uint64_t(f) * Wk * Hk
+               : nullptr;
     FlagAcc acc;
     for (uint32_t idx = threadIdx.x; idx < lh * lw; idx += 256) {
         const uint32_t ly = idx / lw, lx = idx % lw;
         const uint32_t Y = yk0 + ly, X = xk0 + lx;
-        if (Y < g.H && X < g.W) {
+        if (Y < Hk && X < Wk) {
             const uint32_t py = 2 * ly, px = 2 * lx;
             const uint32_t px1 = min(px + 1, pxmax);
             const uint32_t py1 = min(py + 1, pymax);
@@ -227,52 +231,63 @@ deep_level(const FusedParams& p,
                                       prev[py1 * pw + px],
                                       prev[py1 * pw + px1]);
             cur[ly * lw + lx] = v;
-            if (fb)
-                put_tile<T, 1>(g, fb, fl, Y, X, &v, 1, acc);
+            if (ref.tiles)
+                put_tile<T, 1>(tg, ref.tiles, ref.flags, Y, X, &v, 1, acc);
             if (scr)
-                scr[uint64_t(Y) * g.W + X] = v;
+                scr[uint64_t(Y) * Wk + X] = v;
         }
     }
     acc.flush_wave();
 }
 
-template<typename T, int M>
-__global__ __launch_bounds__(256) void
-fused_pyramid(const FusedParams p)
+// Levels 3..n_fused of one region inside LDS; level 2 is in lds_b.
+template<typename T, int M, uint32_t RW>
+__device__ __forceinline__ void
+deep_levels(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
+            T* lds_a, T* lds_b)
 {
-    constexpr int VEC = 16 / sizeof(T); // pixels per 16-B row vector
-    constexpr int HV = VEC / 2;         // level-1 pixels per vector pair
-    constexpr uint32_t RW = 32 * VEC;   // region width (512 B of row)
-    // level-1 region (<= 32 rows) and level-2 region (<= 16 rows)
-    __shared__ __attribute__((aligned(16))) T lds_a[32 * (RW / 2)];
-    __shared__ __attribute__((aligned(16))) T lds_b[16 * (RW / 4)];
+    if (p.n_fused >= 3) {
+        __syncthreads();
+        deep_level<T, M, 3, RW>(p, f, y0, x0, lds_b, lds_a);
+    }
+    if (p.n_fused >= 4) {
+        __syncthreads();
+        deep_level<T, M, 4, RW>(p, f, y0, x0, lds_a, lds_b);
+    }
+    if (p.n_fused >= 5) {
+        __syncthreads();
+        deep_level<T, M, 5, RW>(p, f, y0, x0, lds_b, lds_a);
+    }
+    if (p.n_fused >= 6) {
+        __syncthreads();
+        deep_level<T, M, 6, RW>(p, f, y0, x0, lds_a, lds_b);
+    }
+}
 
+// Edge regions (or layouts the fast path does not cover): every access
+// bounds-checked, columns and rows clamped for the edge replication of
+// scale_image (downsampler.cpp:187-196); level 1 -> lds_a, level 2 -> lds_b.
+template<typename T, int M, uint32_t RW>
+__device__ void
+generic_region(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
+               T* lds_a, T* lds_b)
+{
+    constexpr int VEC = 16 / sizeof(T);
+    constexpr int HV = VEC / 2;
     const uint32_t tid = threadIdx.x;
-    const uint32_t rp = tid >> 5; // row pair within a 16-row pass
-    const uint32_t cv = tid & 31; // 16-B column vector
-    const uint32_t nreg = p.nbx * p.nby;
-    const uint32_t f = blockIdx.x / nreg;
-    const uint32_t r = blockIdx.x - f * nreg;
-    const uint32_t by = r / p.nbx;
-    const uint32_t bx = r - by * p.nbx;
-    const uint32_t y0 = by << p.rh_log2;
-    const uint32_t x0 = bx * RW;
+    const uint32_t rp = tid >> 5;
+    const uint32_t cv = tid & 31;
     const uint32_t npass = 1u << (p.rh_log2 - 4);
-
-    const LevelGeom& g0 = p.lv[0];
-    const LevelGeom& g1 = p.lv[1];
-    const uint32_t W0 = g0.W, H0 = g0.H;
+    const uint32_t W0 = p.W[0], H0 = p.H[0];
     const T* src = reinterpret_cast<const T*>(p.src + uint64_t(f) * p.src_stride);
 
-    uint8_t *fb0 = nullptr, *fb1 = nullptr;
-    uint32_t *fl0 = nullptr, *fl1 = nullptr;
-    if (g0.base)
-        frame_base(g0, f, fb0, fl0);
+    const FrameRef r0ref = p.refs[f];
     const bool l1 = p.n_fused >= 1;
-    if (l1 && g1.base)
-        frame_base(g1, f, fb1, fl1);
-    T* scr1 = (l1 && g1.scratch)
-                ? reinterpret_cast<T*>(g1.scratch) + uint64_t(f) * g1.W * g1.H
+    const FrameRef r1ref = l1 ? p.refs[p.n_frames + f] : FrameRef{ nullptr, nullptr };
+    const Tiles tg0 = tiles_of(p, 0);
+    const Tiles tg1 = tiles_of(p, 1);
+    T* scr1 = (l1 && p.scratch_level == 1)
+                ? reinterpret_cast<T*>(p.scratch) + uint64_t(f) * p.W[1] * p.H[1]
                 : nullptr;
     const bool keep_l1 = p.n_fused >= 2;
 
@@ -300,10 +315,11 @@ fused_pyramid(const FusedParams p)
                     r1[i] = src[uint64_t(ya) * W0 + xi];
                 }
             }
-            if (fb0) {
-                put_tile<T, VEC>(g0, fb0, fl0, y, x, r0, nv0, acc0);
+            if (r0ref.tiles) {
+                put_tile<T, VEC>(tg0, r0ref.tiles, r0ref.flags, y, x, r0, nv0, acc0);
                 if (y + 1 < H0)
-                    put_tile<T, VEC>(g0, fb0, fl0, y + 1, x, r1, nv0, acc0);
+                    put_tile<T, VEC>(tg0, r0ref.tiles, r0ref.flags, y + 1, x, r1,
+                                     nv0, acc0);
             }
             if (l1) {
                 T o[HV];
@@ -312,12 +328,12 @@ fused_pyramid(const FusedParams p)
                     o[i] = reduce4<M, T>(
                       r0[2 * i], r0[2 * i + 1], r1[2 * i], r1[2 * i + 1]);
                 const uint32_t Y = y >> 1, X = x >> 1;
-                const int nv1 = int(min(uint32_t(HV), g1.W - X));
-                if (fb1)
-                    put_tile<T, HV>(g1, fb1, fl1, Y, X, o, nv1, acc1);
+                const int nv1 = int(min(uint32_t(HV), p.W[1] - X));
+                if (r1ref.tiles)
+                    put_tile<T, HV>(tg1, r1ref.tiles, r1ref.flags, Y, X, o, nv1, acc1);
                 if (scr1)
                     for (int i = 0; i < nv1; ++i)
-                        scr1[uint64_t(Y) * g1.W + X + i] = o[i];
+                        scr1[uint64_t(Y) * p.W[1] + X + i] = o[i];
                 if (keep_l1) {
 #pragma unroll
                     for (int i = 0; i < HV; ++i)
@@ -328,28 +344,294 @@ fused_pyramid(const FusedParams p)
     }
     acc0.flush_wave();
     acc1.flush_wave();
-
-    // cascaded levels 2..n_fused inside LDS (ping-pong A -> B -> A ...)
     if (p.n_fused >= 2) {
         __syncthreads();
         deep_level<T, M, 2, RW>(p, f, y0, x0, lds_a, lds_b);
     }
-    if (p.n_fused >= 3) {
-        __syncthreads();
-        deep_level<T, M, 3, RW>(p, f, y0, x0, lds_b, lds_a);
+}
+
+// ---------------------------------------------------------------------------
+// Fast path for interior regions whose rows lie in one chunk-tile row at
+// every fused level and whose 16-B vectors never straddle a tile: every
+// thread's tile addresses are set up once per region.
+// ---------------------------------------------------------------------------
+struct FastTile
+{
+    uint8_t* p;      // (region row 0 at this level, this thread's column)
+    uint32_t* flag;  // has_data word of that chunk
+    bool nz;
+};
+
+template<typename T>
+__device__ __forceinline__ FastTile
+fast_tile(const FusedParams& p, int k, uint32_t f, uint32_t Y0, uint32_t X)
+{
+    FastTile t{ nullptr, nullptr, false };
+    const FrameRef ref = p.refs[k * p.n_frames + f];
+    if (!ref.tiles)
+        return t;
+    const uint32_t ty = fdiv(Y0, p.dth);
+    const uint32_t tx = fdiv(X, p.dtw);
+    const uint32_t ry = Y0 - ty * p.th;
+    const uint32_t rx = X - tx * p.tw;
+    const uint32_t chunk = ty * p.ntx[k] + tx;
+    t.p = ref.tiles + uint64_t(chunk) * p.bpc + uint64_t(ry * p.tw + rx) * sizeof(T);
+    t.flag = ref.flags + chunk;
+    return t;
+}
+
+__device__ __forceinline__ void
+flush_tile_flag(FastTile& t)
+{
+    FlagAcc a;
+    a.ptr = t.flag;
+    a.nz = t.nz;
+    a.flush_wave();
+    t.nz = false;
+}
+
+template<typename T>
+__device__ __forceinline__ T
+shfl_xor_t(T v, int mask)
+{
+    if constexpr (sizeof(T) == 8) {
+        uint64_t u;
+        __builtin_memcpy(&u, &v, 8);
+        const uint32_t lo = __shfl_xor(uint32_t(u), mask);
+        const uint32_t hi = __shfl_xor(uint32_t(u >> 32), mask);
+        u = (uint64_t(hi) << 32) | lo;
+        T r;
+        __builtin_memcpy(&r, &u, 8);
+        return r;
+    } else {
+        uint32_t u = 0;
+        __builtin_memcpy(&u, &v, sizeof(T));
+        u = __shfl_xor(u, mask);
+        T r;
+        __builtin_memcpy(&r, &u, sizeof(T));
+        return r;
     }
-    if (p.n_fused >= 4) {
-        __syncthreads();
-        deep_level<T, M, 4, RW>(p, f, y0, x0, lds_a, lds_b);
+}
+
+template<typename T>
+__device__ __forceinline__ T
+shfl_down_t(T v, int d)
+{
+    if constexpr (sizeof(T) == 8) {
+        uint64_t u;
+        __builtin_memcpy(&u, &v, 8);
+        const uint32_t lo = __shfl_down(uint32_t(u), d);
+        const uint32_t hi = __shfl_down(uint32_t(u >> 32), d);
+        u = (uint64_t(hi) << 32) | lo;
+        T r;
+        __builtin_memcpy(&r, &u, 8);
+        return r;
+    } else {
+        uint32_t u = 0;
+        __builtin_memcpy(&u, &v, sizeof(T));
+        u = __shfl_down(u, d);
+        T r;
+        __builtin_memcpy(&r, &u, sizeof(T));
+        return r;
     }
-    if (p.n_fused >= 5) {
-        __syncthreads();
-        deep_level<T, M, 5, RW>(p, f, y0, x0, lds_b, lds_a);
+}
+
+// The two 16-B row vectors of this thread for one pass of an interior region.
+__device__ __forceinline__ void
+load_pass(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
+          uint32_t pass, uint32_t bpp, uint4& a, uint4& b)
+{
+    const uint32_t y = y0 + pass * 16 + 2 * (threadIdx.x >> 5);
+    const uint64_t row = uint64_t(p.W[0]) * bpp;
+    const uint8_t* s = p.src + uint64_t(f) * p.src_stride + uint64_t(y) * row +
+                       uint64_t(x0 + (threadIdx.x & 31) * (16 / bpp)) * bpp;
+    a = *reinterpret_cast<const uint4*>(s);
+    b = *reinterpret_cast<const uint4*>(s + row);
+}
+
+// One 16-row pass of an interior region: level-0 tile rows, level 1 (2x2 in
+// registers), level 2 (rows of lanes l and l^32 meet by a cross-lane swap).
+template<typename T, int M, uint32_t RW>
+__device__ __forceinline__ void
+fast_pass(const FusedParams& p, uint32_t pass, const uint4& ra, const uint4& rb,
+          FastTile& t0, FastTile& t1, FastTile& t2, T* lds_l2)
+{
+    constexpr int VEC = 16 / sizeof(T);
+    constexpr int HV = VEC / 2;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t rp = threadIdx.x >> 5;
+    const uint32_t cv = threadIdx.x & 31;
+    const uint32_t trow = p.tw * uint32_t(sizeof(T)); // bytes per tile row
+    if (t0.p) {
+        const uint32_t dy = pass * 16 + 2 * rp;
+        *reinterpret_cast<uint4*>(t0.p + uint64_t(dy) * trow) = ra;
+        *reinterpret_cast<uint4*>(t0.p + uint64_t(dy + 1) * trow) = rb;
+        t0.nz |= ((ra.x | ra.y | ra.z | ra.w) | (rb.x | rb.y | rb.z | rb.w)) != 0u;
     }
-    if (p.n_fused >= 6) {
-        __syncthreads();
-        deep_level<T, M, 6, RW>(p, f, y0, x0, lds_a, lds_b);
+    if (p.n_fused < 1)
+        return;
+    T r0[VEC], r1[VEC];
+    __builtin_memcpy(r0, &ra, 16);
+    __builtin_memcpy(r1, &rb, 16);
+    T o[HV];
+#pragma unroll
+    for (int i = 0; i < HV; ++i)
+        o[i] = reduce4<M, T>(r0[2 * i], r0[2 * i + 1], r1[2 * i], r1[2 * i + 1]);
+    if (t1.p) {
+        store_vec<T, HV>(t1.p + uint64_t(pass * 8 + rp) * trow, o);
+        t1.nz |= any_nonzero<T, HV>(o);
     }
+    if (p.n_fused < 2)
+        return;
+    const uint32_t row2 = pass * 4 + (rp >> 1);
+    if constexpr (HV >= 2) {
+        constexpr int QV = HV / 2;
+        // level-1 row below lives in lane ^ 32: move HV*sizeof(T) = 8 bytes
+        uint2 mine, below;
+        __builtin_memcpy(&mine, o, 8);
+        below.x = __shfl_xor(mine.x, 32);
+        below.y = __shfl_xor(mine.y, 32);
+        T b[HV];
+        __builtin_memcpy(b, &below, 8);
+        if (lane < 32) {
+            T q[QV];
+#pragma unroll
+            for (int j = 0; j < QV; ++j)
+                q[j] = reduce4<M, T>(o[2 * j], o[2 * j + 1], b[2 * j], b[2 * j + 1]);
+            if (t2.p) {
+                store_vec<T, QV>(t2.p + uint64_t(row2) * trow, q);
+                t2.nz |= any_nonzero<T, QV>(q);
+            }
+            if (lds_l2) {
+#pragma unroll
+                for (int j = 0; j < QV; ++j)
+                    lds_l2[row2 * (RW / 4) + cv * QV + j] = q[j];
+            }
+        }
+    } else {
+        // one level-1 pixel per lane: the 2x2 block spans lanes l, l+1,
+        // l^32, (l^32)+1
+        const T b = shfl_xor_t(o[0], 32);
+        const T rt = shfl_down_t(o[0], 1);
+        const T brt = shfl_down_t(b, 1);
+        if (lane < 32 && (cv & 1) == 0) {
+            const T q = reduce4<M, T>(o[0], rt, b, brt);
+            if (t2.p) {
+                store_vec<T, 1>(t2.p + uint64_t(row2) * trow, &q);
+                t2.nz |= nonzero_bits(q);
+            }
+            if (lds_l2)
+                lds_l2[row2 * (RW / 4) + (cv >> 1)] = q;
+        }
+    }
+}
+
+// Interior regions: persistent grid-stride loop over (region, pass) units
+// with the next unit's rows prefetched while the current one is stored and
+// reduced.  Region r of [0, n_frames * nby_in * nbx_in).
+template<typename T, int M>
+__global__ __launch_bounds__(256) void
+fused_pyramid(const FusedParams p)
+{
+    constexpr int VEC = 16 / sizeof(T); // pixels per 16-B row vector
+    constexpr uint32_t RW = 32 * VEC;   // region width (512 B of row)
+    __shared__ __attribute__((aligned(16))) T lds_a[(kMaxRegionRows / 2) * (RW / 2)];
+    __shared__ __attribute__((aligned(16))) T lds_b[(kMaxRegionRows / 4) * (RW / 4)];
+
+    const uint32_t total = p.n_frames * p.nbx_in * p.nby_in;
+    const uint32_t npass = 1u << (p.rh_log2 - 4);
+    const uint32_t cv = threadIdx.x & 31;
+
+    auto decode = [&](uint32_t r, uint32_t& f, uint32_t& y0, uint32_t& x0) {
+        f = fdiv(r, p.d_nreg_in);
+        const uint32_t q = r - f * (p.nbx_in * p.nby_in);
+        const uint32_t by = fdiv(q, p.d_nbx_in);
+        y0 = by << p.rh_log2;
+        x0 = (q - by * p.nbx_in) * RW;
+    };
+
+    uint32_t r = blockIdx.x;
+    if (r >= total)
+        return;
+    uint32_t pass = 0, f, y0, x0;
+    decode(r, f, y0, x0);
+    uint4 ca, cb;
+    load_pass(p, f, y0, x0, 0, sizeof(T), ca, cb);
+    FastTile t0{}, t1{}, t2{};
+    T* lds_l2 = p.n_fused >= 3 ? lds_b : nullptr;
+
+    while (true) {
+        if (pass == 0) {
+            t0 = fast_tile<T>(p, 0, f, y0, x0 + cv * VEC);
+            if (p.n_fused >= 1)
+                t1 = fast_tile<T>(p, 1, f, y0 >> 1, (x0 >> 1) + cv * (VEC / 2));
+            if (p.n_fused >= 2)
+                t2 = fast_tile<T>(p, 2, f, y0 >> 2,
+                                  (x0 >> 2) + (VEC >= 4 ? cv * (VEC / 4) : (cv >> 1)));
+        }
+        // prefetch the next pass (of this region or of the next one)
+        uint32_t rn = r, pn = pass + 1, fn = f, yn = y0, xn = x0;
+        if (pn == npass) {
+            rn = r + gridDim.x;
+            pn = 0;
+            if (rn < total)
+                decode(rn, fn, yn, xn);
+        }
+        const bool more = rn < total;
+        uint4 na{}, nb{};
+        if (more)
+            load_pass(p, fn, yn, xn, pn, sizeof(T), na, nb);
+
+        fast_pass<T, M, RW>(p, pass, ca, cb, t0, t1, t2, lds_l2);
+
+        if (pass == npass - 1) {
+            flush_tile_flag(t0);
+            flush_tile_flag(t1);
+            flush_tile_flag(t2);
+            if (p.n_fused >= 3) {
+                deep_levels<T, M, RW>(p, f, y0, x0, lds_a, lds_b);
+                __syncthreads();
+            }
+        }
+        if (!more)
+            break;
+        ca = na;
+        cb = nb;
+        r = rn;
+        pass = pn;
+        f = fn;
+        y0 = yn;
+        x0 = xn;
+    }
+}
+
+// Edge regions (right column strip, bottom row strip; or every region when
+// the fast path does not apply): one workgroup per region, fully checked.
+template<typename T, int M>
+__global__ __launch_bounds__(256) void
+fused_pyramid_edge(const FusedParams p)
+{
+    constexpr int VEC = 16 / sizeof(T);
+    constexpr uint32_t RW = 32 * VEC;
+    __shared__ __attribute__((aligned(16))) T lds_a[(kMaxRegionRows / 2) * (RW / 2)];
+    __shared__ __attribute__((aligned(16))) T lds_b[(kMaxRegionRows / 4) * (RW / 4)];
+    const uint32_t right = p.nby_in * (p.nbx - p.nbx_in);
+    const uint32_t per_frame = p.nbx * p.nby - p.nbx_in * p.nby_in;
+    const uint32_t f = blockIdx.x / per_frame;
+    const uint32_t e = blockIdx.x - f * per_frame;
+    uint32_t by, bx;
+    if (e < right) {
+        const uint32_t w = p.nbx - p.nbx_in;
+        by = e / w;
+        bx = p.nbx_in + (e - by * w);
+    } else {
+        const uint32_t e2 = e - right;
+        by = p.nby_in + e2 / p.nbx;
+        bx = e2 - (by - p.nby_in) * p.nbx;
+    }
+    const uint32_t y0 = by << p.rh_log2, x0 = bx * RW;
+    generic_region<T, M, RW>(p, f, y0, x0, lds_a, lds_b);
+    deep_levels<T, M, RW>(p, f, y0, x0, lds_a, lds_b);
 }
 
 // ---------------------------------------------------------------------------
@@ -393,8 +675,8 @@ level_kernel(const LevelParams p)
         if (op.scratch_out)
             reinterpret_cast<T*>(op.scratch_out)[idx] = v;
         if (op.has_tile)
-            put_tile<T, 1>(g, g.base + op.tile_off, g.flags + op.flag_off, Y,
-                           X, &v, 1, acc);
+            put_tile<T, 1>(tiles_of(g), g.base + op.tile_off,
+                           g.flags + op.flag_off, Y, X, &v, 1, acc);
     }
     acc.flush_wave();
 }
@@ -418,7 +700,6 @@ zero_frame_tiles(uint8_t* fb, uint64_t bpc, uint32_t n_tiles,
 // ---------------------------------------------------------------------------
 // Host launchers: dtype x method dispatch.
 // ---------------------------------------------------------------------------
-
 #define AQZ_DISPATCH(DT, M, CALL)                                              \
     switch (DT) {                                                              \
         case 0: AQZ_DISPATCH_M(uint8_t, M, CALL); break;                       \
@@ -447,15 +728,44 @@ hipError_t
 launch_fused_pyramid(int dtype, int method, const FusedParams& p,
                      hipStream_t stream)
 {
-    const uint64_t blocks = uint64_t(p.n_frames) * p.nbx * p.nby;
-    if (blocks == 0)
-        return hipSuccess;
-    if (blocks > 0x7fffffffull || p.n_fused > uint32_t(kMaxFused) ||
-        p.rh_log2 < 4 || p.rh_log2 > 6)
+    if (p.n_fused > uint32_t(kMaxFused) || p.rh_log2 < 4 ||
+        (1u << p.rh_log2) > uint32_t(kMaxRegionRows) || p.nbx_in > p.nbx ||
+        p.nby_in > p.nby || (1u << p.rh_log2) < (1u << p.n_fused))
         return hipErrorInvalidValue;
+    const uint64_t interior = uint64_t(p.n_frames) * p.nbx_in * p.nby_in;
+    const uint64_t edge =
+      uint64_t(p.n_frames) * (uint64_t(p.nbx) * p.nby - uint64_t(p.nbx_in) * p.nby_in);
+    if (interior > 0x7fffffffull || edge > 0x7fffffffull)
+        return hipErrorInvalidValue;
+    // persistent grid: as many workgroups as are resident
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
+                                  dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    static int occ[10][4] = {};
 #define CALL(T, MM)                                                            \
-    hipLaunchKernelGGL((fused_pyramid<T, MM>), dim3(uint32_t(blocks)),         \
-                       dim3(256), 0, stream, p)
+    do {                                                                       \
+        if (interior) {                                                        \
+            int& o = occ[dtype][MM];                                           \
+            if (o == 0 &&                                                      \
+                (hipOccupancyMaxActiveBlocksPerMultiprocessor(                 \
+                   &o, fused_pyramid<T, MM>, 256, 0) != hipSuccess ||          \
+                 o <= 0))                                                      \
+                o = 4;                                                         \
+            const uint64_t cap =                                               \
+              uint64_t(cus) * (p.blocks_per_cu ? p.blocks_per_cu : uint32_t(o)); \
+            const uint32_t blocks = uint32_t(interior < cap ? interior : cap); \
+            hipLaunchKernelGGL((fused_pyramid<T, MM>), dim3(blocks), dim3(256),\
+                               0, stream, p);                                  \
+        }                                                                      \
+        if (edge)                                                              \
+            hipLaunchKernelGGL((fused_pyramid_edge<T, MM>),                    \
+                               dim3(uint32_t(edge)), dim3(256), 0, stream, p); \
+    } while (0)
     AQZ_DISPATCH(dtype, method, CALL)
 #undef CALL
     return hipGetLastError();
@@ -488,12 +798,6 @@ launch_zero_frame_tiles(uint8_t* fb, uint64_t bpc, uint32_t n_tiles,
     hipLaunchKernelGGL(zero_frame_tiles, dim3(gx, n_tiles), dim3(256), 0,
                        stream, fb, bpc, n_tiles, tile_bytes);
     return hipGetLastError();
-}
-
-const char*
-fused_kernel_symbol_hint()
-{
-    return "fused_pyramid";
 }
 
 } // namespace aqz

@@ -44,17 +44,40 @@ struct LevelGeom
 };
 
 constexpr int kMaxFused = 6;
+constexpr int kMaxRegionRows = 128; // LDS is sized for this region height
 
+// Where frame f of a level lands: the base of its tiles inside the resident
+// chunk layer (= slot base + tile_group_offset*bytes_per_chunk +
+// chunk_internal_offset, array.dimensions.cpp:264-314) and its has_data words.
+struct FrameRef
+{
+    uint8_t* tiles;  // nullptr: this level is not tile-split
+    uint32_t* flags;
+};
+
+// The fused pyramid launch.  Chunk sizes are the same at every level
+// (downsample_dimension keeps chunk_size_px, downsampler.cpp:15-17), so only
+// the level extents vary per level.
 struct FusedParams
 {
     const uint8_t* src;      // level-0 frames, row-major
     uint64_t src_stride;     // bytes between frames
+    const FrameRef* refs;    // [(n_fused + 1) * n_frames], level-major
+    uint8_t* scratch;        // row-major frames of level scratch_level
+    uint32_t scratch_level;  // 0: no scratch output
     uint32_t n_frames;
     uint32_t n_fused;        // levels 1..n_fused computed here (<= kMaxFused)
     uint32_t rh_log2;        // region height = 1 << rh_log2 (>= 4)
     uint32_t nbx, nby;       // regions per frame along x / y
+    uint32_t nbx_in, nby_in; // interior (fast-path) regions along x / y
     uint32_t vec_rows;       // 1: every row start is 16-B aligned
-    LevelGeom lv[kMaxFused + 1];
+    uint32_t fast_ok;        // 1: tiles fit the interior fast path
+    uint32_t blocks_per_cu;  // persistent grid size (0 = occupancy)
+    uint32_t tw, th;         // chunk tile (x, y) in pixels
+    FastDiv dtw, dth;
+    uint64_t bpc;            // bytes per chunk
+    FastDiv d_nreg_in, d_nbx_in;
+    uint32_t W[kMaxFused + 1], H[kMaxFused + 1], ntx[kMaxFused + 1];
 };
 
 // One output frame (or partial plane) of the generic level kernel.  Pixel

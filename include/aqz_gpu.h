@@ -202,6 +202,8 @@ typedef struct
                                   halving XY until this many levels exist. */
     int32_t skip_level0_split; /* 1 = do not tile-split level 0 (pyramid
                                   only); default 0 = full stage */
+    uint32_t blocks_per_cu;    /* persistent-grid workgroups per CU of the
+                                  fused kernel (0 = occupancy limit) */
 } aqz_stage_options;
 
 typedef struct
