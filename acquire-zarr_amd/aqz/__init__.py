@@ -61,7 +61,7 @@ class ArrayDescC(C.Structure):
 class StageOptionsC(C.Structure):
     _fields_ = [("layer_slots", C.c_uint32), ("max_batch_frames", C.c_uint32),
                 ("force_levels", C.c_uint32), ("skip_level0_split", C.c_int32),
-                ("blocks_per_cu", C.c_uint32)]
+                ("blocks_per_cu", C.c_uint32), ("first_frame", C.c_uint64)]
 
 
 class LevelLayoutC(C.Structure):
@@ -340,12 +340,12 @@ class Stage:
     def __init__(self, dims, dtype, method, max_levels=0, multiscale=True,
                  storage_order=None, device=0, layer_slots=0,
                  max_batch_frames=0, force_levels=0, skip_level0_split=False,
-                 blocks_per_cu=0):
+                 blocks_per_cu=0, first_frame=0):
         self.dtype = dtype
         d, self._keep = _desc(dims, dtype, method, max_levels, multiscale,
                               storage_order, device)
         o = StageOptionsC(layer_slots, max_batch_frames, force_levels,
-                          1 if skip_level0_split else 0, blocks_per_cu)
+                          1 if skip_level0_split else 0, blocks_per_cu, first_frame)
         h = C.c_void_p()
         _check(lib().aqz_stage_create(C.byref(d), C.byref(o), C.byref(h)),
                "aqz_stage_create")

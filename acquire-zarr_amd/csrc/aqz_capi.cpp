@@ -397,6 +397,7 @@ aqz_stage_create(const aqz_array_desc* desc, const aqz_stage_options* opt,
             o.force_levels = opt->force_levels;
             o.skip_level0_split = opt->skip_level0_split != 0;
             o.blocks_per_cu = opt->blocks_per_cu;
+            o.first_frame = opt->first_frame;
         }
         auto* s = new aqz_stage;
         try {

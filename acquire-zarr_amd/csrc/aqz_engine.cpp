@@ -204,6 +204,8 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
     // 64-row regions whenever LDS-cascaded levels (>= 3) exist: amortises
     // the per-region barriers of the cascade over 32 KiB of input
     rh_log2_ = n_fused_ >= 3 ? 6 : 4;
+    if (const char* ev = std::getenv("AQZ_NT")) // tuning knob
+        nt_mode_ = uint32_t(std::atoi(ev)) & 3u;
     if (const char* ev = std::getenv("AQZ_REGION_ROWS_LOG2")) { // tuning knob
         const uint32_t v = uint32_t(std::atoi(ev));
         if (v >= std::max<uint32_t>(4, n_fused_) && (1u << v) <= uint32_t(kMaxRegionRows))
@@ -215,6 +217,17 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         max_frames_ = 1;
         for (size_t i = 0; i + 2 < n; ++i)
             max_frames_ *= lv_[0].dims[i].array_size_px;
+    }
+    // z-slab sharding: this stage continues a stream at first_frame
+    if (opt_.first_frame > 0) {
+        const uint64_t p0 = std::max<uint32_t>(1, lv_[0].planes);
+        for (auto& L : lv_) {
+            const uint64_t pk = std::max<uint32_t>(1, L.planes);
+            if ((opt_.first_frame * pk) % p0 != 0)
+                throw Error(9, "first_frame does not align with the z pyramid");
+            L.frames_written = opt_.first_frame * pk / p0;
+            L.level_frame_count = uint32_t(L.frames_written);
+        }
     }
     pend_.resize(lv_.size());
     for (auto& e : stage_ev_)
@@ -448,6 +461,7 @@ Stage::fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
                   ? 1
                   : 0;
     p.blocks_per_cu = opt_blocks_per_cu_;
+    p.nt = nt_mode_;
     p.nbx_in = p.fast_ok ? L0.W / RW : 0;
     p.nby_in = p.fast_ok ? L0.H >> rh_log2 : 0;
     p.d_nreg_in = make_fastdiv(std::max<uint32_t>(1, p.nbx_in * p.nby_in));

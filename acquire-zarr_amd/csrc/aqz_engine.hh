@@ -81,6 +81,7 @@ struct StageOptions
     uint32_t force_levels = 0;
     bool skip_level0_split = false;
     uint32_t blocks_per_cu = 0;
+    uint64_t first_frame = 0;
 };
 
 struct LevelLayout
@@ -185,6 +186,7 @@ class Stage
     hipEvent_t refs_ev_[2] = { nullptr, nullptr };
     int refs_idx_ = 0;
     uint32_t opt_blocks_per_cu_ = 0; // 0 = occupancy
+    uint32_t nt_mode_ = 0;           // non-temporal load/store bits
     std::vector<Pending> pend_;
     // kernel timing
     bool timing_ = false;

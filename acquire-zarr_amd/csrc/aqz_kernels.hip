@@ -436,6 +436,29 @@ shfl_down_t(T v, int d)
     }
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4
+ld16(const uint8_t* s, bool nt)
+{
+    u32x4 v;
+    if (nt)
+        v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s));
+    else
+        v = *reinterpret_cast<const u32x4*>(s);
+    return uint4{ v.x, v.y, v.z, v.w };
+}
+
+__device__ __forceinline__ void
+st16(uint8_t* d, const uint4& a, bool nt)
+{
+    const u32x4 v = { a.x, a.y, a.z, a.w };
+    if (nt)
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(d));
+    else
+        *reinterpret_cast<u32x4*>(d) = v;
+}
+
 // The two 16-B row vectors of this thread for one pass of an interior region.
 __device__ __forceinline__ void
 load_pass(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
@@ -445,8 +468,8 @@ load_pass(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
     const uint64_t row = uint64_t(p.W[0]) * bpp;
     const uint8_t* s = p.src + uint64_t(f) * p.src_stride + uint64_t(y) * row +
                        uint64_t(x0 + (threadIdx.x & 31) * (16 / bpp)) * bpp;
-    a = *reinterpret_cast<const uint4*>(s);
-    b = *reinterpret_cast<const uint4*>(s + row);
+    a = ld16(s, p.nt & 1);
+    b = ld16(s + row, p.nt & 1);
 }
 
 // One 16-row pass of an interior region: level-0 tile rows, level 1 (2x2 in
@@ -464,8 +487,8 @@ fast_pass(const FusedParams& p, uint32_t pass, const uint4& ra, const uint4& rb,
     const uint32_t trow = p.tw * uint32_t(sizeof(T)); // bytes per tile row
     if (t0.p) {
         const uint32_t dy = pass * 16 + 2 * rp;
-        *reinterpret_cast<uint4*>(t0.p + uint64_t(dy) * trow) = ra;
-        *reinterpret_cast<uint4*>(t0.p + uint64_t(dy + 1) * trow) = rb;
+        st16(t0.p + uint64_t(dy) * trow, ra, p.nt & 2);
+        st16(t0.p + uint64_t(dy + 1) * trow, rb, p.nt & 2);
         t0.nz |= ((ra.x | ra.y | ra.z | ra.w) | (rb.x | rb.y | rb.z | rb.w)) != 0u;
     }
     if (p.n_fused < 1)

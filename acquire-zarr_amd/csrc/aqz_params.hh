@@ -73,6 +73,7 @@ struct FusedParams
     uint32_t vec_rows;       // 1: every row start is 16-B aligned
     uint32_t fast_ok;        // 1: tiles fit the interior fast path
     uint32_t blocks_per_cu;  // persistent grid size (0 = occupancy)
+    uint32_t nt;             // bit0: non-temporal input loads, bit1: nt level-0 stores
     uint32_t tw, th;         // chunk tile (x, y) in pixels
     FastDiv dtw, dth;
     uint64_t bpc;            // bytes per chunk

@@ -204,6 +204,11 @@ typedef struct
                                   only); default 0 = full stage */
     uint32_t blocks_per_cu;    /* persistent-grid workgroups per CU of the
                                   fused kernel (0 = occupancy limit) */
+    uint64_t first_frame;      /* level-0 frame id of this stage's first
+                                  frame (z-slab sharding across GPUs: the
+                                  slab's first plane); level k starts at
+                                  first_frame * planes_k / planes_0, which
+                                  must be exact.  0 = a whole stream. */
 } aqz_stage_options;
 
 typedef struct

@@ -140,6 +140,25 @@ ref_dims_create(const or_dim* dims, int ndims, int dtype)
     }
 }
 
+void*
+ref_dims_create_ordered(const or_dim* dims, int ndims, int dtype,
+                        const size_t* order)
+{
+    try {
+        std::vector<size_t> ord(order, order + ndims);
+        return new ArrayDimensions(to_dims(dims, ndims),
+                                   static_cast<ZarrDataType>(dtype), ord);
+    } catch (...) {
+        return nullptr;
+    }
+}
+
+uint64_t
+ref_dims_transpose_frame_id(void* h, uint64_t fid)
+{
+    return static_cast<ArrayDimensions*>(h)->transpose_frame_id(fid);
+}
+
 void
 ref_dims_destroy(void* h)
 {

@@ -115,6 +115,10 @@ def ref():
         L.ref_ds_take_frame.argtypes = [vp, i32, vp, sz, C.POINTER(sz)]
         L.ref_dims_create.argtypes = [D, i32, i32]
         L.ref_dims_create.restype = vp
+        L.ref_dims_create_ordered.argtypes = [D, i32, i32, C.POINTER(sz)]
+        L.ref_dims_create_ordered.restype = vp
+        L.ref_dims_transpose_frame_id.argtypes = [vp, u64]
+        L.ref_dims_transpose_frame_id.restype = u64
         L.ref_dims_destroy.argtypes = [vp]
         for name, rt, extra in [
             ("tile_group_offset", u32, [u64]),
@@ -236,7 +240,7 @@ def oracle_average_two(dst: np.ndarray, src: np.ndarray, dtype: int, method: int
 class OracleDims:
     """ArrayDimensions index math on the C restatement or the reference."""
 
-    def __init__(self, dims, dtype, use_ref=False):
+    def __init__(self, dims, dtype, use_ref=False, order=None):
         self.dims = list(dims)
         self.dtype = dtype
         self.use_ref = use_ref
@@ -244,15 +248,24 @@ class OracleDims:
         self.n = len(dims)
         if use_ref:
             self.L = ref()
-            self.h = self.L.ref_dims_create(self._d, self.n, dtype)
+            if order is None:
+                self.h = self.L.ref_dims_create(self._d, self.n, dtype)
+            else:
+                self._o = (C.c_size_t * len(order))(*order)
+                self.h = self.L.ref_dims_create_ordered(self._d, self.n, dtype, self._o)
             assert self.h
         else:
+            assert order is None, "the C oracle takes storage-order dims"
             self.L = lib()
 
     def __del__(self):
         if self.use_ref and getattr(self, "h", None):
             self.L.ref_dims_destroy(self.h)
             self.h = None
+
+    def transpose_frame_id(self, fid):
+        assert self.use_ref
+        return self.L.ref_dims_transpose_frame_id(self.h, fid)
 
     def tile_group_offset(self, fid):
         if self.use_ref:

@@ -1,0 +1,134 @@
+"""CPU suite, part 2: the C-ABI library loads and exports every entry point
+include/aqz_gpu.h declares, and its host-side restatement of the chunk
+lattice / level geometry (which drives the kernels' addressing) matches the
+oracle and the compiled reference.  No GPU compute is called here."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import aqz
+import oracle_bindings as ob
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "aqz_gpu.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(aqz_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = aqz.lib()
+    names = declared_functions()
+    assert len(names) >= 40
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    # the binding wires every declared entry point
+    import inspect
+    src = inspect.getsource(aqz.lib)
+    assert all(f'"{n}"' in src for n in names)
+
+
+def test_library_is_gfx950_and_in_tree():
+    assert aqz.LIB_PATH.startswith(os.path.join(REPO, "acquire-zarr_amd"))
+    blob = open(aqz.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_status_messages_and_version():
+    L = aqz.lib()
+    assert L.aqz_version() == b"0.1.0"
+    assert L.aqz_status_message(0) == b"Success"
+    assert L.aqz_status_message(12) == b"Attempted write beyond array boundary"
+    assert aqz.device_count() >= 0
+
+
+def test_invalid_settings_map_to_status_codes():
+    with pytest.raises(aqz.AqzError) as e:
+        aqz.Dims([(ob.SPACE, 10, 5, 1)], ob.U16)
+    assert e.value.status == 9
+    with pytest.raises(aqz.AqzError) as e:
+        aqz.Dims([(ob.TIME, 0, 1, 1), (ob.CHANNEL, 3, 1, 1), (ob.SPACE, 10, 5, 1)], ob.U16)
+    assert e.value.status == 9
+    with pytest.raises(aqz.AqzError) as e:
+        aqz.Dims([(ob.TIME, 0, 1, 1), (ob.SPACE, 10, 5, 1), (ob.SPACE, 10, 5, 1)], 10)
+    assert e.value.status == 1
+    with pytest.raises(aqz.AqzError) as e:  # dim 0 moved away
+        aqz.Dims([(ob.TIME, 0, 1, 1), (ob.SPACE, 4, 2, 1), (ob.SPACE, 10, 5, 1),
+                  (ob.SPACE, 10, 5, 1)], ob.U16, storage_order=[1, 0, 2, 3])
+    assert e.value.status == 9
+
+
+def _random_dims(rng):
+    nd = int(rng.integers(3, 6))
+    dims = [(ob.TIME, int(rng.integers(0, 3)) * 4, int(rng.integers(1, 6)),
+             int(rng.integers(1, 3)))]
+    for _ in range(nd - 3):
+        dims.append((int(rng.integers(0, 3)), int(rng.integers(1, 7)),
+                     int(rng.integers(1, 4)), int(rng.integers(1, 3))))
+    dims += [(ob.SPACE, int(rng.integers(1, 80)), int(rng.integers(1, 12)),
+              int(rng.integers(1, 3))),
+             (ob.SPACE, int(rng.integers(1, 80)), int(rng.integers(1, 12)),
+              int(rng.integers(1, 3)))]
+    return dims
+
+
+def test_host_index_math_matches_oracle():
+    rng = np.random.default_rng(11)
+    for _ in range(150):
+        dims = _random_dims(rng)
+        dt = int(rng.integers(0, 10))
+        a, o = aqz.Dims(dims, dt), ob.OracleDims(dims, dt)
+        assert a.dims() == [tuple(d) for d in dims]
+        assert a.bytes_per_chunk() == o.bytes_per_chunk()
+        assert a.number_of_chunks_in_memory() == o.number_of_chunks_in_memory()
+        assert a.frames_per_chunk_layer() == o.frames_per_chunk_layer()
+        for fid in range(40):
+            assert a.tile_group_offset(fid) == o.tile_group_offset(fid)
+            assert a.chunk_internal_offset(fid) == o.chunk_internal_offset(fid)
+            for d in range(len(dims) - 2):
+                assert a.chunk_lattice_index(fid, d) == o.chunk_lattice_index(fid, d)
+            assert a.transpose_frame_id(fid) == fid
+        cps = int(np.prod([d[3] for d in dims]))
+        nsh = int(np.prod([-(-(-(-d[1] // d[2])) // d[3]) for d in dims[1:]]))
+        for c in range(min(cps * nsh, 200)):
+            assert a.shard_index_for_chunk(c) == o.shard_index_for_chunk(c)
+            assert a.shard_internal_index(c) == o.shard_internal_index(c)
+
+
+def test_host_pyramid_levels_match_oracle():
+    rng = np.random.default_rng(12)
+    for _ in range(200):
+        dims = _random_dims(rng)
+        ml = int(rng.integers(0, 4))
+        lv = aqz.pyramid_levels(dims, ml)
+        od = ob.OracleDownsampler(dims, ob.U16, ob.MEAN, ml)
+        assert len(lv) == od.n_levels()
+        for l, d in enumerate(lv):
+            assert [tuple(x) for x in d] == [tuple(x) for x in od.level_dims(l)]
+    # 2-D arrays get the phantom singleton (array.dimensions.cpp:149-153)
+    lv = aqz.pyramid_levels([(ob.SPACE, 64, 16, 1), (ob.SPACE, 64, 16, 1)])
+    assert len(lv) == 3 and lv[0][0] == (ob.OTHER, 1, 1, 1)
+
+
+@pytest.mark.skipif(not ob.ref_available(), reason="oracle/_ref not built")
+def test_host_transposition_matches_reference():
+    rng = np.random.default_rng(13)
+    for _ in range(60):
+        inner = [(ob.CHANNEL, int(rng.integers(1, 5)), 1, 1),
+                 (ob.SPACE, int(rng.integers(1, 6)), int(rng.integers(1, 3)), 1),
+                 (ob.OTHER, int(rng.integers(1, 4)), 1, 1)]
+        dims = [(ob.TIME, int(rng.integers(0, 2)) * 3, int(rng.integers(1, 3)), 1)] + inner + \
+               [(ob.SPACE, 12, 4, 1), (ob.SPACE, 8, 4, 1)]
+        perm = [0] + [1 + int(i) for i in rng.permutation(3)] + [4, 5]
+        a = aqz.Dims(dims, ob.U16, storage_order=perm)
+        r = ob.OracleDims(dims, ob.U16, use_ref=True, order=perm)
+        n = 60 if dims[0][1] == 0 else int(np.prod([d[1] for d in dims[:-2]]))
+        for fid in range(n):
+            assert a.transpose_frame_id(fid) == r.transpose_frame_id(fid)
+            assert a.tile_group_offset(a.transpose_frame_id(fid)) == \
+                r.tile_group_offset(r.transpose_frame_id(fid))

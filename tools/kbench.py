@@ -33,7 +33,9 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--bpc", type=int, default=0)
-    ap.add_argument("--rh", default="5,6,7")
+    ap.add_argument("--rh", default="6,7")
+    ap.add_argument("--bpcs", default="2,3,4,6,8")
+    ap.add_argument("--nt", default="0")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     stream = torch.cuda.Stream(dev)
@@ -45,18 +47,27 @@ def main():
     dst = torch.empty(B * fbytes, dtype=torch.uint8, device=dev)
     dims = [(TIME, 0, 64, 1), (SPACE, H, 256, 1), (SPACE, W, 256, 1)]
     variants = {}
+    bytes_moved_extra = {}
 
     def mk(name, **kw):
-        st = aqz.Stage(dims, 1, 1, max_batch_frames=B, layer_slots=2,
-                       blocks_per_cu=args.bpc, **kw)
+        kw.setdefault("blocks_per_cu", args.bpc)
+        st = aqz.Stage(dims, 1, 1, max_batch_frames=B, layer_slots=2, **kw)
         st.set_stream(stream.cuda_stream)
         variants[name] = st
 
     for rh in args.rh.split(","):
         os.environ["AQZ_REGION_ROWS_LOG2"] = rh
-        mk(f"full5_rh{rh}", force_levels=5)
+        for nt in args.nt.split(","):
+            os.environ["AQZ_NT"] = nt
+            mk(f"full5_rh{rh}_nt{nt}", force_levels=5)
+        os.environ["AQZ_NT"] = "0"
         mk(f"pyr5_rh{rh}", force_levels=5, skip_level0_split=True)
     os.environ.pop("AQZ_REGION_ROWS_LOG2")
+    os.environ.pop("AQZ_NT")
+    for b in args.bpcs.split(","):
+        if b:
+            mk(f"full5_bpc{b}", force_levels=5, blocks_per_cu=int(b))
+            bytes_moved_extra[f"full5_bpc{b}"] = B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64 + 1 / 256))
     mk("split_only", multiscale=False)
     mk("full4_refrule")
     state = {"i": 0}
@@ -76,12 +87,13 @@ def main():
         return ring[i * B * fbytes:(i + 1) * B * fbytes].view(torch.int64).sum()
 
     bytes_moved = {
-        **{f"full5_rh{rh}": B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64 + 1 / 256)) for rh in args.rh.split(",")},
+        **{f"full5_rh{rh}_nt{nt}": B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64 + 1 / 256)) for rh in args.rh.split(",") for nt in args.nt.split(",")},
         **{f"pyr5_rh{rh}": B * fbytes * (1 + (1 / 4 + 1 / 16 + 1 / 64 + 1 / 256)) for rh in args.rh.split(",")},
         "split_only": B * fbytes * 2,
         "full4_refrule": B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64)),
         "torch_copy": B * fbytes * 2,
         "torch_sum": B * fbytes,
+        **bytes_moved_extra,
     }
     res = {k: [] for k in bytes_moved}
     for rnd in range(args.rounds):
