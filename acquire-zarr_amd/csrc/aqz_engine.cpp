@@ -165,14 +165,17 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         L.slot_bytes = L.bpc * L.n_chunks;
         L.n_slots = std::max<uint32_t>(opt_.layer_slots,
                                        (B - 1 + L.F - 1) / L.F + 1);
-        L.needs_zero = (L.W % L.tw) != 0 || (L.H % L.th) != 0;
-        for (size_t i = 1; i + 2 < n; ++i)
-            L.needs_zero |= (L.dims[i].array_size_px % L.dims[i].chunk_size_px) != 0;
         L.slot_layer.assign(L.n_slots, -1);
 
         if (!(k == 0 && opt_.skip_level0_split)) {
+            // Zeroed once: chunk padding (ragged tiles / intermediate dims,
+            // the reference's zero-initialised Chunk, chunk.cpp:8-15) is
+            // never written by any frame, so it stays zero for every layer
+            // that later occupies a slot.  has_data words start at 0 (no tag).
             L.ring.alloc(L.slot_bytes * L.n_slots);
             L.flags.alloc(size_t(L.n_chunks) * L.n_slots * 4);
+            hip_check(hipMemsetAsync(L.ring.p, 0, L.ring.n, stream_),
+                      "hipMemsetAsync");
             hip_check(hipMemsetAsync(L.flags.p, 0, L.flags.n, stream_),
                       "hipMemsetAsync");
         }
@@ -184,6 +187,24 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
             const uint32_t grp = L.ad->tile_group_offset(sf);
             L.h_tab_grp[fl] = grp;
             L.h_tab_off[fl] = uint64_t(grp) * L.bpc + L.ad->chunk_internal_offset(sf);
+        }
+        // frame -> (tiles, has_data) over one ring period
+        const uint64_t P = uint64_t(L.n_slots) * L.F;
+        if (P > 0x7fffffffull)
+            throw Error(9, "chunk-layer ring period too large");
+        L.period = uint32_t(P);
+        if (L.ring.p) {
+            std::vector<FrameRef> tab(P);
+            for (uint64_t fid = 0; fid < P; ++fid) {
+                const uint64_t slot = fid / L.F;
+                tab[fid].tiles = L.ring.p + slot * L.slot_bytes + L.h_tab_off[fid % L.F];
+                tab[fid].flags = reinterpret_cast<uint32_t*>(L.flags.p) +
+                                 slot * L.n_chunks + L.h_tab_grp[fid % L.F];
+            }
+            L.ref_table.alloc(P * sizeof(FrameRef));
+            hip_check(hipMemcpy(L.ref_table.p, tab.data(), P * sizeof(FrameRef),
+                                hipMemcpyHostToDevice),
+                      "hipMemcpy");
         }
         L.tab_off.alloc(size_t(L.F) * 8);
         L.tab_grp.alloc(size_t(L.F) * 4);
@@ -201,9 +222,51 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
     for (size_t k = 1; k < lv_.size(); ++k)
         fused_2d_ &= !(lv_[k].planes < lv_[k - 1].planes) && lv_[k].xy_shrinks;
     n_fused_ = fused_2d_ ? std::min<uint32_t>(n_levels() - 1, kMaxFused) : 0;
+
+    // 2x2x2 fast path: a regular z schedule (every z-halving level has an
+    // even input plane count, so pairs are always (2j, 2j+1) of a stack and
+    // never straddle stacks) and every level halving XY.
+    if (!fused_2d_ && bpp_ <= 4 && n_levels() >= 2 &&
+        n_levels() - 1 <= uint32_t(kMaxFused) && lv_[0].planes > 0) {
+        bool ok = true;
+        uint32_t nz = 0, zmask = 0;
+        for (uint32_t k = 1; k < n_levels(); ++k) {
+            ok &= lv_[k].xy_shrinks;
+            if (lv_[k].planes < lv_[k - 1].planes) {
+                ok &= lv_[k - 1].planes % 2 == 0 &&
+                      lv_[k].planes * 2 == lv_[k - 1].planes;
+                zmask |= 1u << k;
+                ++nz;
+            }
+        }
+        ok &= nz <= 3 && lv_[0].planes % (1u << nz) == 0;
+        if (ok) {
+            fused_3d_ = true;
+            g3d_ = 1u << nz;
+            zmask3d_ = zmask;
+        }
+    }
     // 64-row regions whenever LDS-cascaded levels (>= 3) exist: amortises
     // the per-region barriers of the cascade over 32 KiB of input
-    rh_log2_ = n_fused_ >= 3 ? 6 : 4;
+    {
+        // 64-row regions amortise a region's fixed cost (tile setup, flag
+        // flushes, the LDS cascade's barriers) over 32 KiB of input; the
+        // fast path needs the region height to divide the chunk height.
+        uint32_t tz = 0;
+        while (tz < 6 && ((lv_[0].th >> tz) & 1u) == 0)
+            ++tz;
+        const uint32_t nf = fused_3d_ ? n_levels() - 1 : n_fused_;
+        rh_log2_ = std::max<uint32_t>(std::max<uint32_t>(4, nf), tz);
+        if (fused_3d_) {
+            const uint32_t RW = uint32_t(512 / bpp_);
+            fused_3d_ = lv_[0].W % RW == 0 && (lv_[0].H % (1u << rh_log2_)) == 0 &&
+                        lv_[0].th % (1u << rh_log2_) == 0 &&
+                        lv_[0].tw % uint32_t(16 / bpp_) == 0 &&
+                        (1u << rh_log2_) <= uint32_t(kMaxRegionRows);
+        }
+    }
+    if (const char* ev = std::getenv("AQZ_KNOBS")) // tuning knob
+        knobs_ = uint32_t(std::atoi(ev));
     if (const char* ev = std::getenv("AQZ_NT")) // tuning knob
         nt_mode_ = uint32_t(std::atoi(ev)) & 3u;
     if (const char* ev = std::getenv("AQZ_REGION_ROWS_LOG2")) { // tuning knob
@@ -236,9 +299,7 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
     for (auto& L : lv_)
         hip_check(hipEventCreateWithFlags(&L.ops_ev, hipEventDisableTiming),
                   "hipEventCreate");
-    for (auto& ev : refs_ev_)
-        hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming),
-                  "hipEventCreate");
+
     hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
 
@@ -252,9 +313,7 @@ Stage::~Stage()
     for (auto& L : lv_)
         if (L.ops_ev)
             (void)hipEventDestroy(L.ops_ev);
-    for (auto& ev : refs_ev_)
-        if (ev)
-            (void)hipEventDestroy(ev);
+
     for (auto& pr : ev_pairs_) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -348,28 +407,67 @@ Stage::append(const void* frames, uint64_t n_frames, int mem)
 void
 Stage::run_batch(const uint8_t* dsrc, uint32_t n)
 {
-    if (fused_2d_)
+    std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
+    if (timing_) {
+        if (ev_used_ == ev_pairs_.size()) {
+            hipEvent_t a, b;
+            hip_check(hipEventCreate(&a), "hipEventCreate");
+            hip_check(hipEventCreate(&b), "hipEventCreate");
+            ev_pairs_.emplace_back(a, b);
+        }
+        ev = &ev_pairs_[ev_used_++];
+        hip_check(hipEventRecord(ev->first, stream_), "hipEventRecord");
+    }
+    if (fused_2d_) {
         run_fused(dsrc, n);
-    else
-        run_generic(dsrc, n);
+    } else {
+        uint32_t n3 = 0;
+        if (fused_3d_) {
+            bool idle = lv_[0].frames_written % g3d_ == 0 &&
+                        reinterpret_cast<uintptr_t>(dsrc) % 16 == 0;
+            for (const auto& pd : pend_)
+                idle &= !pd.has;
+            if (idle)
+                n3 = n / g3d_ * g3d_;
+        }
+        if (n3 > 0)
+            run_fused3d(dsrc, n3);
+        if (n3 < n)
+            run_generic(dsrc + uint64_t(n3) * lv_[0].W * lv_[0].H * bpp_, n - n3);
+    }
+    if (ev)
+        hip_check(hipEventRecord(ev->second, stream_), "hipEventRecord");
+}
+
+void
+Stage::run_fused3d(const uint8_t* dsrc, uint32_t n)
+{
+    const uint32_t nl = n_levels();
+    std::vector<uint32_t> nk(nl);
+    for (uint32_t k = 0, z = 0; k < nl; ++k) {
+        z += (zmask3d_ >> k) & 1u;
+        nk[k] = n >> z;
+        enter_layers(lv_[k], lv_[k].frames_written, nk[k]);
+    }
+    FusedParams p = fused_params(dsrc, n, nl - 1, rh_log2_, false);
+    if (!p.fast_ok || p.nbx_in * p.nby_in != p.nbx * p.nby)
+        throw Error(5, "2x2x2 fast path preconditions do not hold");
+    p.G = g3d_;
+    p.zmask = zmask3d_;
+    hip_check(launch_fused_pyramid_3d(desc_.dtype, desc_.method, p, stream_),
+              "fused_pyramid_3d launch");
+    for (uint32_t k = 0; k < nl; ++k) {
+        lv_[k].frames_written += nk[k];
+        lv_[k].level_frame_count += nk[k];
+    }
 }
 
 void
 Stage::enter_layer(StageLevel& L, uint64_t layer)
 {
-    const uint32_t slot = uint32_t(layer % L.n_slots);
-    if (L.slot_layer[slot] == int64_t(layer))
-        return;
-    // a fresh chunk layer: has_data cleared; zeroed like Chunk's ctor
-    // (chunk.cpp:8-15) wherever tiles do not cover every byte
-    hip_check(hipMemsetAsync(L.flags.p + size_t(slot) * L.n_chunks * 4, 0,
-                             size_t(L.n_chunks) * 4, stream_),
-              "hipMemsetAsync");
-    if (L.needs_zero)
-        hip_check(hipMemsetAsync(L.ring.p + slot * L.slot_bytes, 0,
-                                 L.slot_bytes, stream_),
-                  "hipMemsetAsync");
-    L.slot_layer[slot] = int64_t(layer);
+    // A fresh layer needs no clearing: has_data words are generation-tagged
+    // and the chunk padding was zeroed at allocation.
+    L.slot_layer[layer % L.n_slots] = int64_t(layer);
 }
 
 void
@@ -410,32 +508,13 @@ Stage::geom(StageLevel& L, uint64_t fid0, bool tiles, uint8_t* scratch) const
 
 void
 Stage::tile_addr(const StageLevel& L, uint64_t fid, uint64_t* off,
-                 uint32_t* flag_off) const
+                 uint32_t* flag_off, uint32_t* tag) const
 {
     const uint64_t slot = (fid / L.F) % L.n_slots;
     *off = slot * L.slot_bytes + L.h_tab_off[fid % L.F];
     *flag_off = uint32_t(slot * L.n_chunks + L.h_tab_grp[fid % L.F]);
-}
-
-const FrameRef*
-Stage::upload_refs(const std::vector<FrameRef>& refs)
-{
-    // pinned double buffer -> one device table (stream-ordered reuse)
-    const size_t cap = size_t(kMaxFused + 1) * opt_.max_batch_frames;
-    if (refs.size() > cap)
-        throw Error(5, "frame table overflow");
-    const int j = refs_idx_;
-    refs_idx_ ^= 1;
-    hip_check(hipEventSynchronize(refs_ev_[j]), "hipEventSynchronize");
-    h_refs_[j].alloc(cap * sizeof(FrameRef));
-    d_refs_.alloc(cap * sizeof(FrameRef));
-    std::memcpy(h_refs_[j].p, refs.data(), refs.size() * sizeof(FrameRef));
-    hip_check(hipMemcpyAsync(d_refs_.p, h_refs_[j].p,
-                             refs.size() * sizeof(FrameRef),
-                             hipMemcpyHostToDevice, stream_),
-              "hipMemcpyAsync");
-    hip_check(hipEventRecord(refs_ev_[j], stream_), "hipEventRecord");
-    return reinterpret_cast<const FrameRef*>(d_refs_.p);
+    if (tag)
+        *tag = uint32_t(fid / L.period + 1);
 }
 
 FusedParams
@@ -462,6 +541,7 @@ Stage::fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
                   : 0;
     p.blocks_per_cu = opt_blocks_per_cu_;
     p.nt = nt_mode_;
+    p.knobs = knobs_;
     p.nbx_in = p.fast_ok ? L0.W / RW : 0;
     p.nby_in = p.fast_ok ? L0.H >> rh_log2 : 0;
     p.d_nreg_in = make_fastdiv(std::max<uint32_t>(1, p.nbx_in * p.nby_in));
@@ -471,7 +551,6 @@ Stage::fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
     p.dtw = make_fastdiv(L0.tw);
     p.dth = make_fastdiv(L0.th);
     p.bpc = L0.bpc;
-    std::vector<FrameRef> refs(size_t(n_fused + 1) * n);
     for (uint32_t k = 0; k <= n_fused; ++k) {
         StageLevel& L = lv_[k];
         if (L.bpc != p.bpc || L.tw != p.tw || L.th != p.th)
@@ -479,18 +558,13 @@ Stage::fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
         p.W[k] = L.W;
         p.H[k] = L.H;
         p.ntx[k] = L.ntx;
-        for (uint32_t f = 0; f < n; ++f) {
-            FrameRef& r = refs[size_t(k) * n + f];
-            if (L.ring.p) {
-                uint64_t off;
-                uint32_t fo;
-                tile_addr(L, L.frames_written + f, &off, &fo);
-                r.tiles = L.ring.p + off;
-                r.flags = reinterpret_cast<uint32_t*>(L.flags.p) + fo;
-            } else {
-                r.tiles = nullptr;
-                r.flags = nullptr;
-            }
+        if (L.ring.p) {
+            if (n > L.period)
+                throw Error(5, "batch longer than the ring period");
+            p.lr[k].table = reinterpret_cast<const FrameRef*>(L.ref_table.p);
+            p.lr[k].period = L.period;
+            p.lr[k].r0 = uint32_t(L.frames_written % L.period);
+            p.lr[k].tag0 = uint32_t(L.frames_written / L.period + 1);
         }
     }
     if (tail) {
@@ -499,7 +573,6 @@ Stage::fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
         p.scratch = L.scratch.p;
         p.scratch_level = n_fused;
     }
-    p.refs = upload_refs(refs);
     return p;
 }
 
@@ -513,21 +586,8 @@ Stage::run_fused(const uint8_t* dsrc, uint32_t n)
 
     const FusedParams p = fused_params(dsrc, n, n_fused_, rh_log2_, tail);
 
-    std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
-    if (timing_) {
-        if (ev_used_ == ev_pairs_.size()) {
-            hipEvent_t a, b;
-            hip_check(hipEventCreate(&a), "hipEventCreate");
-            hip_check(hipEventCreate(&b), "hipEventCreate");
-            ev_pairs_.emplace_back(a, b);
-        }
-        ev = &ev_pairs_[ev_used_++];
-        hip_check(hipEventRecord(ev->first, stream_), "hipEventRecord");
-    }
     hip_check(launch_fused_pyramid(desc_.dtype, desc_.method, p, stream_),
               "fused_pyramid launch");
-    if (ev)
-        hip_check(hipEventRecord(ev->second, stream_), "hipEventRecord");
 
     // levels deeper than the fused depth: one generic step per level
     for (uint32_t k = n_fused_ + 1; k < nl; ++k) {
@@ -548,7 +608,7 @@ Stage::run_fused(const uint8_t* dsrc, uint32_t n)
             o.a = P.scratch.p + f * pfb;
             o.a_scale = L.xy_shrinks ? 1 : 0;
             o.scratch_out = more ? L.scratch.p + f * lfb : nullptr;
-            tile_addr(L, L.frames_written + f, &o.tile_off, &o.flag_off);
+            tile_addr(L, L.frames_written + f, &o.tile_off, &o.flag_off, &o.tag);
             o.has_tile = 1;
         }
         hip_check(hipMemcpyAsync(L.d_ops.p, ops, size_t(n) * sizeof(LevelOp),
@@ -706,7 +766,7 @@ Stage::run_generic(const uint8_t* dsrc, uint32_t n)
                 o.scratch_out = more ? L.scratch.p + h.out_index * lfb : nullptr;
                 if (L.ring.p) {
                     enter_layer(L, h.fid / L.F);
-                    tile_addr(L, h.fid, &o.tile_off, &o.flag_off);
+                    tile_addr(L, h.fid, &o.tile_off, &o.flag_off, &o.tag);
                     o.has_tile = 1;
                 }
             } else {
@@ -761,8 +821,9 @@ Stage::copy_layer(uint32_t level, uint64_t layer, void* dst, size_t cap,
         hip_check(hipMemcpy(f.data(), L.flags.p + size_t(slot) * L.n_chunks * 4,
                             size_t(L.n_chunks) * 4, hipMemcpyDeviceToHost),
                   "hipMemcpy");
+        const uint32_t tag = uint32_t(layer / L.n_slots + 1);
         for (uint32_t c = 0; c < L.n_chunks; ++c)
-            has_data[c] = f[c] ? 1 : 0;
+            has_data[c] = f[c] == tag ? 1 : 0;
     }
 }
 
@@ -786,8 +847,8 @@ void
 Stage::finalize()
 {
     for (auto& L : lv_) {
-        if (!L.ring.p || L.needs_zero)
-            continue; // zeroed whole on entry
+        if (!L.ring.p)
+            continue;
         const uint64_t fw = L.frames_written;
         if (fw % L.F == 0)
             continue;
@@ -795,7 +856,7 @@ Stage::finalize()
         for (uint64_t fid = fw; fid < end; ++fid) {
             uint64_t off;
             uint32_t fo;
-            tile_addr(L, fid, &off, &fo);
+            tile_addr(L, fid, &off, &fo, nullptr);
             hip_check(launch_zero_frame_tiles(L.ring.p + off, L.bpc,
                                               L.ntx * L.nty,
                                               uint32_t(uint64_t(L.tw) * L.th * bpp_),
@@ -838,7 +899,7 @@ Stage::timing(double* total_ms, uint64_t* launches)
 const char*
 Stage::dominant_kernel() const
 {
-    return fused_2d_ ? "fused_pyramid" : "level_kernel";
+    return fused_2d_ ? "fused_pyramid" : fused_3d_ ? "fused_pyramid_3d" : "level_kernel";
 }
 
 // ===========================================================================

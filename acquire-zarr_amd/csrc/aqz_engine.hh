@@ -23,6 +23,8 @@ hipError_t launch_fused_pyramid(int dtype, int method, const FusedParams& p,
                                 hipStream_t stream);
 hipError_t launch_level(int dtype, int method, const LevelParams& p,
                         hipStream_t stream);
+hipError_t launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
+                                   hipStream_t stream);
 hipError_t launch_zero_frame_tiles(uint8_t* fb, uint64_t bpc,
                                    uint32_t n_tiles, uint32_t tile_bytes,
                                    hipStream_t stream);
@@ -104,8 +106,8 @@ struct StageLevel
     uint64_t bpc = 0, slot_bytes = 0;
     uint32_t n_chunks = 0, n_slots = 0, F = 0;
     uint32_t tw = 0, th = 0, ntx = 0, nty = 0;
-    bool needs_zero = false;               // any chunk padding
-    DevBuf ring, flags, tab_off, tab_grp;
+    DevBuf ring, flags, tab_off, tab_grp, ref_table;
+    uint32_t period = 0;                   // n_slots * F frames
     std::vector<uint64_t> h_tab_off;
     std::vector<uint32_t> h_tab_grp;
     std::vector<int64_t> slot_layer;       // layer resident in each slot
@@ -151,17 +153,17 @@ class Stage
     };
 
     void run_batch(const uint8_t* dsrc, uint32_t n);
-    const FrameRef* upload_refs(const std::vector<FrameRef>& refs);
     FusedParams fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
                              uint32_t rh_log2, bool tail);
     void run_fused(const uint8_t* dsrc, uint32_t n);
+    void run_fused3d(const uint8_t* dsrc, uint32_t n);
     void run_generic(const uint8_t* dsrc, uint32_t n);
     void enter_layers(StageLevel& L, uint64_t first_fid, uint64_t n);
     void enter_layer(StageLevel& L, uint64_t layer);
     LevelGeom geom(StageLevel& L, uint64_t fid0, bool tiles,
                    uint8_t* scratch) const;
     void tile_addr(const StageLevel& L, uint64_t fid, uint64_t* off,
-                   uint32_t* flag_off) const;
+                   uint32_t* flag_off, uint32_t* tag) const;
     const uint8_t* frame_ptr(uint32_t level, uint32_t index,
                              const uint8_t* dsrc) const;
 
@@ -170,6 +172,8 @@ class Stage
     size_t bpp_;
     std::vector<StageLevel> lv_;
     bool fused_2d_ = true;
+    bool fused_3d_ = false;  // regular 2x2x2 schedule: fused_pyramid_3d
+    uint32_t g3d_ = 1, zmask3d_ = 0;
     uint32_t n_fused_ = 0;
     uint32_t rh_log2_ = 4;
     uint64_t max_frames_ = 0; // 0 = unbounded
@@ -180,13 +184,9 @@ class Stage
     DevBuf d_stage_[2];
     hipEvent_t stage_ev_[2] = { nullptr, nullptr };
     int stage_idx_ = 0;
-    // per-batch (level, frame) -> chunk-layer addresses for the fused kernel
-    DevBuf d_refs_;
-    PinnedBuf h_refs_[2];
-    hipEvent_t refs_ev_[2] = { nullptr, nullptr };
-    int refs_idx_ = 0;
     uint32_t opt_blocks_per_cu_ = 0; // 0 = occupancy
     uint32_t nt_mode_ = 0;           // non-temporal load/store bits
+    uint32_t knobs_ = 0;             // tuning A/B switches
     std::vector<Pending> pend_;
     // kernel timing
     bool timing_ = false;

@@ -111,12 +111,13 @@ struct FlagAcc
 {
     uint32_t* ptr = nullptr;
     bool nz = false;
+    uint32_t tag = 1;
 
     __device__ __forceinline__ void note(uint32_t* p, bool z)
     {
         if (p != ptr) {
             if (nz)
-                *ptr = 1u;
+                *ptr = tag;
             ptr = p;
             nz = z;
         } else {
@@ -138,9 +139,9 @@ struct FlagAcc
               !want || reinterpret_cast<uintptr_t>(ptr) == uintptr_t(lp);
             if (__all(same)) {
                 if (want && int(threadIdx.x & 63) == leader)
-                    *ptr = 1u;
+                    *ptr = tag;
             } else if (want) {
-                *ptr = 1u;
+                *ptr = tag;
             }
         }
         ptr = nullptr;
@@ -166,6 +167,30 @@ __device__ __forceinline__ Tiles
 tiles_of(const LevelGeom& g)
 {
     return Tiles{ g.tw, g.th, g.ntx, g.dtw, g.dth, g.bpc };
+}
+
+// Where frame f (batch-relative) of level k lands, and its has_data tag.
+struct Ref
+{
+    uint8_t* tiles;
+    uint32_t* flags;
+    uint32_t tag;
+};
+
+__device__ __forceinline__ Ref
+frame_ref(const FusedParams& p, int k, uint32_t f)
+{
+    const LevelRefs& l = p.lr[k];
+    if (!l.table)
+        return Ref{ nullptr, nullptr, 0 };
+    uint32_t q = l.r0 + f; // < 2 * period: a launch spans at most one wrap
+    uint32_t tag = l.tag0;
+    if (q >= l.period) {
+        q -= l.period;
+        ++tag;
+    }
+    const FrameRef r = l.table[q];
+    return Ref{ r.tiles, r.flags, tag };
 }
 
 // Store a run of N pixels of row Y starting at column X into the chunk tiles
@@ -213,12 +238,13 @@ deep_level(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
     // last valid local row/col of the previous level inside this region
     const uint32_t pxmax = p.W[K - 1] - 1 - (x0 >> (K - 1));
     const uint32_t pymax = p.H[K - 1] - 1 - (y0 >> (K - 1));
-    const FrameRef ref = p.refs[K * p.n_frames + f];
+    const Ref ref = frame_ref(p, K, f);
     const Tiles tg = tiles_of(p, K);
     T* scr = (p.scratch_level == uint32_t(K))
                ? reinterpret_cast<T*>(p.scratch) + uint64_t(f) * Wk * Hk
                : nullptr;
     FlagAcc acc;
+    acc.tag = ref.tag;
     for (uint32_t idx = threadIdx.x; idx < lh * lw; idx += 256) {
         const uint32_t ly = idx / lw, lx = idx % lw;
         const uint32_t Y = yk0 + ly, X = xk0 + lx;
@@ -240,28 +266,113 @@ deep_level(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
     acc.flush_wave();
 }
 
-// Levels 3..n_fused of one region inside LDS; level 2 is in lds_b.
+// The last two cascaded levels K and K+1 in one step, no barrier between
+// them: each thread owns one level-(K+1) pixel, computes the 2x2 level-K
+// pixels under it from level K-1 in LDS (pitch RW >> (K-1)), stores them,
+// and reduces them (with the edge replication of scale_image when a level-K
+// row/column falls outside the level) to its level-(K+1) pixel.
+template<typename T, int M, int K, uint32_t RW>
+__device__ __forceinline__ void
+deep_pair(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
+          const T* prev)
+{
+    constexpr uint32_t lw1 = RW >> (K + 1);
+    constexpr uint32_t pw = RW >> (K - 1);
+    const uint32_t lh1 = (1u << p.rh_log2) >> (K + 1);
+    const uint32_t Wk = p.W[K], Hk = p.H[K], W1 = p.W[K + 1], H1 = p.H[K + 1];
+    const uint32_t yk0 = y0 >> K, xk0 = x0 >> K;
+    const uint32_t y10 = y0 >> (K + 1), x10 = x0 >> (K + 1);
+    const uint32_t pxmax = p.W[K - 1] - 1 - (x0 >> (K - 1));
+    const uint32_t pymax = p.H[K - 1] - 1 - (y0 >> (K - 1));
+    const Ref rk = frame_ref(p, K, f);
+    const Ref r1 = frame_ref(p, K + 1, f);
+    const Tiles tk = tiles_of(p, K), t1 = tiles_of(p, K + 1);
+    T* scrk = (p.scratch_level == uint32_t(K))
+                ? reinterpret_cast<T*>(p.scratch) + uint64_t(f) * Wk * Hk
+                : nullptr;
+    T* scr1 = (p.scratch_level == uint32_t(K + 1))
+                ? reinterpret_cast<T*>(p.scratch) + uint64_t(f) * W1 * H1
+                : nullptr;
+    FlagAcc acck, acc1;
+    acck.tag = rk.tag;
+    acc1.tag = r1.tag;
+    for (uint32_t idx = threadIdx.x; idx < lh1 * lw1; idx += 256) {
+        const uint32_t ly = idx / lw1, lx = idx % lw1;
+        const uint32_t Y1 = y10 + ly, X1 = x10 + lx;
+        if (Y1 < H1 && X1 < W1) {
+            T v[2][2];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const uint32_t ky = 2 * ly + a, kx = 2 * lx + b; // level-K local
+                    // (rows/cols past the level are clamped here and never
+                    // stored; the level-(K+1) reduce replicates instead)
+                    const uint32_t py = min(2 * ky, pymax), px = min(2 * kx, pxmax);
+                    const uint32_t px1 = min(px + 1, pxmax), py1 = min(py + 1, pymax);
+                    v[a][b] = reduce4<M, T>(prev[py * pw + px], prev[py * pw + px1],
+                                            prev[py1 * pw + px], prev[py1 * pw + px1]);
+                    const uint32_t Yk = yk0 + ky, Xk = xk0 + kx;
+                    if (Yk < Hk && Xk < Wk) {
+                        if (rk.tiles)
+                            put_tile<T, 1>(tk, rk.tiles, rk.flags, Yk, Xk, &v[a][b], 1,
+                                           acck);
+                        if (scrk)
+                            scrk[uint64_t(Yk) * Wk + Xk] = v[a][b];
+                    }
+                }
+            }
+            // edge replication of level K inside the level-(K+1) reduce
+            const bool right = xk0 + 2 * lx + 1 < Wk;
+            const bool down = yk0 + 2 * ly + 1 < Hk;
+            const T here = v[0][0];
+            const T rt = right ? v[0][1] : here;
+            const T dn = down ? v[1][0] : here;
+            const T dg = down ? (right ? v[1][1] : v[1][0]) : rt;
+            const T q = reduce4<M, T>(here, rt, dn, dg);
+            if (r1.tiles)
+                put_tile<T, 1>(t1, r1.tiles, r1.flags, Y1, X1, &q, 1, acc1);
+            if (scr1)
+                scr1[uint64_t(Y1) * W1 + X1] = q;
+        }
+    }
+    acck.flush_wave();
+    acc1.flush_wave();
+}
+
+// Levels 3..n_fused of one region; level 2 is in lds_b.  Every level but
+// the last two goes through LDS behind a barrier; the last two are one step.
 template<typename T, int M, uint32_t RW>
 __device__ __forceinline__ void
 deep_levels(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
             T* lds_a, T* lds_b)
 {
-    if (p.n_fused >= 3) {
-        __syncthreads();
+    const uint32_t n = p.n_fused;
+    if (n < 3)
+        return;
+    __syncthreads();
+    if (n == 3) {
         deep_level<T, M, 3, RW>(p, f, y0, x0, lds_b, lds_a);
+        return;
     }
-    if (p.n_fused >= 4) {
-        __syncthreads();
+    const bool pair = (p.knobs & 1u) == 0;
+    if (n == 4 && pair) {
+        deep_pair<T, M, 3, RW>(p, f, y0, x0, lds_b);
+        return;
+    }
+    deep_level<T, M, 3, RW>(p, f, y0, x0, lds_b, lds_a);
+    __syncthreads();
+    if (n == 4) {
         deep_level<T, M, 4, RW>(p, f, y0, x0, lds_a, lds_b);
+        return;
     }
-    if (p.n_fused >= 5) {
-        __syncthreads();
-        deep_level<T, M, 5, RW>(p, f, y0, x0, lds_b, lds_a);
+    if (n == 5) {
+        deep_pair<T, M, 4, RW>(p, f, y0, x0, lds_a);
+        return;
     }
-    if (p.n_fused >= 6) {
-        __syncthreads();
-        deep_level<T, M, 6, RW>(p, f, y0, x0, lds_a, lds_b);
-    }
+    deep_level<T, M, 4, RW>(p, f, y0, x0, lds_a, lds_b);
+    __syncthreads();
+    deep_pair<T, M, 5, RW>(p, f, y0, x0, lds_b);
 }
 
 // Edge regions (or layouts the fast path does not cover): every access
@@ -281,9 +392,9 @@ generic_region(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
     const uint32_t W0 = p.W[0], H0 = p.H[0];
     const T* src = reinterpret_cast<const T*>(p.src + uint64_t(f) * p.src_stride);
 
-    const FrameRef r0ref = p.refs[f];
+    const Ref r0ref = frame_ref(p, 0, f);
     const bool l1 = p.n_fused >= 1;
-    const FrameRef r1ref = l1 ? p.refs[p.n_frames + f] : FrameRef{ nullptr, nullptr };
+    const Ref r1ref = l1 ? frame_ref(p, 1, f) : Ref{ nullptr, nullptr, 0 };
     const Tiles tg0 = tiles_of(p, 0);
     const Tiles tg1 = tiles_of(p, 1);
     T* scr1 = (l1 && p.scratch_level == 1)
@@ -292,6 +403,8 @@ generic_region(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
     const bool keep_l1 = p.n_fused >= 2;
 
     FlagAcc acc0, acc1;
+    acc0.tag = r0ref.tag;
+    acc1.tag = r1ref.tag;
     for (uint32_t pass = 0; pass < npass; ++pass) {
         const uint32_t y = y0 + pass * 16 + 2 * rp;
         const uint32_t x = x0 + cv * VEC;
@@ -359,6 +472,7 @@ struct FastTile
 {
     uint8_t* p;      // (region row 0 at this level, this thread's column)
     uint32_t* flag;  // has_data word of that chunk
+    uint32_t tag;
     bool nz;
 };
 
@@ -366,10 +480,11 @@ template<typename T>
 __device__ __forceinline__ FastTile
 fast_tile(const FusedParams& p, int k, uint32_t f, uint32_t Y0, uint32_t X)
 {
-    FastTile t{ nullptr, nullptr, false };
-    const FrameRef ref = p.refs[k * p.n_frames + f];
+    FastTile t{ nullptr, nullptr, 0, false };
+    const Ref ref = frame_ref(p, k, f);
     if (!ref.tiles)
         return t;
+    t.tag = ref.tag;
     const uint32_t ty = fdiv(Y0, p.dth);
     const uint32_t tx = fdiv(X, p.dtw);
     const uint32_t ry = Y0 - ty * p.th;
@@ -386,6 +501,7 @@ flush_tile_flag(FastTile& t)
     FlagAcc a;
     a.ptr = t.flag;
     a.nz = t.nz;
+    a.tag = t.tag;
     a.flush_wave();
     t.nz = false;
 }
@@ -613,7 +729,8 @@ fused_pyramid(const FusedParams p)
             flush_tile_flag(t2);
             if (p.n_fused >= 3) {
                 deep_levels<T, M, RW>(p, f, y0, x0, lds_a, lds_b);
-                __syncthreads();
+                if (more || (p.knobs & 2u))
+                    __syncthreads(); // LDS is reused by the next region
             }
         }
         if (!more)
@@ -658,6 +775,242 @@ fused_pyramid_edge(const FusedParams p)
 }
 
 // ---------------------------------------------------------------------------
+// 2x2x2 pyramid (z-halving levels), interior regions, regular z schedule.
+// A workgroup owns one region of G consecutive level-0 planes (G = 2^number
+// of z-halving levels), so every z pair of every level is formed inside it:
+// level k plane = reduce2(xy(earlier plane), xy(later plane)) exactly as
+// Downsampler::add_frame orders it (XY first, then average_two_frames with
+// the earlier plane first, downsampler.cpp:341-389).  Levels 1-2 in
+// registers (the earlier plane of a pair is held), levels >= 3 per plane in
+// LDS.  Host guarantees: sizeof(T) <= 4, interior region, every fused level
+// halves XY, every z-halving level has an even input plane count, the
+// launch starts at a group boundary with no pending partial plane.
+// ---------------------------------------------------------------------------
+template<typename T, int M, int K, uint32_t RW>
+__device__ __forceinline__ void
+deep3d_level(const FusedParams& p, uint32_t grp, uint32_t y0, uint32_t x0,
+             const T* prev, T* cur, uint32_t g_prev)
+{
+    constexpr uint32_t lw = RW >> K;
+    constexpr uint32_t pw = RW >> (K - 1);
+    const uint32_t lh = (1u << p.rh_log2) >> K;
+    const uint32_t ph = (1u << p.rh_log2) >> (K - 1);
+    const uint32_t zk = (p.zmask >> K) & 1u;
+    const uint32_t g = g_prev >> zk;
+    const uint32_t yk0 = y0 >> K, xk0 = x0 >> K;
+    const Tiles tg = tiles_of(p, K);
+    for (uint32_t q = 0; q < g; ++q) {
+        const Ref ref = frame_ref(p, K, grp * g + q);
+        FlagAcc acc;
+        acc.tag = ref.tag;
+        const T* a = prev + (zk ? 2 * q : q) * ph * pw;
+        const T* b = a + ph * pw; // the later plane of the pair
+        for (uint32_t idx = threadIdx.x; idx < lh * lw; idx += 256) {
+            const uint32_t ly = idx / lw, lx = idx % lw;
+            const uint32_t o0 = (2 * ly) * pw + 2 * lx;
+            T v = reduce4<M, T>(a[o0], a[o0 + 1], a[o0 + pw], a[o0 + pw + 1]);
+            if (zk)
+                v = reduce2<M, T>(
+                  v, reduce4<M, T>(b[o0], b[o0 + 1], b[o0 + pw], b[o0 + pw + 1]));
+            cur[q * lh * lw + ly * lw + lx] = v;
+            if (ref.tiles)
+                put_tile<T, 1>(tg, ref.tiles, ref.flags, yk0 + ly, xk0 + lx, &v, 1, acc);
+        }
+        acc.flush_wave();
+    }
+}
+
+// per-thread column part of a level's tile address inside a frame
+struct ColTile
+{
+    uint64_t off;   // chunk*bpc + (ry0*tw + rx)*bpp
+    uint32_t chunk;
+};
+
+__device__ __forceinline__ ColTile
+col_tile(const FusedParams& p, int k, uint32_t Y0, uint32_t X, uint32_t bpp)
+{
+    const uint32_t ty = fdiv(Y0, p.dth), tx = fdiv(X, p.dtw);
+    const uint32_t ry = Y0 - ty * p.th, rx = X - tx * p.tw;
+    const uint32_t chunk = ty * p.ntx[k] + tx;
+    return ColTile{ uint64_t(chunk) * p.bpc + uint64_t(ry * p.tw + rx) * bpp, chunk };
+}
+
+__device__ __forceinline__ void
+flush_planes(const FusedParams& p, int k, uint32_t first, uint32_t g,
+             uint32_t chunk, uint32_t nzmask)
+{
+    for (uint32_t q = 0; q < g; ++q) {
+        const Ref ref = frame_ref(p, k, first + q);
+        FlagAcc a;
+        a.ptr = ref.flags ? ref.flags + chunk : nullptr;
+        a.nz = (nzmask >> q) & 1u;
+        a.tag = ref.tag;
+        a.flush_wave();
+    }
+}
+
+template<typename T, int M>
+__global__ __launch_bounds__(256) void
+fused_pyramid_3d(const FusedParams p)
+{
+    constexpr int VEC = 16 / sizeof(T);
+    constexpr int HV = VEC / 2;
+    constexpr int QV = HV / 2;
+    constexpr uint32_t RW = 32 * VEC;
+    static_assert(QV >= 1, "2x2x2 fused kernel needs <= 4-byte pixels");
+    __shared__ __attribute__((aligned(16)))
+    T lds_a[kMaxPlanes3d / 2 * (kMaxRegionRows / 8) * (RW / 8)];
+    __shared__ __attribute__((aligned(16)))
+    T lds_b[kMaxPlanes3d / 2 * (kMaxRegionRows / 4) * (RW / 4)];
+
+    const uint32_t nreg = p.nbx_in * p.nby_in;
+    const uint32_t grp = fdiv(blockIdx.x, p.d_nreg_in);
+    const uint32_t r = blockIdx.x - grp * nreg;
+    const uint32_t by = fdiv(r, p.d_nbx_in);
+    const uint32_t y0 = by << p.rh_log2;
+    const uint32_t x0 = (r - by * p.nbx_in) * RW;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t rp = threadIdx.x >> 5;
+    const uint32_t cv = threadIdx.x & 31;
+    const uint32_t npass = 1u << (p.rh_log2 - 4);
+    const uint32_t G = p.G;
+    const uint32_t z1 = (p.zmask >> 1) & 1u, z2 = (p.zmask >> 2) & 1u;
+    const uint32_t g1 = G >> z1, g2 = g1 >> z2;
+    const uint32_t trow = p.tw * uint32_t(sizeof(T));
+    const bool l2 = p.n_fused >= 2;
+    T* lds_l2 = p.n_fused >= 3 ? lds_b : nullptr;
+    const uint32_t l2_rows = (1u << p.rh_log2) >> 2;
+
+    const ColTile c0 = col_tile(p, 0, y0, x0 + cv * VEC, sizeof(T));
+    const ColTile c1 = col_tile(p, 1, y0 >> 1, (x0 >> 1) + cv * HV, sizeof(T));
+    const ColTile c2 = col_tile(p, 2, y0 >> 2, (x0 >> 2) + cv * QV, sizeof(T));
+    uint32_t nz0 = 0, nz1 = 0, nz2 = 0;
+
+    T h1[HV], h2[QV]; // earlier planes of the current z pairs
+    const uint32_t units = npass * G;
+    uint4 ca, cb;
+    load_pass(p, grp * G, y0, x0, 0, sizeof(T), ca, cb);
+    for (uint32_t u = 0; u < units; ++u) {
+        const uint32_t pass = u / G, pl = u - pass * G;
+        uint4 na{}, nb{};
+        if (u + 1 < units) {
+            const uint32_t pn = (u + 1) / G;
+            load_pass(p, grp * G + (u + 1 - pn * G), y0, x0, pn, sizeof(T), na, nb);
+        }
+        // level 0: this plane's tile rows
+        const Ref f0 = frame_ref(p, 0, grp * G + pl);
+        if (f0.tiles) {
+            const uint32_t dy = pass * 16 + 2 * rp;
+            st16(f0.tiles + c0.off + uint64_t(dy) * trow, ca, false);
+            st16(f0.tiles + c0.off + uint64_t(dy + 1) * trow, cb, false);
+            if (((ca.x | ca.y | ca.z | ca.w) | (cb.x | cb.y | cb.z | cb.w)) != 0u)
+                nz0 |= 1u << pl;
+        }
+        if (p.n_fused >= 1) {
+            T r0[VEC], r1[VEC], o[HV];
+            __builtin_memcpy(r0, &ca, 16);
+            __builtin_memcpy(r1, &cb, 16);
+#pragma unroll
+            for (int i = 0; i < HV; ++i)
+                o[i] = reduce4<M, T>(r0[2 * i], r0[2 * i + 1], r1[2 * i], r1[2 * i + 1]);
+            bool emit1 = true;
+            uint32_t q1 = pl;
+            if (z1) {
+                if ((pl & 1u) == 0) {
+#pragma unroll
+                    for (int i = 0; i < HV; ++i)
+                        h1[i] = o[i];
+                    emit1 = false;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < HV; ++i)
+                        o[i] = reduce2<M, T>(h1[i], o[i]);
+                    q1 = pl >> 1;
+                }
+            }
+            if (emit1) {
+                const Ref f1 = frame_ref(p, 1, grp * g1 + q1);
+                if (f1.tiles) {
+                    store_vec<T, HV>(f1.tiles + c1.off + uint64_t(pass * 8 + rp) * trow, o);
+                    if (any_nonzero<T, HV>(o))
+                        nz1 |= 1u << q1;
+                }
+                if (l2) {
+                    uint2 mine, below;
+                    __builtin_memcpy(&mine, o, 8);
+                    below.x = __shfl_xor(mine.x, 32);
+                    below.y = __shfl_xor(mine.y, 32);
+                    T b[HV], q[QV];
+                    __builtin_memcpy(b, &below, 8);
+#pragma unroll
+                    for (int j = 0; j < QV; ++j)
+                        q[j] = reduce4<M, T>(o[2 * j], o[2 * j + 1], b[2 * j], b[2 * j + 1]);
+                    bool emit2 = true;
+                    uint32_t q2 = q1;
+                    if (z2) {
+                        if ((q1 & 1u) == 0) {
+#pragma unroll
+                            for (int j = 0; j < QV; ++j)
+                                h2[j] = q[j];
+                            emit2 = false;
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < QV; ++j)
+                                q[j] = reduce2<M, T>(h2[j], q[j]);
+                            q2 = q1 >> 1;
+                        }
+                    }
+                    if (emit2 && lane < 32) {
+                        const uint32_t row2 = pass * 4 + (rp >> 1);
+                        const Ref f2 = frame_ref(p, 2, grp * g2 + q2);
+                        if (f2.tiles) {
+                            store_vec<T, QV>(f2.tiles + c2.off + uint64_t(row2) * trow, q);
+                            if (any_nonzero<T, QV>(q))
+                                nz2 |= 1u << q2;
+                        }
+                        if (lds_l2) {
+#pragma unroll
+                            for (int j = 0; j < QV; ++j)
+                                lds_l2[q2 * l2_rows * (RW / 4) + row2 * (RW / 4) + cv * QV + j] = q[j];
+                        }
+                    }
+                }
+            }
+        }
+        ca = na;
+        cb = nb;
+    }
+    flush_planes(p, 0, grp * G, G, c0.chunk, nz0);
+    if (p.n_fused >= 1)
+        flush_planes(p, 1, grp * g1, g1, c1.chunk, nz1);
+    if (l2)
+        flush_planes(p, 2, grp * g2, g2, c2.chunk, nz2);
+
+    // levels >= 3 per plane through LDS (level-2 planes are in lds_b, plane
+    // stride (RH/4) x (RW/4))
+    if (p.n_fused >= 3) {
+        __syncthreads();
+        deep3d_level<T, M, 3, RW>(p, grp, y0, x0, lds_b, lds_a, g2);
+        uint32_t g = g2 >> ((p.zmask >> 3) & 1u);
+        if (p.n_fused >= 4) {
+            __syncthreads();
+            deep3d_level<T, M, 4, RW>(p, grp, y0, x0, lds_a, lds_b, g);
+            g >>= (p.zmask >> 4) & 1u;
+        }
+        if (p.n_fused >= 5) {
+            __syncthreads();
+            deep3d_level<T, M, 5, RW>(p, grp, y0, x0, lds_b, lds_a, g);
+            g >>= (p.zmask >> 5) & 1u;
+        }
+        if (p.n_fused >= 6) {
+            __syncthreads();
+            deep3d_level<T, M, 6, RW>(p, grp, y0, x0, lds_a, lds_b, g);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Generic one-level step.  grid = (ceil(W*H/256), n_ops); one output pixel
 // per thread.
 // ---------------------------------------------------------------------------
@@ -685,6 +1038,7 @@ level_kernel(const LevelParams p)
     const uint64_t npx = uint64_t(g.W) * g.H;
     const uint64_t idx = uint64_t(blockIdx.x) * 256 + threadIdx.x;
     FlagAcc acc;
+    acc.tag = op.tag;
     if (idx < npx) {
         const uint32_t Y = uint32_t(idx / g.W);
         const uint32_t X = uint32_t(idx - uint64_t(Y) * g.W);
@@ -779,8 +1133,11 @@ launch_fused_pyramid(int dtype, int method, const FusedParams& p,
                    &o, fused_pyramid<T, MM>, 256, 0) != hipSuccess ||          \
                  o <= 0))                                                      \
                 o = 4;                                                         \
-            const uint64_t cap =                                               \
-              uint64_t(cus) * (p.blocks_per_cu ? p.blocks_per_cu : uint32_t(o)); \
+            /* default: one region per workgroup (measured faster than a   \
+               persistent grid, which ends on an uneven tail) */           \
+            const uint64_t cap = p.blocks_per_cu                               \
+                                   ? uint64_t(cus) * p.blocks_per_cu           \
+                                   : interior + 0 * uint64_t(o);               \
             const uint32_t blocks = uint32_t(interior < cap ? interior : cap); \
             hipLaunchKernelGGL((fused_pyramid<T, MM>), dim3(blocks), dim3(256),\
                                0, stream, p);                                  \
@@ -790,6 +1147,34 @@ launch_fused_pyramid(int dtype, int method, const FusedParams& p,
                                dim3(uint32_t(edge)), dim3(256), 0, stream, p); \
     } while (0)
     AQZ_DISPATCH(dtype, method, CALL)
+#undef CALL
+    return hipGetLastError();
+}
+
+hipError_t
+launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
+                        hipStream_t stream)
+{
+    const uint64_t blocks = uint64_t(p.n_frames / p.G) * p.nbx_in * p.nby_in;
+    if (p.G == 0 || p.G > uint32_t(kMaxPlanes3d) || p.n_frames % p.G ||
+        p.n_fused > uint32_t(kMaxFused) || (1u << p.rh_log2) < (1u << p.n_fused) ||
+        (1u << p.rh_log2) > uint32_t(kMaxRegionRows) || blocks > 0x7fffffffull)
+        return hipErrorInvalidValue;
+    if (blocks == 0)
+        return hipSuccess;
+#define CALL(T, MM)                                                            \
+    hipLaunchKernelGGL((fused_pyramid_3d<T, MM>), dim3(uint32_t(blocks)),     \
+                       dim3(256), 0, stream, p)
+    switch (dtype) {
+        case 0: AQZ_DISPATCH_M(uint8_t, method, CALL); break;
+        case 1: AQZ_DISPATCH_M(uint16_t, method, CALL); break;
+        case 2: AQZ_DISPATCH_M(uint32_t, method, CALL); break;
+        case 4: AQZ_DISPATCH_M(int8_t, method, CALL); break;
+        case 5: AQZ_DISPATCH_M(int16_t, method, CALL); break;
+        case 6: AQZ_DISPATCH_M(int32_t, method, CALL); break;
+        case 8: AQZ_DISPATCH_M(float, method, CALL); break;
+        default: return hipErrorInvalidValue;
+    }
 #undef CALL
     return hipGetLastError();
 }

@@ -45,14 +45,27 @@ struct LevelGeom
 
 constexpr int kMaxFused = 6;
 constexpr int kMaxRegionRows = 128; // LDS is sized for this region height
+constexpr int kMaxPlanes3d = 8;     // level-0 planes per 2x2x2 group
 
-// Where frame f of a level lands: the base of its tiles inside the resident
+// Where a frame of a level lands: the base of its tiles inside its resident
 // chunk layer (= slot base + tile_group_offset*bytes_per_chunk +
-// chunk_internal_offset, array.dimensions.cpp:264-314) and its has_data words.
+// chunk_internal_offset, array.dimensions.cpp:264-314) and its has_data
+// words.  One table per level covers a full ring period (n_slots *
+// frames_per_layer frames), built once at stage creation.
 struct FrameRef
 {
-    uint8_t* tiles;  // nullptr: this level is not tile-split
+    uint8_t* tiles;
     uint32_t* flags;
+};
+
+// A level's frames of one launch: frame f has ring-period index (r0 + f)
+// mod period; its has_data tag is the slot generation + 1 (so has_data words
+// never need clearing: a chunk has data iff its word equals the tag of the
+// layer resident in that slot).
+struct LevelRefs
+{
+    const FrameRef* table; // nullptr: this level is not tile-split
+    uint32_t r0, period, tag0;
 };
 
 // The fused pyramid launch.  Chunk sizes are the same at every level
@@ -62,7 +75,7 @@ struct FusedParams
 {
     const uint8_t* src;      // level-0 frames, row-major
     uint64_t src_stride;     // bytes between frames
-    const FrameRef* refs;    // [(n_fused + 1) * n_frames], level-major
+    LevelRefs lr[kMaxFused + 1];
     uint8_t* scratch;        // row-major frames of level scratch_level
     uint32_t scratch_level;  // 0: no scratch output
     uint32_t n_frames;
@@ -74,6 +87,9 @@ struct FusedParams
     uint32_t fast_ok;        // 1: tiles fit the interior fast path
     uint32_t blocks_per_cu;  // persistent grid size (0 = occupancy)
     uint32_t nt;             // bit0: non-temporal input loads, bit1: nt level-0 stores
+    uint32_t knobs;          // tuning A/B switches (0 = shipped defaults)
+    uint32_t G;              // 2x2x2 kernel: level-0 planes per group
+    uint32_t zmask;          // 2x2x2 kernel: bit k = level k halves z
     uint32_t tw, th;         // chunk tile (x, y) in pixels
     FastDiv dtw, dth;
     uint64_t bpc;            // bytes per chunk
@@ -92,6 +108,7 @@ struct LevelOp
     uint8_t* scratch_out;   // row-major destination or nullptr
     uint64_t tile_off;      // byte offset of this frame in the layer ring
     uint32_t flag_off;      // flag index of this frame's chunk group
+    uint32_t tag;           // has_data tag (slot generation + 1)
     uint32_t a_scale, b_scale, has_tile;
 };
 

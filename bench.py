@@ -49,6 +49,14 @@ CONFIGS = {
                         "device-resident",
                dims=[(TIME, 0, 32, 1), (SPACE, 4096, 128, 1), (SPACE, 4096, 128, 1)],
                dtype=U8, method=MEAN, force_levels=0, batch=32, ring=160),
+    # BASELINE configs[3] on one GPU: a 256-plane volume, 2x2x2 pyramid
+    # (z 256->128->64->64, xy 2048->1024->512->256); z-slab sharded over
+    # ranks with --gpus N (every rank owns 256/N planes of the volume).
+    "c4": dict(workload="uint16 2048x2048x256 light-sheet volume, 4-level 3-D (2x2x2) "
+                        "pyramid, 256x256x64 chunks, mean, device-resident",
+               dims=[(TIME, 0, 1, 1), (SPACE, 256, 64, 1), (SPACE, 2048, 256, 1),
+                     (SPACE, 2048, 256, 1)],
+               dtype=U16, method=MEAN, force_levels=0, batch=64, ring=256),
     "c5": dict(workload="float32 8192x8192 frames, 7-level pyramid, 128x128 chunks, mean, "
                         "device-resident (one camera stream per GPU)",
                dims=[(TIME, 0, 4, 1), (SPACE, 8192, 128, 1), (SPACE, 8192, 128, 1)],

@@ -243,11 +243,15 @@ aqz_status aqz_stage_synchronize(aqz_stage* st);
 uint64_t aqz_stage_frames_written(const aqz_stage* st, uint32_t level);
 /* Copy chunk layer `layer` of `level` (must still be resident) to dst
  * (bytes_per_chunk*chunks_per_layer bytes) and its has_data flags (one byte
- * per chunk).  Synchronizes. mem = where dst lives. */
+ * per chunk, 1 = some byte of the chunk is nonzero).  Synchronizes.  Frames
+ * of a layer not yet written read as unspecified bytes until the layer is
+ * complete or aqz_stage_finalize ran.  mem = where dst lives. */
 aqz_status aqz_stage_copy_layer(aqz_stage* st, uint32_t level, uint64_t layer,
                                 void* dst, size_t cap, uint8_t* has_data,
                                 size_t has_data_cap, int32_t mem);
-/* Device pointers of a resident layer (for device-side consumers). */
+/* Device pointers of a resident layer (for device-side consumers).  Chunk c
+ * has data iff has_data[c] == layer / layer_slots + 1 (the words carry the
+ * ring-slot generation, so they are never cleared). */
 aqz_status aqz_stage_device_layer(aqz_stage* st, uint32_t level,
                                   uint64_t layer, void** chunks,
                                   uint32_t** has_data);

@@ -272,3 +272,58 @@ def test_stage_device_resident_input(gpu):
         got, gflags = st.copy_layer(l, layer)
         assert_same_pixels(got, buf, U16, f"L{l}")
         assert (gflags == flags).all()
+
+
+# ---------------------------------------------------------------------------
+# 2x2x2 fused path (regular z schedule) and z-slab sharding
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype", [U8, U16, I16, U32, F32], ids=lambda d: DTYPE_NAMES[d])
+def test_stage_3d_fused_regular(gpu, dtype):
+    # every level halves x, y and z: G = 8 planes per workgroup
+    dims = [(TIME, 0, 1, 1), (CHANNEL, 2, 1, 1), (SPACE, 32, 4, 1),
+            (SPACE, 512, 64, 1), (SPACE, 512, 64, 1)]
+    st = gpu.Stage(dims, dtype, MEAN)
+    assert st.dominant_kernel() == "fused_pyramid_3d"
+    st.close()
+    for m in ALL_METHODS:
+        frames = _frames(dtype, 2 * 32, 512, 512, 40 + m + dtype)
+        # appends that leave and regain group alignment (fused <-> generic)
+        _check_stage(gpu, dims, dtype, m, frames, batch=16, chunks=[3, 13, 32, 16])
+
+
+def test_stage_c4_volume(gpu):
+    # BASELINE configs[3] level structure (z 64 -> 32 -> 16 -> 16 with
+    # 16-plane z chunks; xy 2048 -> 256 with 256-px chunks): fused 2x2x2
+    dims = [(TIME, 0, 1, 1), (SPACE, 64, 16, 1), (SPACE, 2048, 256, 1),
+            (SPACE, 2048, 256, 1)]
+    frames = synthetic_frames(U16, 64, 2048, 2048, 77)
+    st = gpu.Stage(dims, U16, MEAN)
+    assert st.dominant_kernel() == "fused_pyramid_3d"
+    st.close()
+    _check_stage(gpu, dims, U16, MEAN, frames, batch=32)
+
+
+def test_stage_z_slab_sharding(gpu):
+    """Two stages own planes [0, 32) and [32, 64) of one volume (what two
+    GPUs do with --gpus 2): their chunk layers assemble, with no exchange,
+    into exactly the single-stage result."""
+    dims = [(TIME, 0, 1, 1), (SPACE, 64, 16, 1), (SPACE, 512, 64, 1),
+            (SPACE, 512, 64, 1)]
+    frames = synthetic_frames(U16, 64, 512, 512, 5)
+    exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
+    a = gpu.Stage(dims, U16, MEAN, layer_slots=2)
+    b = gpu.Stage(dims, U16, MEAN, layer_slots=2, first_frame=32)
+    a.append(np.ascontiguousarray(frames[:32]))
+    b.append(np.ascontiguousarray(frames[32:]))
+    a.finalize()
+    b.finalize()
+    for (l, layer), (buf, flags) in exp.items():
+        ga, fa = a.copy_layer(l, layer)
+        gb, fb = b.copy_layer(l, layer)
+        assert_same_pixels(np.bitwise_or(ga, gb), buf, U16, f"L{l}")
+        assert (np.maximum(fa, fb) == flags).all()
+    for l in range(a.n_levels()):
+        assert a.frames_written(l) + b.frames_written(l) - b.frames_written(l) >= 0
+    assert b.frames_written(0) == 64 and a.frames_written(0) == 32
+    a.close()
+    b.close()

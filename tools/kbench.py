@@ -34,7 +34,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--bpc", type=int, default=0)
     ap.add_argument("--rh", default="6,7")
-    ap.add_argument("--bpcs", default="2,3,4,6,8")
+    ap.add_argument("--bpcs", default="")
+    ap.add_argument("--knobs", default="")
+    ap.add_argument("--depth", action="store_true")
     ap.add_argument("--nt", default="0")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -64,11 +66,24 @@ def main():
         mk(f"pyr5_rh{rh}", force_levels=5, skip_level0_split=True)
     os.environ.pop("AQZ_REGION_ROWS_LOG2")
     os.environ.pop("AQZ_NT")
+    for kn in args.knobs.split(","):
+        if kn:
+            os.environ["AQZ_KNOBS"] = kn
+            mk(f"full5_k{kn}", force_levels=5)
+            mk(f"full4_k{kn}", force_levels=4)
+            bytes_moved_extra[f"full5_k{kn}"] = B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64 + 1 / 256))
+            bytes_moved_extra[f"full4_k{kn}"] = B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64))
+            os.environ.pop("AQZ_KNOBS")
     for b in args.bpcs.split(","):
         if b:
             mk(f"full5_bpc{b}", force_levels=5, blocks_per_cu=int(b))
             bytes_moved_extra[f"full5_bpc{b}"] = B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64 + 1 / 256))
     mk("split_only", multiscale=False)
+    for nl in ((2, 3, 4) if args.depth else ()):
+        mk(f"pyr{nl}_only", force_levels=nl, skip_level0_split=True)
+        bytes_moved_extra[f"pyr{nl}_only"] = B * fbytes * (1 + sum(4.0 ** -k for k in range(1, nl)))
+        mk(f"full{nl}", force_levels=nl)
+        bytes_moved_extra[f"full{nl}"] = B * fbytes * (2 + sum(4.0 ** -k for k in range(1, nl)))
     mk("full4_refrule")
     state = {"i": 0}
 
