@@ -118,7 +118,6 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         opt_.layer_slots = 2;
     if (opt_.max_batch_frames == 0)
         opt_.max_batch_frames = 64;
-    opt_blocks_per_cu_ = opt_.blocks_per_cu;
 
     auto base = std::make_unique<ArrayDimensions>(desc.dims, desc.dtype,
                                                   desc.storage_order);
@@ -535,11 +534,14 @@ Stage::fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
                   reinterpret_cast<uintptr_t>(dsrc) % 16 == 0)
                    ? 1
                    : 0;
-    p.fast_ok = (p.vec_rows && L0.th % (1u << rh_log2) == 0 &&
+    // (the interior kernel addresses a frame's tiles with 32-bit offsets)
+    bool small_layers = true;
+    for (uint32_t k = 0; k <= n_fused; ++k)
+        small_layers = small_layers && lv_[k].slot_bytes < (uint64_t(1) << 32);
+    p.fast_ok = (p.vec_rows && small_layers && L0.th % (1u << rh_log2) == 0 &&
                  L0.tw % uint32_t(16 / bpp_) == 0 && !(tail && n_fused <= 2))
                   ? 1
                   : 0;
-    p.blocks_per_cu = opt_blocks_per_cu_;
     p.nt = nt_mode_;
     p.knobs = knobs_;
     p.nbx_in = p.fast_ok ? L0.W / RW : 0;

@@ -184,7 +184,6 @@ class Stage
     DevBuf d_stage_[2];
     hipEvent_t stage_ev_[2] = { nullptr, nullptr };
     int stage_idx_ = 0;
-    uint32_t opt_blocks_per_cu_ = 0; // 0 = occupancy
     uint32_t nt_mode_ = 0;           // non-temporal load/store bits
     uint32_t knobs_ = 0;             // tuning A/B switches
     std::vector<Pending> pend_;

@@ -375,6 +375,120 @@ deep_levels(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
     deep_pair<T, M, 5, RW>(p, f, y0, x0, lds_b);
 }
 
+// ---- interior cascade (levels >= 3) ----------------------------------------
+// An interior region lies wholly inside level 0, so every level-k pixel of it
+// exists and so do its four parents: no clamping.  Stores address the tiles
+// with 32-bit offsets from the frame's FrameRef (the host keeps the fast path
+// to layers < 4 GiB) and raise has_data with a plain per-pixel store, which
+// keeps these rarely-run loops from pinning registers the row passes need.
+template<typename T>
+__device__ __forceinline__ void
+put_px(const FusedParams& p, int k, const Ref& r, uint32_t Y, uint32_t X, T v)
+{
+    const uint32_t ty = fdiv(Y, p.dth), tx = fdiv(X, p.dtw);
+    const uint32_t chunk = ty * p.ntx[k] + tx;
+    const uint32_t off = chunk * uint32_t(p.bpc) +
+                         ((Y - ty * p.th) * p.tw + (X - tx * p.tw)) * uint32_t(sizeof(T));
+    *reinterpret_cast<T*>(r.tiles + off) = v;
+    if (nonzero_bits(v))
+        r.flags[chunk] = r.tag;
+}
+
+template<typename T>
+__device__ __forceinline__ T*
+scratch_of(const FusedParams& p, int k, uint32_t f)
+{
+    return p.scratch_level == uint32_t(k)
+             ? reinterpret_cast<T*>(p.scratch) + uint64_t(f) * p.W[k] * p.H[k]
+             : nullptr;
+}
+
+template<typename T, int M, int K, uint32_t RW>
+__device__ __forceinline__ void
+lean_level(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0, const T* prev,
+           T* cur)
+{
+    constexpr uint32_t lw = RW >> K, pw = RW >> (K - 1);
+    const uint32_t n = ((1u << p.rh_log2) >> K) * lw;
+    const Ref ref = frame_ref(p, K, f);
+    T* scr = scratch_of<T>(p, K, f);
+#pragma unroll 1
+    for (uint32_t idx = threadIdx.x; idx < n; idx += 256) {
+        const uint32_t ly = idx / lw, lx = idx % lw;
+        const T* q = prev + 2 * ly * pw + 2 * lx;
+        const T v = reduce4<M, T>(q[0], q[1], q[pw], q[pw + 1]);
+        cur[idx] = v;
+        const uint32_t Y = (y0 >> K) + ly, X = (x0 >> K) + lx;
+        if (ref.tiles)
+            put_px<T>(p, K, ref, Y, X, v);
+        if (scr)
+            scr[uint64_t(Y) * p.W[K] + X] = v;
+    }
+}
+
+// levels K and K+1 in one step: each thread owns one level-(K+1) pixel
+template<typename T, int M, int K, uint32_t RW>
+__device__ __forceinline__ void
+lean_pair(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0, const T* prev)
+{
+    constexpr uint32_t lw1 = RW >> (K + 1), pw = RW >> (K - 1);
+    const uint32_t n = ((1u << p.rh_log2) >> (K + 1)) * lw1;
+    const Ref rk = frame_ref(p, K, f), r1 = frame_ref(p, K + 1, f);
+    T* scrk = scratch_of<T>(p, K, f);
+    T* scr1 = scratch_of<T>(p, K + 1, f);
+#pragma unroll 1
+    for (uint32_t idx = threadIdx.x; idx < n; idx += 256) {
+        const uint32_t ly = idx / lw1, lx = idx % lw1;
+        T v[2][2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const T* q = prev + (4 * ly + 2 * a) * pw + 4 * lx + 2 * b;
+                v[a][b] = reduce4<M, T>(q[0], q[1], q[pw], q[pw + 1]);
+                const uint32_t Y = (y0 >> K) + 2 * ly + a, X = (x0 >> K) + 2 * lx + b;
+                if (rk.tiles)
+                    put_px<T>(p, K, rk, Y, X, v[a][b]);
+                if (scrk)
+                    scrk[uint64_t(Y) * p.W[K] + X] = v[a][b];
+            }
+        }
+        const T w = reduce4<M, T>(v[0][0], v[0][1], v[1][0], v[1][1]);
+        const uint32_t Y1 = (y0 >> (K + 1)) + ly, X1 = (x0 >> (K + 1)) + lx;
+        if (r1.tiles)
+            put_px<T>(p, K + 1, r1, Y1, X1, w);
+        if (scr1)
+            scr1[uint64_t(Y1) * p.W[K + 1] + X1] = w;
+    }
+}
+
+// Levels 3..n_fused of an interior region; level 2 is in lds_b.
+template<typename T, int M, uint32_t RW>
+__device__ __forceinline__ void
+lean_levels(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0, T* lds_a,
+            T* lds_b)
+{
+    const uint32_t n = p.n_fused;
+    if (n < 3)
+        return;
+    __syncthreads();
+    if (n == 3) {
+        lean_level<T, M, 3, RW>(p, f, y0, x0, lds_b, lds_a);
+    } else if (n == 4) {
+        lean_pair<T, M, 3, RW>(p, f, y0, x0, lds_b);
+    } else if (n == 5) {
+        lean_level<T, M, 3, RW>(p, f, y0, x0, lds_b, lds_a);
+        __syncthreads();
+        lean_pair<T, M, 4, RW>(p, f, y0, x0, lds_a);
+    } else {
+        lean_level<T, M, 3, RW>(p, f, y0, x0, lds_b, lds_a);
+        __syncthreads();
+        lean_level<T, M, 4, RW>(p, f, y0, x0, lds_a, lds_b);
+        __syncthreads();
+        lean_pair<T, M, 5, RW>(p, f, y0, x0, lds_b);
+    }
+}
+
 // Edge regions (or layouts the fast path does not cover): every access
 // bounds-checked, columns and rows clamped for the edge replication of
 // scale_image (downsampler.cpp:187-196); level 1 -> lds_a, level 2 -> lds_b.
@@ -616,7 +730,7 @@ fast_pass(const FusedParams& p, uint32_t pass, const uint4& ra, const uint4& rb,
 #pragma unroll
     for (int i = 0; i < HV; ++i)
         o[i] = reduce4<M, T>(r0[2 * i], r0[2 * i + 1], r1[2 * i], r1[2 * i + 1]);
-    if (t1.p) {
+    if (t1.p && !(p.knobs & 4u)) {
         store_vec<T, HV>(t1.p + uint64_t(pass * 8 + rp) * trow, o);
         t1.nz |= any_nonzero<T, HV>(o);
     }
@@ -637,7 +751,7 @@ fast_pass(const FusedParams& p, uint32_t pass, const uint4& ra, const uint4& rb,
 #pragma unroll
             for (int j = 0; j < QV; ++j)
                 q[j] = reduce4<M, T>(o[2 * j], o[2 * j + 1], b[2 * j], b[2 * j + 1]);
-            if (t2.p) {
+            if (t2.p && !(p.knobs & 8u)) {
                 store_vec<T, QV>(t2.p + uint64_t(row2) * trow, q);
                 t2.nz |= any_nonzero<T, QV>(q);
             }
@@ -665,9 +779,14 @@ fast_pass(const FusedParams& p, uint32_t pass, const uint4& ra, const uint4& rb,
     }
 }
 
-// Interior regions: persistent grid-stride loop over (region, pass) units
-// with the next unit's rows prefetched while the current one is stored and
-// reduced.  Region r of [0, n_frames * nby_in * nbx_in).
+// Interior regions, one per workgroup (region r of n_frames * nby_in * nbx_in).
+// The rows of up to kPassBatch passes are loaded before any is reduced, so a
+// wave keeps its whole region in flight; then level 0 goes to its tiles,
+// levels 1-2 are formed in registers, and levels >= 3 in LDS.  Not a
+// persistent loop: a grid-stride loop lets the compiler keep every
+// cascade invariant live across the row passes, which costs occupancy.
+constexpr uint32_t kPassBatch = 4;
+
 template<typename T, int M>
 __global__ __launch_bounds__(256) void
 fused_pyramid(const FusedParams p)
@@ -677,72 +796,41 @@ fused_pyramid(const FusedParams p)
     __shared__ __attribute__((aligned(16))) T lds_a[(kMaxRegionRows / 2) * (RW / 2)];
     __shared__ __attribute__((aligned(16))) T lds_b[(kMaxRegionRows / 4) * (RW / 4)];
 
-    const uint32_t total = p.n_frames * p.nbx_in * p.nby_in;
+    const uint32_t r = blockIdx.x;
+    const uint32_t f = fdiv(r, p.d_nreg_in);
+    const uint32_t q = r - f * (p.nbx_in * p.nby_in);
+    const uint32_t by = fdiv(q, p.d_nbx_in);
+    const uint32_t y0 = by << p.rh_log2;
+    const uint32_t x0 = (q - by * p.nbx_in) * RW;
     const uint32_t npass = 1u << (p.rh_log2 - 4);
     const uint32_t cv = threadIdx.x & 31;
 
-    auto decode = [&](uint32_t r, uint32_t& f, uint32_t& y0, uint32_t& x0) {
-        f = fdiv(r, p.d_nreg_in);
-        const uint32_t q = r - f * (p.nbx_in * p.nby_in);
-        const uint32_t by = fdiv(q, p.d_nbx_in);
-        y0 = by << p.rh_log2;
-        x0 = (q - by * p.nbx_in) * RW;
-    };
-
-    uint32_t r = blockIdx.x;
-    if (r >= total)
-        return;
-    uint32_t pass = 0, f, y0, x0;
-    decode(r, f, y0, x0);
-    uint4 ca, cb;
-    load_pass(p, f, y0, x0, 0, sizeof(T), ca, cb);
-    FastTile t0{}, t1{}, t2{};
+    FastTile t0 = fast_tile<T>(p, 0, f, y0, x0 + cv * VEC);
+    FastTile t1{}, t2{};
+    if (p.n_fused >= 1)
+        t1 = fast_tile<T>(p, 1, f, y0 >> 1, (x0 >> 1) + cv * (VEC / 2));
+    if (p.n_fused >= 2)
+        t2 = fast_tile<T>(p, 2, f, y0 >> 2,
+                          (x0 >> 2) + (VEC >= 4 ? cv * (VEC / 4) : (cv >> 1)));
     T* lds_l2 = p.n_fused >= 3 ? lds_b : nullptr;
 
-    while (true) {
-        if (pass == 0) {
-            t0 = fast_tile<T>(p, 0, f, y0, x0 + cv * VEC);
-            if (p.n_fused >= 1)
-                t1 = fast_tile<T>(p, 1, f, y0 >> 1, (x0 >> 1) + cv * (VEC / 2));
-            if (p.n_fused >= 2)
-                t2 = fast_tile<T>(p, 2, f, y0 >> 2,
-                                  (x0 >> 2) + (VEC >= 4 ? cv * (VEC / 4) : (cv >> 1)));
-        }
-        // prefetch the next pass (of this region or of the next one)
-        uint32_t rn = r, pn = pass + 1, fn = f, yn = y0, xn = x0;
-        if (pn == npass) {
-            rn = r + gridDim.x;
-            pn = 0;
-            if (rn < total)
-                decode(rn, fn, yn, xn);
-        }
-        const bool more = rn < total;
-        uint4 na{}, nb{};
-        if (more)
-            load_pass(p, fn, yn, xn, pn, sizeof(T), na, nb);
-
-        fast_pass<T, M, RW>(p, pass, ca, cb, t0, t1, t2, lds_l2);
-
-        if (pass == npass - 1) {
-            flush_tile_flag(t0);
-            flush_tile_flag(t1);
-            flush_tile_flag(t2);
-            if (p.n_fused >= 3) {
-                deep_levels<T, M, RW>(p, f, y0, x0, lds_a, lds_b);
-                if (more || (p.knobs & 2u))
-                    __syncthreads(); // LDS is reused by the next region
-            }
-        }
-        if (!more)
-            break;
-        ca = na;
-        cb = nb;
-        r = rn;
-        pass = pn;
-        f = fn;
-        y0 = yn;
-        x0 = xn;
+    for (uint32_t p0 = 0; p0 < npass; p0 += kPassBatch) {
+        uint4 ra[kPassBatch], rb[kPassBatch];
+#pragma unroll
+        for (uint32_t i = 0; i < kPassBatch; ++i) // passes past npass re-read the last
+            load_pass(p, f, y0, x0, min(p0 + i, npass - 1), sizeof(T), ra[i], rb[i]);
+#pragma unroll
+        for (uint32_t i = 0; i < kPassBatch; ++i)
+            if (p0 + i < npass)
+                fast_pass<T, M, RW>(p, p0 + i, ra[i], rb[i], t0, t1, t2, lds_l2);
     }
+    if (!(p.knobs & 32u)) {
+        flush_tile_flag(t0);
+        flush_tile_flag(t1);
+        flush_tile_flag(t2);
+    }
+    if (!(p.knobs & 16u))
+        lean_levels<T, M, RW>(p, f, y0, x0, lds_a, lds_b);
 }
 
 // Edge regions (right column strip, bottom row strip; or every region when
@@ -1114,31 +1202,10 @@ launch_fused_pyramid(int dtype, int method, const FusedParams& p,
       uint64_t(p.n_frames) * (uint64_t(p.nbx) * p.nby - uint64_t(p.nbx_in) * p.nby_in);
     if (interior > 0x7fffffffull || edge > 0x7fffffffull)
         return hipErrorInvalidValue;
-    // persistent grid: as many workgroups as are resident
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
-                                  dev) != hipSuccess || cus <= 0)
-            cus = 256;
-    }
-    static int occ[10][4] = {};
 #define CALL(T, MM)                                                            \
     do {                                                                       \
         if (interior) {                                                        \
-            int& o = occ[dtype][MM];                                           \
-            if (o == 0 &&                                                      \
-                (hipOccupancyMaxActiveBlocksPerMultiprocessor(                 \
-                   &o, fused_pyramid<T, MM>, 256, 0) != hipSuccess ||          \
-                 o <= 0))                                                      \
-                o = 4;                                                         \
-            /* default: one region per workgroup (measured faster than a   \
-               persistent grid, which ends on an uneven tail) */           \
-            const uint64_t cap = p.blocks_per_cu                               \
-                                   ? uint64_t(cus) * p.blocks_per_cu           \
-                                   : interior + 0 * uint64_t(o);               \
-            const uint32_t blocks = uint32_t(interior < cap ? interior : cap); \
+            const uint32_t blocks = uint32_t(interior);                        \
             hipLaunchKernelGGL((fused_pyramid<T, MM>), dim3(blocks), dim3(256),\
                                0, stream, p);                                  \
         }                                                                      \

@@ -85,7 +85,6 @@ struct FusedParams
     uint32_t nbx_in, nby_in; // interior (fast-path) regions along x / y
     uint32_t vec_rows;       // 1: every row start is 16-B aligned
     uint32_t fast_ok;        // 1: tiles fit the interior fast path
-    uint32_t blocks_per_cu;  // persistent grid size (0 = occupancy)
     uint32_t nt;             // bit0: non-temporal input loads, bit1: nt level-0 stores
     uint32_t knobs;          // tuning A/B switches (0 = shipped defaults)
     uint32_t G;              // 2x2x2 kernel: level-0 planes per group

@@ -202,8 +202,8 @@ typedef struct
                                   halving XY until this many levels exist. */
     int32_t skip_level0_split; /* 1 = do not tile-split level 0 (pyramid
                                   only); default 0 = full stage */
-    uint32_t blocks_per_cu;    /* persistent-grid workgroups per CU of the
-                                  fused kernel (0 = occupancy limit) */
+    uint32_t blocks_per_cu;    /* reserved, ignored: the fused kernels run
+                                  one region per workgroup */
     uint64_t first_frame;      /* level-0 frame id of this stage's first
                                   frame (z-slab sharding across GPUs: the
                                   slab's first plane); level k starts at
