@@ -24,7 +24,7 @@ LIB_PATH = os.path.join(PKG_DIR, "libaqz_gpu.so")
 UINT8, UINT16, UINT32, UINT64, INT8, INT16, INT32, INT64, FLOAT32, FLOAT64 = range(10)
 DECIMATE, MEAN, MIN, MAX = range(4)
 SPACE, CHANNEL, TIME, OTHER = range(4)
-MEM_HOST, MEM_DEVICE = 0, 1
+MEM_HOST, MEM_DEVICE, MEM_HOST_PINNED = 0, 1, 2
 
 NP_DTYPES = {UINT8: np.uint8, UINT16: np.uint16, UINT32: np.uint32,
              UINT64: np.uint64, INT8: np.int8, INT16: np.int16,
@@ -146,6 +146,10 @@ def lib():
         "aqz_stage_synchronize": ([vp], i32),
         "aqz_stage_frames_written": ([vp, u32], u64),
         "aqz_stage_copy_layer": ([vp, u32, u64, vp, sz, vp, sz, i32], i32),
+        "aqz_stage_copy_layer_async": ([vp, u32, u64, vp, sz, vp, sz], i32),
+        "aqz_stage_wait_copies": ([vp], i32),
+        "aqz_host_alloc": ([sz, C.POINTER(vp)], i32),
+        "aqz_host_free": ([vp], None),
         "aqz_stage_device_layer": ([vp, u32, u64, C.POINTER(vp), C.POINTER(vp)], i32),
         "aqz_stage_finalize": ([vp], i32),
         "aqz_stage_enable_kernel_timing": ([vp, i32], i32),
@@ -264,8 +268,36 @@ def _desc(dims, dtype, method, max_levels, multiscale, storage_order, device):
     return d, keep
 
 
+class HostBuffer:
+    """Page-locked host memory (aqz_host_alloc) with a numpy view; frames in
+    it are appended with MEM_HOST_PINNED (no staging copy) and hand-off
+    copies into it overlap the kernels."""
+
+    def __init__(self, nbytes):
+        p = C.c_void_p()
+        _check(lib().aqz_host_alloc(nbytes, C.byref(p)), "aqz_host_alloc")
+        self.ptr = p.value
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(self.ptr))
+
+    def view(self, dtype=np.uint8, shape=None):
+        a = self.array.view(dtype)
+        return a.reshape(shape) if shape is not None else a
+
+    def close(self):
+        if getattr(self, "ptr", None) and _lib is not None:
+            self.array = None
+            _lib.aqz_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.close()
+
+
 def _ptr(buf):
     """(pointer, mem kind) for numpy arrays / torch tensors / raw ints."""
+    if isinstance(buf, HostBuffer):
+        return buf.ptr, MEM_HOST_PINNED
     if isinstance(buf, np.ndarray):
         assert buf.flags.c_contiguous
         return buf.ctypes.data, MEM_HOST
@@ -401,6 +433,16 @@ class Stage:
                                           nbytes, flags.ctypes.data, flags.size,
                                           MEM_HOST), "copy_layer")
         return out, flags
+
+    def copy_layer_async(self, level, layer, dst_ptr, cap, has_data_ptr=None,
+                         has_data_cap=0):
+        """Enqueue the D2H hand-off of a resident layer (returns at once)."""
+        _check(lib().aqz_stage_copy_layer_async(self.h, level, layer, dst_ptr, cap,
+                                                has_data_ptr, has_data_cap),
+               "copy_layer_async")
+
+    def wait_copies(self):
+        _check(lib().aqz_stage_wait_copies(self.h), "wait_copies")
 
     def finalize(self):
         _check(lib().aqz_stage_finalize(self.h), "finalize")

@@ -460,7 +460,11 @@ aqz_status
 aqz_stage_append(aqz_stage* st, const void* frames, uint64_t n_frames,
                  int32_t mem)
 {
-    return guard_sticky(st, [&] { st->st->append(frames, n_frames, mem); });
+    return guard_sticky(st, [&] {
+        if (mem != AQZ_MEM_HOST && mem != AQZ_MEM_DEVICE && mem != AQZ_MEM_HOST_PINNED)
+            throw aqz::Error(AQZ_STATUS_INVALID_ARGUMENT, "unknown memory kind");
+        st->st->append(frames, n_frames, mem);
+    });
 }
 
 aqz_status
@@ -485,6 +489,39 @@ aqz_stage_copy_layer(aqz_stage* st, uint32_t level, uint64_t layer, void* dst,
     return guard_sticky(st, [&] {
         st->st->copy_layer(level, layer, dst, cap, has_data, has_data_cap, mem);
     });
+}
+
+aqz_status
+aqz_stage_copy_layer_async(aqz_stage* st, uint32_t level, uint64_t layer, void* dst,
+                           size_t cap, uint8_t* has_data, size_t has_data_cap)
+{
+    return guard_sticky(st, [&] {
+        st->st->copy_layer_async(level, layer, dst, cap, has_data, has_data_cap);
+    });
+}
+
+aqz_status
+aqz_stage_wait_copies(aqz_stage* st)
+{
+    return guard_sticky(st, [&] { st->st->wait_copies(); });
+}
+
+aqz_status
+aqz_host_alloc(size_t bytes, void** out)
+{
+    if (!out || bytes == 0)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    *out = nullptr;
+    return hipHostMalloc(out, bytes, hipHostMallocDefault) == hipSuccess
+             ? AQZ_STATUS_SUCCESS
+             : AQZ_STATUS_OUT_OF_MEMORY;
+}
+
+void
+aqz_host_free(void* p)
+{
+    if (p)
+        (void)hipHostFree(p);
 }
 
 aqz_status

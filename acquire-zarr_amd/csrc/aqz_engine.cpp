@@ -5,11 +5,13 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 namespace aqz {
 
 
 constexpr int kMemDevice = 1;
+constexpr int kMemHostPinned = 2;
 
 void
 hip_check(hipError_t e, const char* what)
@@ -87,6 +89,16 @@ PinnedBuf::alloc(size_t bytes)
     hip_check(hipHostMalloc(&q, bytes, hipHostMallocDefault), "hipHostMalloc");
     p = static_cast<uint8_t*>(q);
     n = bytes;
+}
+
+// host threads for the pageable -> pinned staging copy (AQZ_COPY_THREADS)
+static unsigned
+copy_workers()
+{
+    if (const char* s = std::getenv("AQZ_COPY_THREADS"))
+        return unsigned(std::max(0, std::atoi(s)));
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    return std::min(7u, hw / 2);
 }
 
 static hipMemcpyKind
@@ -292,12 +304,30 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         }
     }
     pend_.resize(lv_.size());
-    for (auto& e : stage_ev_)
-        hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming),
+    for (int j = 0; j < 2; ++j) {
+        hip_check(hipEventCreateWithFlags(&h2d_ev_[j], hipEventDisableTiming),
                   "hipEventCreate");
-    for (auto& L : lv_)
+        hip_check(hipEventCreateWithFlags(&consume_ev_[j], hipEventDisableTiming),
+                  "hipEventCreate");
+    }
+    hip_check(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking), "hipStreamCreate");
+    hip_check(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking), "hipStreamCreate");
+    for (auto& L : lv_) {
         hip_check(hipEventCreateWithFlags(&L.ops_ev, hipEventDisableTiming),
                   "hipEventCreate");
+        if (!L.ring.p)
+            continue;
+        L.ready_ev.assign(L.n_slots, nullptr);
+        L.copy_ev.assign(L.n_slots, nullptr);
+        L.copy_pending.assign(L.n_slots, 0);
+        for (uint32_t s = 0; s < L.n_slots; ++s) {
+            hip_check(hipEventCreateWithFlags(&L.ready_ev[s], hipEventDisableTiming),
+                      "hipEventCreate");
+            hip_check(hipEventCreateWithFlags(&L.copy_ev[s], hipEventDisableTiming),
+                      "hipEventCreate");
+        }
+        L.flag_bytes.alloc(size_t(L.n_slots) * L.n_chunks);
+    }
 
     hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
@@ -306,12 +336,25 @@ Stage::~Stage()
 {
     if (stream_)
         (void)hipStreamSynchronize(stream_);
-    for (auto& e : stage_ev_)
-        if (e)
-            (void)hipEventDestroy(e);
-    for (auto& L : lv_)
+    for (hipStream_t s : { h2d_, d2h_ })
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
+    for (int j = 0; j < 2; ++j)
+        for (hipEvent_t e : { h2d_ev_[j], consume_ev_[j] })
+            if (e)
+                (void)hipEventDestroy(e);
+    for (auto& L : lv_) {
         if (L.ops_ev)
             (void)hipEventDestroy(L.ops_ev);
+        for (hipEvent_t e : L.ready_ev)
+            if (e)
+                (void)hipEventDestroy(e);
+        for (hipEvent_t e : L.copy_ev)
+            if (e)
+                (void)hipEventDestroy(e);
+    }
 
     for (auto& pr : ev_pairs_) {
         (void)hipEventDestroy(pr.first);
@@ -359,7 +402,15 @@ Stage::frames_written(uint32_t level) const
 void
 Stage::synchronize()
 {
+    hip_check(hipStreamSynchronize(h2d_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    hip_check(hipStreamSynchronize(d2h_), "hipStreamSynchronize");
+}
+
+void
+Stage::wait_copies()
+{
+    hip_check(hipStreamSynchronize(d2h_), "hipStreamSynchronize");
 }
 
 void
@@ -383,19 +434,37 @@ Stage::append(const void* frames, uint64_t n_frames, int mem)
         if (mem == kMemDevice) {
             run_batch(p, b);
         } else {
-            // pinned double buffer: the copy of batch i+1 overlaps batch i
+            // Double buffer: batch i+1's host copy and H2D (on h2d_) overlap
+            // batch i's kernels.  A pageable source is first copied into the
+            // pinned staging buffer (the one copy ZarrStream_append makes,
+            // frame.queue.cpp:37-39); a pinned source is DMA'd directly and
+            // append waits for that DMA so the caller may reuse its buffer.
             const int j = stage_idx_;
             stage_idx_ ^= 1;
-            h_stage_[j].alloc(size_t(B) * fbytes);
+            const size_t nbytes = size_t(b) * fbytes;
             d_stage_[j].alloc(size_t(B) * fbytes);
-            hip_check(hipEventSynchronize(stage_ev_[j]), "hipEventSynchronize");
-            std::memcpy(h_stage_[j].p, p, size_t(b) * fbytes);
-            hip_check(hipMemcpyAsync(d_stage_[j].p, h_stage_[j].p,
-                                     size_t(b) * fbytes, hipMemcpyHostToDevice,
-                                     stream_),
+            const uint8_t* hsrc = p;
+            if (mem != kMemHostPinned) {
+                h_stage_[j].alloc(size_t(B) * fbytes);
+                hip_check(hipEventSynchronize(h2d_ev_[j]), "hipEventSynchronize");
+                if (!pool_)
+                    pool_ = std::make_unique<CopyPool>(copy_workers());
+                pool_->copy(h_stage_[j].p, p, nbytes);
+                hsrc = h_stage_[j].p;
+            }
+            if (consume_rec_[j]) // kernels of the batch before last read d_stage_[j]
+                hip_check(hipStreamWaitEvent(h2d_, consume_ev_[j], 0),
+                          "hipStreamWaitEvent");
+            hip_check(hipMemcpyAsync(d_stage_[j].p, hsrc, nbytes,
+                                     hipMemcpyHostToDevice, h2d_),
                       "hipMemcpyAsync");
-            hip_check(hipEventRecord(stage_ev_[j], stream_), "hipEventRecord");
+            hip_check(hipEventRecord(h2d_ev_[j], h2d_), "hipEventRecord");
+            hip_check(hipStreamWaitEvent(stream_, h2d_ev_[j], 0), "hipStreamWaitEvent");
             run_batch(d_stage_[j].p, b);
+            hip_check(hipEventRecord(consume_ev_[j], stream_), "hipEventRecord");
+            consume_rec_[j] = true;
+            if (mem == kMemHostPinned)
+                hip_check(hipEventSynchronize(h2d_ev_[j]), "hipEventSynchronize");
         }
         done += b;
     }
@@ -465,8 +534,14 @@ void
 Stage::enter_layer(StageLevel& L, uint64_t layer)
 {
     // A fresh layer needs no clearing: has_data words are generation-tagged
-    // and the chunk padding was zeroed at allocation.
-    L.slot_layer[layer % L.n_slots] = int64_t(layer);
+    // and the chunk padding was zeroed at allocation.  A hand-off copy still
+    // reading the slot must finish before the slot is written again.
+    const uint32_t slot = uint32_t(layer % L.n_slots);
+    if (!L.copy_pending.empty() && L.copy_pending[slot]) {
+        hip_check(hipStreamWaitEvent(stream_, L.copy_ev[slot], 0), "hipStreamWaitEvent");
+        L.copy_pending[slot] = 0;
+    }
+    L.slot_layer[slot] = int64_t(layer);
 }
 
 void
@@ -827,6 +902,42 @@ Stage::copy_layer(uint32_t level, uint64_t layer, void* dst, size_t cap,
         for (uint32_t c = 0; c < L.n_chunks; ++c)
             has_data[c] = f[c] == tag ? 1 : 0;
     }
+}
+
+void
+Stage::copy_layer_async(uint32_t level, uint64_t layer, void* dst, size_t cap,
+                        uint8_t* has_data, size_t has_data_cap)
+{
+    if (level >= lv_.size())
+        throw Error(3, "level out of range");
+    StageLevel& L = lv_[level];
+    if (!L.ring.p)
+        throw Error(1, "level 0 split disabled for this stage");
+    const uint32_t slot = uint32_t(layer % L.n_slots);
+    if (L.slot_layer[slot] != int64_t(layer))
+        throw Error(3, "chunk layer not resident");
+    if (dst && cap < L.slot_bytes)
+        throw Error(2, "destination too small for a chunk layer");
+    if (has_data && has_data_cap < L.n_chunks)
+        throw Error(2, "has_data too small");
+    // after every kernel enqueued so far; the slot's next layer waits for it
+    hip_check(hipEventRecord(L.ready_ev[slot], stream_), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(d2h_, L.ready_ev[slot], 0), "hipStreamWaitEvent");
+    if (dst)
+        hip_check(hipMemcpyAsync(dst, L.ring.p + slot * L.slot_bytes, L.slot_bytes,
+                                 hipMemcpyDefault, d2h_),
+                  "hipMemcpyAsync");
+    if (has_data) {
+        uint8_t* fb = L.flag_bytes.p + size_t(slot) * L.n_chunks;
+        hip_check(launch_flags_to_bytes(
+                    reinterpret_cast<const uint32_t*>(L.flags.p) + size_t(slot) * L.n_chunks,
+                    fb, L.n_chunks, uint32_t(layer / L.n_slots + 1), d2h_),
+                  "flags launch");
+        hip_check(hipMemcpyAsync(has_data, fb, L.n_chunks, hipMemcpyDefault, d2h_),
+                  "hipMemcpyAsync");
+    }
+    hip_check(hipEventRecord(L.copy_ev[slot], d2h_), "hipEventRecord");
+    L.copy_pending[slot] = 1;
 }
 
 void

@@ -8,6 +8,7 @@
 //                     same add_frame/take_frame contract.
 #pragma once
 
+#include "aqz_copy.hh"
 #include "aqz_geometry.hh"
 #include "aqz_params.hh"
 
@@ -25,6 +26,8 @@ hipError_t launch_level(int dtype, int method, const LevelParams& p,
                         hipStream_t stream);
 hipError_t launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
                                    hipStream_t stream);
+hipError_t launch_flags_to_bytes(const uint32_t* flags, uint8_t* out, uint32_t n,
+                                 uint32_t tag, hipStream_t stream);
 hipError_t launch_zero_frame_tiles(uint8_t* fb, uint64_t bpc,
                                    uint32_t n_tiles, uint32_t tile_bytes,
                                    hipStream_t stream);
@@ -119,6 +122,11 @@ struct StageLevel
     DevBuf d_ops;
     PinnedBuf h_ops;
     hipEvent_t ops_ev = nullptr;
+    // asynchronous hand-off of chunk layers (copy_layer_async): one D2H per
+    // ring slot in flight; the slot's next layer waits for it
+    std::vector<hipEvent_t> ready_ev, copy_ev;
+    std::vector<uint8_t> copy_pending;
+    DevBuf flag_bytes;                     // per slot: has_data as 0/1 bytes
 };
 
 class Stage
@@ -138,6 +146,9 @@ class Stage
                     uint8_t* has_data, size_t has_data_cap, int mem);
     void device_layer(uint32_t level, uint64_t layer, void** chunks,
                       uint32_t** flags);
+    void copy_layer_async(uint32_t level, uint64_t layer, void* dst, size_t cap,
+                          uint8_t* has_data, size_t has_data_cap);
+    void wait_copies();
     void finalize();
     void enable_timing(bool on);
     void timing(double* total_ms, uint64_t* launches);
@@ -179,11 +190,17 @@ class Stage
     uint64_t max_frames_ = 0; // 0 = unbounded
     hipStream_t own_stream_ = nullptr;
     hipStream_t stream_ = nullptr;
-    // host-source staging: pinned double buffer -> device double buffer
+    // host-source staging: pinned double buffer -> device double buffer.
+    // H2D runs on h2d_ (batch i+1's copy overlaps batch i's kernels), layer
+    // hand-off D2H on d2h_; events order them against stream_.
     PinnedBuf h_stage_[2];
     DevBuf d_stage_[2];
-    hipEvent_t stage_ev_[2] = { nullptr, nullptr };
+    hipEvent_t h2d_ev_[2] = { nullptr, nullptr };     // H2D of buffer j done
+    hipEvent_t consume_ev_[2] = { nullptr, nullptr }; // kernels read buffer j
+    bool consume_rec_[2] = { false, false };
     int stage_idx_ = 0;
+    hipStream_t h2d_ = nullptr, d2h_ = nullptr;
+    std::unique_ptr<CopyPool> pool_;
     uint32_t nt_mode_ = 0;           // non-temporal load/store bits
     uint32_t knobs_ = 0;             // tuning A/B switches
     std::vector<Pending> pend_;

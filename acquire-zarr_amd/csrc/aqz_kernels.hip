@@ -1263,6 +1263,28 @@ launch_level(int dtype, int method, const LevelParams& p, hipStream_t stream)
     return hipGetLastError();
 }
 
+// has_data of one chunk layer as 0/1 bytes: a chunk holds data of this layer
+// when its word carries the layer's generation tag (Chunk::has_data,
+// chunk.cpp:17-67)
+__global__ void
+flags_to_bytes(const uint32_t* flags, uint8_t* out, uint32_t n, uint32_t tag)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        out[i] = flags[i] == tag ? 1 : 0;
+}
+
+hipError_t
+launch_flags_to_bytes(const uint32_t* flags, uint8_t* out, uint32_t n, uint32_t tag,
+                      hipStream_t stream)
+{
+    if (n == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(flags_to_bytes, dim3((n + 255) / 256), dim3(256), 0, stream,
+                       flags, out, n, tag);
+    return hipGetLastError();
+}
+
 hipError_t
 launch_zero_frame_tiles(uint8_t* fb, uint64_t bpc, uint32_t n_tiles,
                         uint32_t tile_bytes, hipStream_t stream)

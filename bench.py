@@ -49,9 +49,10 @@ CONFIGS = {
                         "device-resident",
                dims=[(TIME, 0, 32, 1), (SPACE, 4096, 128, 1), (SPACE, 4096, 128, 1)],
                dtype=U8, method=MEAN, force_levels=0, batch=32, ring=160),
-    # BASELINE configs[3] on one GPU: a 256-plane volume, 2x2x2 pyramid
-    # (z 256->128->64->64, xy 2048->1024->512->256); z-slab sharded over
-    # ranks with --gpus N (every rank owns 256/N planes of the volume).
+    # BASELINE configs[3]: a 256-plane volume, 2x2x2 pyramid (z 256->128->
+    # 64->64, xy 2048->1024->512->256).  With --gpus N rank r's stream starts
+    # at its z slab (first_frame = r * 256/N, aligned to the 4-plane z
+    # groups) and runs on from there: one independent stream per GPU.
     "c4": dict(workload="uint16 2048x2048x256 light-sheet volume, 4-level 3-D (2x2x2) "
                         "pyramid, 256x256x64 chunks, mean, device-resident",
                dims=[(TIME, 0, 1, 1), (SPACE, 256, 64, 1), (SPACE, 2048, 256, 1),
@@ -81,6 +82,23 @@ def fill_ring(torch, ring, dtype, seed):
         ring.view(torch.uint8).random_(0, 256, generator=g)
     else:
         ring.view(torch.float32).uniform_(0.0, 65535.0, generator=g)
+
+
+def pmc_traffic(config, pyramid_only, kernel):
+    """Per-launch HBM bytes of the dominant kernel from the newest committed
+    rocprofv3 PMC summary for this configuration (tools/profile.sh ->
+    tools/pmc_summary.py -> profiles/<round>_<config>_pmc.json: FETCH_SIZE x2
+    + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md).  PMC
+    counters cannot be read inside a plain run, so the value is the profiled
+    run of this same command; None when no summary matches."""
+    import glob
+    name = config + ("-pyr" if pyramid_only else "")
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{name}_pmc.json")))
+    for f in reversed(files):
+        d = json.load(open(f))
+        if d.get("config") == name and kernel and kernel in d.get("kernel", ""):
+            return d["traffic_bytes_per_launch"], os.path.relpath(f, REPO)
+    return None, None
 
 
 def cpu_baseline(cfg, seconds):
@@ -149,6 +167,84 @@ def cpu_baseline(cfg, seconds):
                       f"every level, single thread"}
 
 
+def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
+    """Host frame buffer -> H2D -> stage -> D2H of every completed chunk layer
+    (the path BASELINE.json asks to be measured end to end).  The source is a
+    2-batch ring of host frames; layers land in a per-level ring of pinned
+    buffers (no consumer: the sink is out of scope).  Timed from the first
+    append to the last hand-off copy."""
+    dt, B, bpp = cfg["dtype"], cfg["batch"], BPP[cfg["dtype"]]
+    st = aqz.Stage(cfg["dims"], dt, cfg["method"], force_levels=cfg["force_levels"],
+                   max_batch_frames=B, layer_slots=2, device=dev.index)
+    L = st.n_levels()
+    sizes = level_sizes(st)
+    fbytes = sizes[0][0] * sizes[0][1] * bpp
+    lay = [st.layout(l) for l in range(L)]
+    lbytes = [x["bytes_per_chunk"] * x["chunks_per_layer"] for x in lay]
+    src_frames = 2 * B
+    if args.e2e == "pinned":
+        src = aqz.HostBuffer(src_frames * fbytes)
+        src_arr, src_ptr, mem = src.array, src.ptr, aqz.MEM_HOST_PINNED
+    else:
+        src_arr = np.empty(src_frames * fbytes, dtype=np.uint8)
+        src_ptr, mem = src_arr.ctypes.data, aqz.MEM_HOST
+    rng = np.random.default_rng(7 + rank)
+    src_arr[...] = rng.integers(0, 256, size=src_arr.size, dtype=np.uint8)
+    dst = [[aqz.HostBuffer(lbytes[l]) for _ in range(4)] for l in range(L)]
+    hd = [[aqz.HostBuffer(lay[l]["chunks_per_layer"]) for _ in range(4)] for l in range(L)]
+    handed = [0] * L
+    d2h = [0]
+
+    def hand_off():
+        for l in range(L):
+            done = st.frames_written(l) // lay[l]["frames_per_layer"]
+            while handed[l] < done:
+                i = handed[l] % 4
+                st.copy_layer_async(l, handed[l], dst[l][i].ptr, lbytes[l], hd[l][i].ptr,
+                                    hd[l][i].nbytes)
+                d2h[0] += lbytes[l]
+                handed[l] += 1
+
+    def step(s):
+        st.append_ptr(src_ptr + (s % 2) * B * fbytes, B, mem)
+        hand_off()
+
+    for s in range(args.warmup):
+        step(s)
+    st.synchronize()
+    if dist:
+        dist.barrier()
+    d2h[0] = 0
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(args.warmup + s)
+    st.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    st.close()
+    in_bytes = args.steps * B * fbytes
+    return {
+        "metric": "end-to-end input GB/s, host frames -> H2D -> multiscale stage -> "
+                  "D2H of every chunk layer",
+        "value": round(world * in_bytes / el / 1e9, 3), "unit": "GB/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el * 1e3 / args.steps, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": {U8: "u8", U16: "u16", F32: "f32"}[dt],
+        "data": f"synthetic, host {args.e2e} source ring of {src_frames} frames",
+        "config": {"workload": cfg["workload"].replace("device-resident", "host-resident") +
+                   f" [e2e, {args.e2e} source]", "frames_per_step_per_gpu": B,
+                   "levels": L},
+        "h2d_gbs_per_gpu": round(in_bytes / el / 1e9, 3),
+        "d2h_gbs_per_gpu": round(d2h[0] / el / 1e9, 3),
+        "frames_per_s_per_gpu": round(args.steps * B / el, 1),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -159,6 +255,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pyramid-only", action="store_true",
                     help="skip the level-0 tile split (downsample levels only)")
+    ap.add_argument("--no-pyramid-only-line", action="store_true",
+                    help="do not add the pyramid-only side measurement")
+    ap.add_argument("--e2e", choices=["pinned", "pageable"], default=None,
+                    help="end-to-end mode: frames start in host memory (pinned or "
+                         "pageable), every completed chunk layer is handed back to "
+                         "pinned host buffers (DESIGN.md 'End to end')")
     args = ap.parse_args()
 
     import torch
@@ -178,52 +280,78 @@ def main():
     cfg = CONFIGS[args.config]
     dt = cfg["dtype"]
     B = cfg["batch"]
-    st = aqz.Stage(cfg["dims"], dt, cfg["method"], force_levels=cfg["force_levels"],
-                   max_batch_frames=B, layer_slots=2, device=dev.index,
-                   skip_level0_split=args.pyramid_only)
-    stream = torch.cuda.current_stream(dev)
-    st.set_stream(stream.cuda_stream)
-    sizes = level_sizes(st)
-    H, W = sizes[0]
     bpp = BPP[dt]
-    fbytes = H * W * bpp
-    ring_frames = cfg["ring"]
-    ring = torch.empty(ring_frames * fbytes, dtype=torch.uint8, device=dev)
-    fill_ring(torch, ring, dt, 1234 + rank)
-    nb = ring_frames // B
-    base = ring.data_ptr()
+    first = 0
+    if args.config == "c4" and world > 1:
+        from aqz.dist import z_levels, z_slab
+        planes = [lv[1][1] for lv in aqz.pyramid_levels(cfg["dims"])]
+        first = z_slab(planes[0], world, rank, 1 << z_levels(planes))[0]
 
-    def step(s):
-        st.append_ptr(base + (s % nb) * B * fbytes, B)
+    def run(pyramid_only, steps, warmup):
+        """Time `steps` launches of B frames (after `warmup`) between
+        barrier + device sync on both sides; max over ranks."""
+        st = aqz.Stage(cfg["dims"], dt, cfg["method"], force_levels=cfg["force_levels"],
+                       max_batch_frames=B, layer_slots=2, device=dev.index,
+                       skip_level0_split=pyramid_only, first_frame=first)
+        st.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        sizes = level_sizes(st)
+        fbytes = sizes[0][0] * sizes[0][1] * bpp
+        ring_frames = cfg["ring"]
+        ring = torch.empty(ring_frames * fbytes, dtype=torch.uint8, device=dev)
+        fill_ring(torch, ring, dt, 1234 + rank)
+        nb = ring_frames // B
+        base = ring.data_ptr()
 
-    for s in range(args.warmup):
-        step(s)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    st.enable_kernel_timing(True)
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        step(args.warmup + s)
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    if dist:
-        dist.barrier()
-    elapsed = t1 - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    kms, launches = st.kernel_timing()
+        def step(s):
+            st.append_ptr(base + (s % nb) * B * fbytes, B)
 
-    in_bytes = fbytes
-    out_bytes = sum(h * w * bpp for (h, w) in sizes[1:])
-    l0_split = 0 if args.pyramid_only else fbytes
-    alg_per_launch = B * (in_bytes + l0_split + out_bytes)
-    avg_ms = kms / max(1, launches)
-    achieved = alg_per_launch / (avg_ms * 1e-3) / 1e9 if launches else 0.0
-    value = world * args.steps * B * fbytes / elapsed / 1e9
+        for s in range(warmup):
+            step(s)
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        st.enable_kernel_timing(True)
+        t0 = time.perf_counter()
+        for s in range(steps):
+            step(warmup + s)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        if dist:
+            dist.barrier()
+        elapsed = t1 - t0
+        if dist:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        kms, launches = st.kernel_timing()
+        kernel = st.dominant_kernel()
+        st.close()
+        del ring
+        out_bytes = sum(h * w * bpp for (h, w) in sizes[1:])
+        alg = B * (fbytes + (0 if pyramid_only else fbytes) + out_bytes)
+        avg_ms = kms / max(1, launches)
+        return dict(elapsed=elapsed, sizes=sizes, fbytes=fbytes, kernel=kernel,
+                    avg_ms=avg_ms, alg=alg,
+                    achieved=alg / (avg_ms * 1e-3) / 1e9 if launches else 0.0,
+                    value=world * steps * B * fbytes / elapsed / 1e9)
+
+    if args.e2e:
+        res = run_e2e(torch, aqz, dev, cfg, args, world, rank, dist)
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    main_run = run(args.pyramid_only, args.steps, args.warmup)
+    side = None
+    if not args.pyramid_only and not args.no_pyramid_only_line:
+        side = run(True, max(5, args.steps // 2), 2)
+    sizes, elapsed, value = main_run["sizes"], main_run["elapsed"], main_run["value"]
+    kernel, avg_ms, achieved = main_run["kernel"], main_run["avg_ms"], main_run["achieved"]
+    alg_per_launch = main_run["alg"]
+    traffic, traffic_src = pmc_traffic(args.config, args.pyramid_only, kernel)
 
     result = {
         "metric": "input GB/s, device-resident multiscale downsample, uint16 frames @1/2/4/8 GPU",
@@ -246,17 +374,27 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None,
-                     "kernel": st.dominant_kernel(),
+                     "traffic": traffic,
+                     "traffic_unit": "bytes per launch (rocprofv3 PMC)",
+                     "traffic_source": traffic_src,
+                     "kernel": kernel,
                      "kernel_avg_ms": round(avg_ms, 5),
                      "alg_bytes_per_launch": alg_per_launch},
         "input_rate_frac_of_peak": round(value / world / HBM_PEAK_GBS, 4),
     }
+    if side:
+        # the downsample alone (no level-0 tile split): reads each frame once
+        # and writes 1/3 of it; its input rate against the HBM read peak is
+        # the "read roofline" fraction of BASELINE.json's target
+        result["pyramid_only"] = {
+            "value": round(side["value"], 2), "unit": "GB/s",
+            "kernel_avg_ms": round(side["avg_ms"], 5),
+            "achieved": round(side["achieved"], 1),
+            "input_rate_frac_of_peak": round(side["value"] / world / HBM_PEAK_GBS, 4)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    st.close()
     if dist:
         dist.destroy_process_group()
 

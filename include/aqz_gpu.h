@@ -71,8 +71,10 @@ enum
 /* where a frame pointer lives */
 enum
 {
-    AQZ_MEM_HOST = 0,   /* pageable or pinned host memory (H2D copy) */
-    AQZ_MEM_DEVICE = 1  /* already resident in this device's HBM */
+    AQZ_MEM_HOST = 0,        /* pageable host memory (copied to pinned staging) */
+    AQZ_MEM_DEVICE = 1,      /* already resident in this device's HBM */
+    AQZ_MEM_HOST_PINNED = 2  /* page-locked host memory (e.g. aqz_host_alloc):
+                                DMA'd straight to the device */
 };
 
 /* The pixel-geometry subset of ZarrDimensionProperties
@@ -235,7 +237,11 @@ aqz_status aqz_stage_set_stream(aqz_stage* st, void* stream);
 /* Append n_frames full level-0 frames (contiguous, frame after frame).
  * Equivalent to n_frames calls of MultiscaleArray::write_frame.  Device
  * sources are consumed asynchronously (do not modify them until the next
- * aqz_stage_synchronize); host sources are copied before return. */
+ * aqz_stage_synchronize); host sources may be reused when append returns,
+ * as with ZarrStream_append (frame.queue.cpp:37-39): AQZ_MEM_HOST is copied
+ * into a pinned staging buffer by a few host threads, AQZ_MEM_HOST_PINNED is
+ * DMA'd directly.  Either way the H2D runs on the stage's copy stream and
+ * overlaps the previous batch's kernels. */
 aqz_status aqz_stage_append(aqz_stage* st, const void* frames,
                             uint64_t n_frames, int32_t mem);
 aqz_status aqz_stage_synchronize(aqz_stage* st);
@@ -249,6 +255,20 @@ uint64_t aqz_stage_frames_written(const aqz_stage* st, uint32_t level);
 aqz_status aqz_stage_copy_layer(aqz_stage* st, uint32_t level, uint64_t layer,
                                 void* dst, size_t cap, uint8_t* has_data,
                                 size_t has_data_cap, int32_t mem);
+/* Asynchronous hand-off of a resident chunk layer (outputs D2H
+ * straight into host chunk buffers): enqueues, after all work appended so
+ * far, a D2H copy of the layer into dst (pinned memory for a real overlap;
+ * cap >= bytes_per_chunk * chunks_per_layer) and of its has_data bytes into
+ * has_data (NULL to skip), on the stage's hand-off stream.  Returns at once;
+ * the ring slot is not rewritten until the copy has finished.  The copies
+ * are complete after aqz_stage_wait_copies or aqz_stage_synchronize. */
+aqz_status aqz_stage_copy_layer_async(aqz_stage* st, uint32_t level,
+                                      uint64_t layer, void* dst, size_t cap,
+                                      uint8_t* has_data, size_t has_data_cap);
+aqz_status aqz_stage_wait_copies(aqz_stage* st);
+/* Page-locked host memory for frames and hand-off buffers. */
+aqz_status aqz_host_alloc(size_t bytes, void** out);
+void aqz_host_free(void* p);
 /* Device pointers of a resident layer (for device-side consumers).  Chunk c
  * has data iff has_data[c] == layer / layer_slots + 1 (the words carry the
  * ring-slot generation, so they are never cleared). */

@@ -327,3 +327,53 @@ def test_stage_z_slab_sharding(gpu):
     assert b.frames_written(0) == 64 and a.frames_written(0) == 32
     a.close()
     b.close()
+
+
+def test_stage_async_handoff_pinned_and_pageable(gpu):
+    """The ingestion / hand-off pipeline: pinned and pageable (multi-threaded
+    staging copy) host sources, H2D on the copy stream, and every chunk layer
+    handed off with copy_layer_async while the 3-slot ring wraps several
+    times -- the copies must see each layer whole (a slot is not rewritten
+    before its D2H has finished)."""
+    dims = [(TIME, 0, 2, 1), (SPACE, 1024, 128, 1), (SPACE, 1024, 128, 1)]
+    n, B = 20, 4
+    frames = synthetic_frames(U16, n, 1024, 1024, 31)
+    exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
+    st = gpu.Stage(dims, U16, MEAN, layer_slots=2, max_batch_frames=B)
+    L = st.n_levels()
+    lay = [st.layout(l) for l in range(L)]
+    nbytes = [x["bytes_per_chunk"] * x["chunks_per_layer"] for x in lay]
+    pinned_src = gpu.HostBuffer(B * frames[0].nbytes)
+    out, handed = {}, [0] * L
+
+    def hand_off(final=False):
+        for l in range(L):
+            F = lay[l]["frames_per_layer"]
+            done = st.frames_written(l) // F
+            if final and st.frames_written(l) % F:
+                done += 1
+            while handed[l] < done:
+                buf = gpu.HostBuffer(nbytes[l])
+                hd = gpu.HostBuffer(lay[l]["chunks_per_layer"])
+                st.copy_layer_async(l, handed[l], buf.ptr, nbytes[l], hd.ptr, hd.nbytes)
+                out[(l, handed[l])] = (buf, hd)
+                handed[l] += 1
+
+    for i, b0 in enumerate(range(0, n, B)):
+        chunk = np.ascontiguousarray(frames[b0:b0 + B])
+        if i % 2 == 0:
+            pinned_src.view(np.uint16, chunk.shape)[...] = chunk
+            st.append(pinned_src, len(chunk))
+            pinned_src.view(np.uint16)[...] = 0  # reusable once append returns
+        else:
+            st.append(chunk)
+        hand_off()
+    st.finalize()
+    hand_off(final=True)
+    st.wait_copies()
+    assert sorted(out) == sorted(exp)
+    for key, (buf, flags) in sorted(exp.items()):
+        got, gflags = out[key]
+        assert_same_pixels(got.array.copy(), buf, U16, f"L{key[0]} layer{key[1]}")
+        assert (gflags.array == flags).all(), key
+    st.close()

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Summarise one tools/profile.sh output directory into profiles/.
+
+Writes profiles/<tag>_<cfg>_pmc.json (per-launch HBM bytes of the dominant
+kernel from the FETCH_SIZE / WRITE_SIZE passes, corrected as
+MI355X_MICROARCH.md prescribes: FETCH_SIZE is in KiB and reports half the
+bytes of a 16-B-per-lane streaming read on gfx950, so x2; WRITE_SIZE is in
+KiB and exact) and copies the kernel-trace --stats table next to it.
+bench.py reads the JSON for roofline.traffic.
+
+usage: tools/pmc_summary.py gpurun_out/prof_r01_c2 c2 r01
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_kernel(path):
+    out = {}
+    for r in csv.DictReader(open(path)):
+        out.setdefault(r["Kernel_Name"], {}).setdefault(r["Counter_Name"], []).append(
+            float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    d, cfg, tag = sys.argv[1], sys.argv[2], sys.argv[3]
+    stats = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))))
+    ours = [s for s in stats if "aqz::" in s["Name"]]
+    dom = max(ours, key=lambda s: float(s["TotalDurationNs"]))
+    fetch = per_kernel(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"))
+    write = per_kernel(os.path.join(d, "pmc_write", "run_counter_collection.csv"))
+    name = dom["Name"]
+    f_kib = statistics.median(fetch[name]["FETCH_SIZE"])
+    w_kib = statistics.median(write[name]["WRITE_SIZE"])
+    res = {
+        "config": cfg,
+        "kernel": name,
+        "launches_traced": int(dom["Calls"]),
+        "avg_duration_ns": float(dom["AverageNs"]),
+        "fetch_size_kib_median": f_kib,
+        "write_size_kib_median": w_kib,
+        "hbm_read_bytes_per_launch": int(f_kib * 1024 * 2),
+        "hbm_write_bytes_per_launch": int(w_kib * 1024),
+        "traffic_bytes_per_launch": int(f_kib * 1024 * 2 + w_kib * 1024),
+        "correction": "FETCH_SIZE x2 (gfx950 reports half of a 16-B/lane streaming read); "
+                      "KiB -> bytes",
+    }
+    sq = os.path.join(d, "pmc_sq", "run_counter_collection.csv")
+    if os.path.exists(sq):
+        s = per_kernel(sq).get(name, {})
+        res["sq"] = {k: statistics.median(v) for k, v in s.items()}
+    os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
+    base = os.path.join(REPO, "profiles", f"{tag}_{cfg}")
+    with open(base + "_pmc.json", "w") as fh:
+        json.dump(res, fh, indent=1)
+    shutil.copy(os.path.join(d, "trace", "run_kernel_stats.csv"), base + "_kernel_stats.csv")
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
