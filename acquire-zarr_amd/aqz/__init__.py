@@ -147,6 +147,7 @@ def lib():
         "aqz_stage_frames_written": ([vp, u32], u64),
         "aqz_stage_copy_layer": ([vp, u32, u64, vp, sz, vp, sz, i32], i32),
         "aqz_stage_copy_layer_async": ([vp, u32, u64, vp, sz, vp, sz], i32),
+        "aqz_stage_frames_consumed": ([vp], u64),
         "aqz_stage_wait_copies": ([vp], i32),
         "aqz_host_alloc": ([sz, C.POINTER(vp)], i32),
         "aqz_host_free": ([vp], None),
@@ -423,6 +424,10 @@ class Stage:
 
     def frames_written(self, level):
         return lib().aqz_stage_frames_written(self.h, level)
+
+    def frames_consumed(self):
+        """Level-0 frames whose source bytes have been read (reusable)."""
+        return lib().aqz_stage_frames_consumed(self.h)
 
     def copy_layer(self, level, layer):
         lay = self.layout(level)

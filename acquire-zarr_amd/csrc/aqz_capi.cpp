@@ -481,6 +481,17 @@ aqz_stage_frames_written(const aqz_stage* st, uint32_t level)
     return st->st->frames_written(level);
 }
 
+uint64_t
+aqz_stage_frames_consumed(aqz_stage* st)
+{
+    if (!st || st->sticky != AQZ_STATUS_SUCCESS)
+        return 0;
+    uint64_t n = 0;
+    if (guard_sticky(st, [&] { n = st->st->frames_consumed(); }) != AQZ_STATUS_SUCCESS)
+        return 0;
+    return n;
+}
+
 aqz_status
 aqz_stage_copy_layer(aqz_stage* st, uint32_t level, uint64_t layer, void* dst,
                      size_t cap, uint8_t* has_data, size_t has_data_cap,

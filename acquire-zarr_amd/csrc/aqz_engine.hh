@@ -142,6 +142,8 @@ class Stage
     void append(const void* frames, uint64_t n_frames, int mem);
     void synchronize();
     uint64_t frames_written(uint32_t level) const;
+    // level-0 frames whose source bytes the stage has finished reading
+    uint64_t frames_consumed();
     void copy_layer(uint32_t level, uint64_t layer, void* dst, size_t cap,
                     uint8_t* has_data, size_t has_data_cap, int mem);
     void device_layer(uint32_t level, uint64_t layer, void** chunks,
@@ -201,6 +203,13 @@ class Stage
     int stage_idx_ = 0;
     hipStream_t h2d_ = nullptr, d2h_ = nullptr;
     std::unique_ptr<CopyPool> pool_;
+    // source consumption: (event, appended frames when it fires)
+    std::vector<std::pair<hipEvent_t, uint64_t>> inflight_;
+    size_t inflight_head_ = 0;
+    std::vector<hipEvent_t> free_ev_;
+    uint64_t appended_ = 0, consumed_ = 0;
+    void note_consumed(hipStream_t s, uint64_t frames);
+    void retire_consumed(bool wait);
     uint32_t nt_mode_ = 0;           // non-temporal load/store bits
     uint32_t knobs_ = 0;             // tuning A/B switches
     std::vector<Pending> pend_;

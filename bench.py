@@ -167,6 +167,12 @@ def cpu_baseline(cfg, seconds):
                       f"every level, single thread"}
 
 
+def reduce_dev(dist, dev):
+    """Where the max-over-ranks tensor lives: the GPU under RCCL, the CPU
+    under gloo."""
+    return dev if dist.get_backend() == "nccl" else "cpu"
+
+
 def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
     """Host frame buffer -> H2D -> stage -> D2H of every completed chunk layer
     (the path BASELINE.json asks to be measured end to end).  The source is a
@@ -222,7 +228,7 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
     el = time.perf_counter() - t0
     if dist:
         dist.barrier()
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=reduce_dev(dist, dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     st.close()
@@ -245,6 +251,94 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
     }
 
 
+def run_paced(torch, aqz, dev, cfg, args):
+    """Simulated camera: frame i lands in a pinned ring of R frames at
+    t0 + i/fps (its pixels are the ring's synthetic contents).  The consumer
+    appends every batch of b frames as soon as it has landed and hands off
+    completed chunk layers; a frame overwritten by the camera before it was
+    appended is a drop.  Latency = from the arrival of a batch's last frame
+    to the completion of its kernels."""
+    dt, bpp = cfg["dtype"], BPP[cfg["dtype"]]
+    b = args.batch or 8
+    st = aqz.Stage(cfg["dims"], dt, cfg["method"], force_levels=cfg["force_levels"],
+                   max_batch_frames=b, layer_slots=3, device=dev.index)
+    stream = torch.cuda.Stream(dev)
+    st.set_stream(stream.cuda_stream)
+    L = st.n_levels()
+    sizes = level_sizes(st)
+    fbytes = sizes[0][0] * sizes[0][1] * bpp
+    lay = [st.layout(l) for l in range(L)]
+    lbytes = [x["bytes_per_chunk"] * x["chunks_per_layer"] for x in lay]
+    R = max(4 * b, int(args.fps * 0.25))  # a quarter second of camera buffer
+    ring = aqz.HostBuffer(R * fbytes)
+    frame = np.random.default_rng(3).integers(0, 256, size=fbytes, dtype=np.uint8)
+    ring.array.reshape(R, fbytes)[:] = frame  # pixel values do not change the cost
+    dst = [[aqz.HostBuffer(lbytes[l]) for _ in range(4)] for l in range(L)]
+    handed = [0] * L
+
+    def hand_off():
+        for l in range(L):
+            done = st.frames_written(l) // lay[l]["frames_per_layer"]
+            while handed[l] < done:
+                st.copy_layer_async(l, handed[l], dst[l][handed[l] % 4].ptr, lbytes[l])
+                handed[l] += 1
+
+    n_total = int(args.fps * args.seconds)
+    period = 1.0 / args.fps
+    consumed, drops, done_frames, appended = 0, 0, 0, 0
+    inflight, lat = [], []
+    t0 = time.perf_counter() + 0.05
+    while consumed < n_total:
+        now = time.perf_counter()
+        arrived = min(n_total, int((now - t0) / period) + 1) if now >= t0 else 0
+        # ring slots held: landed but not appended + appended but not yet
+        # read by the stage's DMA; a frame finding no free slot is dropped
+        held = (arrived - consumed) + (appended - st.frames_consumed())
+        if held > R:
+            drops += held - R
+            consumed += held - R
+        if arrived - consumed >= b or (arrived == n_total and arrived > consumed):
+            n = min(b, arrived - consumed)
+            s0 = consumed % R
+            first = min(n, R - s0)
+            st.append_ptr(ring.ptr + s0 * fbytes, first, aqz.MEM_HOST_PINNED)
+            if n > first:
+                st.append_ptr(ring.ptr, n - first, aqz.MEM_HOST_PINNED)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            inflight.append((ev, t0 + (consumed + n - 1) * period, n))
+            consumed += n
+            appended += n
+            hand_off()
+        else:
+            time.sleep(min(period / 4, 0.0005))
+        while inflight and inflight[0][0].query():
+            ev, t_arr, n = inflight.pop(0)
+            lat.append(time.perf_counter() - t_arr)
+            done_frames += n
+    st.synchronize()
+    for ev, t_arr, n in inflight:
+        lat.append(time.perf_counter() - t_arr)
+        done_frames += n
+    el = time.perf_counter() - t0
+    st.close()
+    lat_ms = np.array(lat) * 1e3
+    return {
+        "metric": f"sustained fps, simulated camera at {args.fps:g} fps into pinned memory "
+                  "-> H2D -> multiscale stage -> D2H of every chunk layer",
+        "value": round(done_frames / el, 1), "unit": "frames/s", "n_gpus": 1,
+        "higher_is_better": True, "target_fps": args.fps, "frames": n_total,
+        "processed": done_frames, "drops": drops, "batch": b, "camera_ring_frames": R,
+        "latency_ms": {"p50": round(float(np.percentile(lat_ms, 50)), 2),
+                       "p99": round(float(np.percentile(lat_ms, 99)), 2),
+                       "max": round(float(lat_ms.max()), 2)},
+        "input_gbs": round(done_frames * fbytes / el / 1e9, 3),
+        "dtype": {U8: "u8", U16: "u16", F32: "f32"}[dt],
+        "config": {"workload": cfg["workload"].replace("device-resident", "host-resident") +
+                   f" [paced camera {args.fps:g} fps]", "levels": L},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -257,6 +351,17 @@ def main():
                     help="skip the level-0 tile split (downsample levels only)")
     ap.add_argument("--no-pyramid-only-line", action="store_true",
                     help="do not add the pyramid-only side measurement")
+    ap.add_argument("--no-kernel-events", action="store_true",
+                    help="diagnostic: time the region without per-launch HIP events "
+                         "(roofline.achieved then uses the wall time per launch)")
+    ap.add_argument("--fps", type=float, default=0.0,
+                    help="with --e2e pinned: a simulated camera delivering frames "
+                         "at this rate into a pinned ring (SURVEY 8d, C3 @ 500 fps); "
+                         "reports sustained fps, drops and latency")
+    ap.add_argument("--seconds", type=float, default=5.0,
+                    help="duration of the --fps run")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per append (default: the config's batch)")
     ap.add_argument("--e2e", choices=["pinned", "pageable"], default=None,
                     help="end-to-end mode: frames start in host memory (pinned or "
                          "pageable), every completed chunk layer is handed back to "
@@ -270,8 +375,12 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # nccl (= RCCL) on a real node; AQZ_DIST_BACKEND=gloo rehearses the
+        # multi-rank path with ranks sharing the GPUs present
+        backend = os.environ.get("AQZ_DIST_BACKEND", "nccl")
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
@@ -311,7 +420,7 @@ def main():
         if dist:
             dist.barrier()
         torch.cuda.synchronize(dev)
-        st.enable_kernel_timing(True)
+        st.enable_kernel_timing(not args.no_kernel_events)
         t0 = time.perf_counter()
         for s in range(steps):
             step(warmup + s)
@@ -321,10 +430,12 @@ def main():
             dist.barrier()
         elapsed = t1 - t0
         if dist:
-            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            t = torch.tensor([elapsed], dtype=torch.float64, device=reduce_dev(dist, dev))
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         kms, launches = st.kernel_timing()
+        if args.no_kernel_events:
+            kms, launches = elapsed * 1e3, steps
         kernel = st.dominant_kernel()
         st.close()
         del ring
@@ -336,6 +447,10 @@ def main():
                     achieved=alg / (avg_ms * 1e-3) / 1e9 if launches else 0.0,
                     value=world * steps * B * fbytes / elapsed / 1e9)
 
+    if args.e2e and args.fps > 0:
+        res = run_paced(torch, aqz, dev, cfg, args)
+        print(json.dumps(res), flush=True)
+        return
     if args.e2e:
         res = run_e2e(torch, aqz, dev, cfg, args, world, rank, dist)
         if rank == 0:

@@ -74,7 +74,7 @@ enum
     AQZ_MEM_HOST = 0,        /* pageable host memory (copied to pinned staging) */
     AQZ_MEM_DEVICE = 1,      /* already resident in this device's HBM */
     AQZ_MEM_HOST_PINNED = 2  /* page-locked host memory (e.g. aqz_host_alloc):
-                                DMA'd straight to the device */
+                                DMA'd straight to the device, asynchronously */
 };
 
 /* The pixel-geometry subset of ZarrDimensionProperties
@@ -235,18 +235,23 @@ aqz_status aqz_stage_level_layout(const aqz_stage* st, uint32_t level,
  * stage's own stream).  All later work is enqueued there. */
 aqz_status aqz_stage_set_stream(aqz_stage* st, void* stream);
 /* Append n_frames full level-0 frames (contiguous, frame after frame).
- * Equivalent to n_frames calls of MultiscaleArray::write_frame.  Device
- * sources are consumed asynchronously (do not modify them until the next
- * aqz_stage_synchronize); host sources may be reused when append returns,
- * as with ZarrStream_append (frame.queue.cpp:37-39): AQZ_MEM_HOST is copied
- * into a pinned staging buffer by a few host threads, AQZ_MEM_HOST_PINNED is
- * DMA'd directly.  Either way the H2D runs on the stage's copy stream and
- * overlaps the previous batch's kernels. */
+ * Equivalent to n_frames calls of MultiscaleArray::write_frame.
+ *  - AQZ_MEM_HOST: copied into a pinned staging buffer by a few host threads
+ *    before return, so the caller may reuse it at once, as with
+ *    ZarrStream_append (frame.queue.cpp:37-39);
+ *  - AQZ_MEM_HOST_PINNED (a camera's DMA ring) and AQZ_MEM_DEVICE: read
+ *    asynchronously; keep the bytes unchanged until aqz_stage_frames_consumed
+ *    counts them (or aqz_stage_synchronize returns).
+ * The H2D runs on the stage's copy stream and overlaps earlier batches'
+ * kernels and hand-off copies. */
 aqz_status aqz_stage_append(aqz_stage* st, const void* frames,
                             uint64_t n_frames, int32_t mem);
 aqz_status aqz_stage_synchronize(aqz_stage* st);
 /* frames written so far to `level` (Array::frames_written_) */
 uint64_t aqz_stage_frames_written(const aqz_stage* st, uint32_t level);
+/* Level-0 frames appended so far whose source bytes the stage has finished
+ * reading (in append order): their source buffers may be reused. */
+uint64_t aqz_stage_frames_consumed(aqz_stage* st);
 /* Copy chunk layer `layer` of `level` (must still be resident) to dst
  * (bytes_per_chunk*chunks_per_layer bytes) and its has_data flags (one byte
  * per chunk, 1 = some byte of the chunk is nonzero).  Synchronizes.  Frames

@@ -359,15 +359,24 @@ def test_stage_async_handoff_pinned_and_pageable(gpu):
                 out[(l, handed[l])] = (buf, hd)
                 handed[l] += 1
 
+    appended = 0
     for i, b0 in enumerate(range(0, n, B)):
         chunk = np.ascontiguousarray(frames[b0:b0 + B])
         if i % 2 == 0:
+            # a pinned source is read asynchronously: reuse it only once the
+            # stage reports its frames consumed
+            while st.frames_consumed() < appended:
+                pass
             pinned_src.view(np.uint16, chunk.shape)[...] = chunk
             st.append(pinned_src, len(chunk))
-            pinned_src.view(np.uint16)[...] = 0  # reusable once append returns
         else:
-            st.append(chunk)
+            st.append(chunk)  # pageable: copied before return
+            chunk[...] = 0
+        appended += len(chunk)
+        assert st.frames_consumed() <= appended
         hand_off()
+    st.synchronize()
+    assert st.frames_consumed() == n
     st.finalize()
     hand_off(final=True)
     st.wait_copies()

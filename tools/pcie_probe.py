@@ -62,20 +62,36 @@ def main():
             d2h()
             h2d()
 
-        def chunked():  # 8 interleaved 64 MiB pieces per direction
-            p = n // 8
-            for i in range(8):
-                assert hip.hipMemcpyAsync(d_a.data_ptr() + i * p, src + i * p, p, 1,
-                                          s1.cuda_stream) == 0
-                assert hip.hipMemcpyAsync(dst + i * p, d_b.data_ptr() + i * p, p, 2,
-                                          s2.cuda_stream) == 0
+        def pieces(mb, interleave):
+            p = mb << 20
+
+            def fn():
+                if interleave:
+                    for o in range(0, n, p):
+                        assert hip.hipMemcpyAsync(d_a.data_ptr() + o, src + o, p, 1,
+                                                  s1.cuda_stream) == 0
+                        assert hip.hipMemcpyAsync(dst + o, d_b.data_ptr() + o, p, 2,
+                                                  s2.cuda_stream) == 0
+                else:  # all H2D pieces issued first, then all D2H pieces
+                    for o in range(0, n, p):
+                        assert hip.hipMemcpyAsync(d_a.data_ptr() + o, src + o, p, 1,
+                                                  s1.cuda_stream) == 0
+                    for o in range(0, n, p):
+                        assert hip.hipMemcpyAsync(dst + o, d_b.data_ptr() + o, p, 2,
+                                                  s2.cuda_stream) == 0
+            return fn
 
         t_h, t_d = timed(h2d), timed(d2h)
-        t_b, t_r, t_c = timed(both), timed(both_rev), timed(chunked)
+        t_b, t_r = timed(both), timed(both_rev)
         out[kind] = {"h2d_gbs": round(n / t_h / 1e9, 2), "d2h_gbs": round(n / t_d / 1e9, 2),
                      "duplex_total_gbs": round(2 * n / t_b / 1e9, 2),
-                     "duplex_rev_total_gbs": round(2 * n / t_r / 1e9, 2),
-                     "duplex_chunked_total_gbs": round(2 * n / t_c / 1e9, 2)}
+                     "duplex_rev_total_gbs": round(2 * n / t_r / 1e9, 2)}
+        for mb in (8, 32, 64, 128):
+            for il in (True, False):
+                t = timed(pieces(mb, il))
+                out[kind][f"pieces{mb}MiB_{'interleaved' if il else 'h2d_first'}_total_gbs"] = \
+                    round(2 * n / t / 1e9, 2)
+
     print(json.dumps(out))
 
 
