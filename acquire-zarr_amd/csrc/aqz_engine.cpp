@@ -159,9 +159,15 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
 
     auto base = std::make_unique<ArrayDimensions>(desc.dims, desc.dtype,
                                                   desc.storage_order);
-    if (base->needs_xy_transposition())
-        throw Error(4, "XY-transposed storage order is not implemented on "
-                       "the GPU stage");
+    if (base->needs_xy_transposition()) {
+        // Array::write_frame_to_chunks_ transposes the acquired frame
+        // (array.cpp:525-533) and the downsampler sees the transposed frame
+        // (multiscale.array.cpp:66-72): every level works in storage order
+        xy_ = true;
+        const size_t nd = desc.dims.size();
+        acq_rows_ = desc.dims[nd - 2].array_size_px;
+        acq_cols_ = desc.dims[nd - 1].array_size_px;
+    }
     std::vector<std::vector<Dim>> levels;
     if (desc.multiscale)
         levels = make_pyramid_levels(base->dims(), desc.max_levels,
@@ -565,6 +571,13 @@ Stage::append(const void* frames, uint64_t n_frames, int mem)
 void
 Stage::run_batch(const uint8_t* dsrc, uint32_t n)
 {
+    if (xy_) {
+        xbuf_.alloc(size_t(opt_.max_batch_frames) * acq_rows_ * acq_cols_ * bpp_);
+        hip_check(launch_transpose_frames(dsrc, xbuf_.p, acq_rows_, acq_cols_, n,
+                                          uint32_t(bpp_), stream_),
+                  "transpose launch");
+        dsrc = xbuf_.p;
+    }
     std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
     if (timing_) {
         if (ev_used_ == ev_pairs_.size()) {

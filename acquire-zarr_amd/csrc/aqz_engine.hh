@@ -26,6 +26,9 @@ hipError_t launch_level(int dtype, int method, const LevelParams& p,
                         hipStream_t stream);
 hipError_t launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
                                    hipStream_t stream);
+hipError_t launch_transpose_frames(const void* src, void* dst, uint32_t rows,
+                                   uint32_t cols, uint32_t n_frames, uint32_t bpp,
+                                   hipStream_t stream);
 hipError_t launch_flags_to_bytes(const uint32_t* flags, uint8_t* out, uint32_t n,
                                  uint32_t tag, hipStream_t stream);
 hipError_t launch_zero_frame_tiles(uint8_t* fb, uint64_t bpc,
@@ -203,6 +206,11 @@ class Stage
     int stage_idx_ = 0;
     hipStream_t h2d_ = nullptr, d2h_ = nullptr;
     std::unique_ptr<CopyPool> pool_;
+    // XY-transposed storage order: level-0 frames are transposed into xbuf_
+    // (acquisition rows x cols -> storage rows x cols) before the pipeline
+    bool xy_ = false;
+    uint32_t acq_rows_ = 0, acq_cols_ = 0;
+    DevBuf xbuf_;
     // source consumption: (event, appended frames when it fires)
     std::vector<std::pair<hipEvent_t, uint64_t>> inflight_;
     size_t inflight_head_ = 0;

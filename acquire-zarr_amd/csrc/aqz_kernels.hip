@@ -1263,6 +1263,74 @@ launch_level(int dtype, int method, const LevelParams& p, hipStream_t stream)
     return hipGetLastError();
 }
 
+// Y x X -> X x Y transpose of a batch of level-0 frames (Array::
+// transpose_frame, array.cpp:488-504; applied before the split when the
+// storage order swaps the two spatial dims, array.cpp:525-533, and the
+// downsampler then sees the transposed frame).  64x64 tiles through LDS:
+// both the row reads and the row writes are coalesced.  Pixels are moved as
+// opaque words of their size.
+template<typename W>
+__global__ __launch_bounds__(256) void
+transpose_frames(const W* __restrict__ src, W* __restrict__ dst, uint32_t rows,
+                 uint32_t cols)
+{
+    __shared__ W tile[64][65];
+    const uint64_t fe = uint64_t(rows) * cols;
+    const W* s = src + blockIdx.z * fe;
+    W* d = dst + blockIdx.z * fe;
+    const uint32_t x0 = blockIdx.x * 64, y0 = blockIdx.y * 64;
+    const uint32_t tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+    for (uint32_t i = 0; i < 16; ++i) {
+        const uint32_t r = ty + 4 * i;
+        const uint32_t y = y0 + r, x = x0 + tx;
+        if (y < rows && x < cols)
+            tile[r][tx] = s[uint64_t(y) * cols + x];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t i = 0; i < 16; ++i) {
+        const uint32_t r = ty + 4 * i;
+        const uint32_t oy = x0 + r, ox = y0 + tx; // output row = input column
+        if (oy < cols && ox < rows)
+            d[uint64_t(oy) * rows + ox] = tile[tx][r];
+    }
+}
+
+hipError_t
+launch_transpose_frames(const void* src, void* dst, uint32_t rows, uint32_t cols,
+                        uint32_t n_frames, uint32_t bpp, hipStream_t stream)
+{
+    if (n_frames == 0 || rows == 0 || cols == 0)
+        return hipSuccess;
+    const dim3 grid((cols + 63) / 64, (rows + 63) / 64, n_frames);
+    switch (bpp) {
+        case 1:
+            hipLaunchKernelGGL(transpose_frames<uint8_t>, grid, dim3(256), 0, stream,
+                               static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst),
+                               rows, cols);
+            break;
+        case 2:
+            hipLaunchKernelGGL(transpose_frames<uint16_t>, grid, dim3(256), 0, stream,
+                               static_cast<const uint16_t*>(src),
+                               static_cast<uint16_t*>(dst), rows, cols);
+            break;
+        case 4:
+            hipLaunchKernelGGL(transpose_frames<uint32_t>, grid, dim3(256), 0, stream,
+                               static_cast<const uint32_t*>(src),
+                               static_cast<uint32_t*>(dst), rows, cols);
+            break;
+        case 8:
+            hipLaunchKernelGGL(transpose_frames<uint64_t>, grid, dim3(256), 0, stream,
+                               static_cast<const uint64_t*>(src),
+                               static_cast<uint64_t*>(dst), rows, cols);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 // has_data of one chunk layer as 0/1 bytes: a chunk holds data of this layer
 // when its word carries the layer's generation tag (Chunk::has_data,
 // chunk.cpp:17-67)

@@ -386,3 +386,56 @@ def test_stage_async_handoff_pinned_and_pageable(gpu):
         assert_same_pixels(got.array.copy(), buf, U16, f"L{key[0]} layer{key[1]}")
         assert (gflags.array == flags).all(), key
     st.close()
+
+
+@pytest.mark.parametrize("perm", [[0, 2, 1, 3, 4], [0, 1, 2, 4, 3], [0, 2, 1, 4, 3]],
+                         ids=["cz_swap", "xy_swap", "cz_and_xy_swap"])
+def test_stage_storage_dimension_order(gpu, perm):
+    """storage_dimension_order: level-0 frame ids go through
+    transpose_frame_id (array.cpp:557-561), an XY swap transposes every
+    acquired frame before the split and the downsampler sees the transposed
+    frame (array.cpp:525-533, multiscale.array.cpp:66-72); every level
+    works on the storage-order dims (array.dimensions.cpp:12-73)."""
+    acq = [(TIME, 0, 2, 1), (CHANNEL, 3, 2, 1), (SPACE, 4, 2, 1),
+           (SPACE, 40, 16, 1), (SPACE, 57, 8, 1)]
+    n = 3 * 4 * 3 + 5  # three time points and a partial fourth
+    frames = _frames(U16, n, 40, 57, 17 + sum(i * p for i, p in enumerate(perm)),
+                     specials=False)
+    sdims = [acq[i] for i in perm]
+    xy = perm[-1] != len(acq) - 1
+    stored = np.ascontiguousarray(frames.transpose(0, 2, 1)) if xy else frames
+    dims_map = gpu.Dims(acq, U16, storage_order=perm)
+    exp, fw, ldims = expected_stage_layers(sdims, U16, MEAN, stored,
+                                           storage_fid=dims_map.transpose_frame_id)
+    st = gpu.Stage(acq, U16, MEAN, storage_order=perm, max_batch_frames=5)
+    assert st.n_levels() == len(ldims)
+    for l in range(st.n_levels()):
+        assert [tuple(x) for x in st.level_dims(l)] == [tuple(x) for x in ldims[l]]
+    for b0 in range(0, n, 5):
+        st.append(np.ascontiguousarray(frames[b0:b0 + 5]))
+    st.finalize()
+    for l in range(st.n_levels()):
+        assert st.frames_written(l) == fw[l]
+    for (l, layer), (buf, flags) in sorted(exp.items()):
+        got, gflags = st.copy_layer(l, layer)
+        assert_same_pixels(got, buf, U16, f"L{l} layer{layer}")
+        assert (gflags == flags).all(), (l, layer)
+    st.close()
+
+
+@pytest.mark.parametrize("dtype", [U8, U16, F32, F64], ids=lambda d: DTYPE_NAMES[d])
+def test_stage_xy_transpose_sizes(gpu, dtype):
+    # frames larger than one 64x64 transpose tile, ragged on both axes
+    acq = [(TIME, 0, 3, 1), (SPACE, 130, 32, 1), (SPACE, 77, 16, 1)]
+    frames = _frames(dtype, 7, 130, 77, 5 + dtype)
+    stored = np.ascontiguousarray(frames.transpose(0, 2, 1))
+    exp, fw, ldims = expected_stage_layers([acq[0], acq[2], acq[1]], dtype, MAX, stored)
+    st = gpu.Stage(acq, dtype, MAX, storage_order=[0, 2, 1], max_batch_frames=3,
+                   layer_slots=4)
+    st.append(frames)
+    st.finalize()
+    for (l, layer), (buf, flags) in sorted(exp.items()):
+        got, gflags = st.copy_layer(l, layer)
+        assert_same_pixels(got, buf, dtype, f"L{l} layer{layer}")
+        assert (gflags == flags).all()
+    st.close()
