@@ -68,7 +68,8 @@ class LevelLayoutC(C.Structure):
     _fields_ = [("bytes_per_chunk", C.c_uint64),
                 ("chunks_per_layer", C.c_uint32), ("layer_slots", C.c_uint32),
                 ("frames_per_layer", C.c_uint64), ("frame_bytes", C.c_uint64),
-                ("width", C.c_uint32), ("height", C.c_uint32)]
+                ("width", C.c_uint32), ("height", C.c_uint32),
+                ("chunk_pitch", C.c_uint64)]
 
 
 def build_library(force: bool = False) -> str:

@@ -445,7 +445,7 @@ aqz_stage_level_layout(const aqz_stage* st, uint32_t level,
         *out = aqz_level_layout{ l.bytes_per_chunk, l.chunks_per_layer,
                                  l.layer_slots,     l.frames_per_layer,
                                  l.frame_bytes,     l.width,
-                                 l.height };
+                                 l.height,          l.chunk_pitch };
     });
 }
 

@@ -1,3 +1,4 @@
+#include <cstdio>
 // aqz_engine.cpp -- see aqz_engine.hh.  Citations are to
 // /root/reference/src/streaming/.
 #include "aqz_engine.hh"
@@ -63,7 +64,16 @@ DevBuf::alloc(size_t bytes)
     if (bytes == 0)
         return;
     void* q = nullptr;
-    hip_check(hipMalloc(&q, bytes), "hipMalloc");
+    static const unsigned flags = [] {
+        const char* s = std::getenv("AQZ_MALLOC_FLAGS"); // tuning knob
+        return s ? unsigned(std::atoi(s)) : 0u;
+    }();
+    if (flags)
+        hip_check(hipExtMallocWithFlags(&q, bytes, flags), "hipExtMallocWithFlags");
+    else
+        hip_check(hipMalloc(&q, bytes), "hipMalloc");
+    if (std::getenv("AQZ_DEBUG_ALLOC") && bytes >= (size_t(1) << 24))
+        fprintf(stderr, "aqz alloc %p %zu MiB\n", q, bytes >> 20);
     p = static_cast<uint8_t*>(q);
     n = bytes;
 }
@@ -115,6 +125,40 @@ memcpy_pieces(void* dst, const void* src, size_t n, hipMemcpyKind kind,
                                  static_cast<const uint8_t*>(src) + o,
                                  std::min(piece, n - o), kind, stream),
                   "hipMemcpyAsync");
+}
+
+// n chunks of bpc bytes, `pitch` apart in the source, packed into dst, in
+// pieces of about copy_piece_bytes() (full-duplex PCIe, see memcpy_pieces)
+static void
+copy_chunks(void* dst, const uint8_t* src, uint64_t bpc, uint64_t pitch, uint32_t n,
+            hipMemcpyKind kind, hipStream_t stream)
+{
+    if (pitch == bpc) {
+        memcpy_pieces(dst, src, bpc * n, kind, stream);
+        return;
+    }
+    const uint64_t per = std::max<uint64_t>(1, copy_piece_bytes() / bpc);
+    for (uint64_t c = 0; c < n; c += per) {
+        const uint64_t m = std::min<uint64_t>(per, n - c);
+        if (m > 1)
+            hip_check(hipMemcpy2DAsync(static_cast<uint8_t*>(dst) + c * bpc, bpc,
+                                       src + c * pitch, pitch, bpc, m, kind, stream),
+                      "hipMemcpy2DAsync");
+        else // one chunk of at least a piece
+            memcpy_pieces(static_cast<uint8_t*>(dst) + c * bpc, src + c * pitch, bpc,
+                          kind, stream);
+    }
+}
+
+// Device chunk pitch: bpc, or bpc plus a pad that staggers the chunks of a
+// layer across HBM channels (AQZ_CHUNK_PAD bytes; tuning knob).
+static uint64_t
+chunk_pitch(uint64_t bpc, uint32_t n_chunks)
+{
+    (void)n_chunks;
+    if (const char* s = std::getenv("AQZ_CHUNK_PAD"))
+        return bpc + uint64_t(std::max(0L, std::atol(s)));
+    return bpc;
 }
 
 // host threads for the pageable -> pinned staging copy (AQZ_COPY_THREADS)
@@ -205,7 +249,9 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         if (F == 0 || F > 0x7fffffffull)
             throw Error(9, "unsupported frames per chunk layer");
         L.F = uint32_t(F);
-        L.slot_bytes = L.bpc * L.n_chunks;
+        L.pitch = chunk_pitch(L.bpc, L.n_chunks);
+        L.slot_bytes = L.pitch * L.n_chunks;
+        L.layer_bytes = L.bpc * L.n_chunks;
         L.n_slots = std::max<uint32_t>(opt_.layer_slots,
                                        (B - 1 + L.F - 1) / L.F + 1);
         L.slot_layer.assign(L.n_slots, -1);
@@ -229,7 +275,7 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
             const uint64_t sf = L.ad->transpose_frame_id(fl);
             const uint32_t grp = L.ad->tile_group_offset(sf);
             L.h_tab_grp[fl] = grp;
-            L.h_tab_off[fl] = uint64_t(grp) * L.bpc + L.ad->chunk_internal_offset(sf);
+            L.h_tab_off[fl] = uint64_t(grp) * L.pitch + L.ad->chunk_internal_offset(sf);
         }
         // frame -> (tiles, has_data) over one ring period
         const uint64_t P = uint64_t(L.n_slots) * L.F;
@@ -311,7 +357,7 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
     if (const char* ev = std::getenv("AQZ_KNOBS")) // tuning knob
         knobs_ = uint32_t(std::atoi(ev));
     if (const char* ev = std::getenv("AQZ_NT")) // tuning knob
-        nt_mode_ = uint32_t(std::atoi(ev)) & 3u;
+        nt_mode_ = uint32_t(std::atoi(ev)) & 7u;
     if (const char* ev = std::getenv("AQZ_REGION_ROWS_LOG2")) { // tuning knob
         const uint32_t v = uint32_t(std::atoi(ev));
         if (v >= std::max<uint32_t>(4, n_fused_) && (1u << v) <= uint32_t(kMaxRegionRows))
@@ -418,7 +464,7 @@ Stage::layout(uint32_t level) const
     return LevelLayout{ L.bpc,   L.n_chunks,
                         L.n_slots, L.F,
                         uint64_t(L.W) * L.H * bpp_, L.W,
-                        L.H };
+                        L.H,     L.pitch };
 }
 
 void
@@ -668,7 +714,7 @@ Stage::geom(StageLevel& L, uint64_t fid0, bool tiles, uint8_t* scratch) const
     g.ntx = L.ntx;
     g.dtw = make_fastdiv(L.tw);
     g.dth = make_fastdiv(L.th);
-    g.bpc = L.bpc;
+    g.bpc = L.pitch;
     g.slot_bytes = L.slot_bytes;
     g.n_chunks = L.n_chunks;
     g.n_slots = L.n_slots;
@@ -730,10 +776,10 @@ Stage::fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
     p.th = L0.th;
     p.dtw = make_fastdiv(L0.tw);
     p.dth = make_fastdiv(L0.th);
-    p.bpc = L0.bpc;
+    p.bpc = L0.pitch;
     for (uint32_t k = 0; k <= n_fused; ++k) {
         StageLevel& L = lv_[k];
-        if (L.bpc != p.bpc || L.tw != p.tw || L.th != p.th)
+        if (L.pitch != p.bpc || L.tw != p.tw || L.th != p.th)
             throw Error(5, "chunk shape differs between levels");
         p.W[k] = L.W;
         p.H[k] = L.H;
@@ -987,13 +1033,14 @@ Stage::copy_layer(uint32_t level, uint64_t layer, void* dst, size_t cap,
     const uint32_t slot = uint32_t(layer % L.n_slots);
     if (L.slot_layer[slot] != int64_t(layer))
         throw Error(3, "chunk layer not resident");
-    if (dst && cap < L.slot_bytes)
+    if (dst && cap < L.layer_bytes)
         throw Error(2, "destination too small for a chunk layer");
     synchronize();
-    if (dst)
-        hip_check(hipMemcpy(dst, L.ring.p + slot * L.slot_bytes, L.slot_bytes,
-                            kind_from(kMemDevice, mem)),
-                  "hipMemcpy");
+    if (dst) {
+        copy_chunks(dst, L.ring.p + slot * L.slot_bytes, L.bpc, L.pitch, L.n_chunks,
+                    kind_from(kMemDevice, mem), stream_);
+        hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    }
     if (has_data) {
         if (has_data_cap < L.n_chunks)
             throw Error(2, "has_data too small");
@@ -1019,7 +1066,7 @@ Stage::copy_layer_async(uint32_t level, uint64_t layer, void* dst, size_t cap,
     const uint32_t slot = uint32_t(layer % L.n_slots);
     if (L.slot_layer[slot] != int64_t(layer))
         throw Error(3, "chunk layer not resident");
-    if (dst && cap < L.slot_bytes)
+    if (dst && cap < L.layer_bytes)
         throw Error(2, "destination too small for a chunk layer");
     if (has_data && has_data_cap < L.n_chunks)
         throw Error(2, "has_data too small");
@@ -1027,8 +1074,8 @@ Stage::copy_layer_async(uint32_t level, uint64_t layer, void* dst, size_t cap,
     hip_check(hipEventRecord(L.ready_ev[slot], stream_), "hipEventRecord");
     hip_check(hipStreamWaitEvent(d2h_, L.ready_ev[slot], 0), "hipStreamWaitEvent");
     if (dst)
-        memcpy_pieces(dst, L.ring.p + slot * L.slot_bytes, L.slot_bytes, hipMemcpyDefault,
-                      d2h_);
+        copy_chunks(dst, L.ring.p + slot * L.slot_bytes, L.bpc, L.pitch, L.n_chunks,
+                    hipMemcpyDefault, d2h_);
     if (has_data) {
         uint8_t* fb = L.flag_bytes.p + size_t(slot) * L.n_chunks;
         hip_check(launch_flags_to_bytes(
@@ -1072,7 +1119,7 @@ Stage::finalize()
             uint64_t off;
             uint32_t fo;
             tile_addr(L, fid, &off, &fo, nullptr);
-            hip_check(launch_zero_frame_tiles(L.ring.p + off, L.bpc,
+            hip_check(launch_zero_frame_tiles(L.ring.p + off, L.pitch,
                                               L.ntx * L.nty,
                                               uint32_t(uint64_t(L.tw) * L.th * bpp_),
                                               stream_),

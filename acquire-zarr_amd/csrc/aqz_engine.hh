@@ -100,6 +100,7 @@ struct LevelLayout
     uint64_t frames_per_layer;
     uint64_t frame_bytes;
     uint32_t width, height;
+    uint64_t chunk_pitch;  // device bytes from chunk c to c+1 (>= bytes_per_chunk)
 };
 
 // Per-level device state shared by Stage.
@@ -109,7 +110,10 @@ struct StageLevel
     std::unique_ptr<ArrayDimensions> ad;   // chunk lattice of this level
     uint32_t W = 0, H = 0, planes = 0;
     bool xy_shrinks = false;               // vs previous level
-    uint64_t bpc = 0, slot_bytes = 0;
+    uint64_t bpc = 0;                      // bytes per chunk (the reference's)
+    uint64_t pitch = 0;                    // device chunk pitch, >= bpc
+    uint64_t slot_bytes = 0;               // device bytes per layer slot
+    uint64_t layer_bytes = 0;              // bpc * n_chunks (host layout)
     uint32_t n_chunks = 0, n_slots = 0, F = 0;
     uint32_t tw = 0, th = 0, ntx = 0, nty = 0;
     DevBuf ring, flags, tab_off, tab_grp, ref_table;

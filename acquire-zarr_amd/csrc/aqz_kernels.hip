@@ -86,11 +86,25 @@ struct VecT<1>
 
 template<typename T, int N>
 __device__ __forceinline__ void
-store_vec(uint8_t* p, const T* v)
+store_vec(uint8_t* p, const T* v, bool nt = false)
 {
     using V = typename VecT<N * sizeof(T)>::type;
     V raw;
     __builtin_memcpy(&raw, v, N * sizeof(T));
+    if constexpr (N * sizeof(T) == 8) {
+        if (nt) {
+            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            u32x2 w;
+            __builtin_memcpy(&w, &raw, 8);
+            __builtin_nontemporal_store(w, reinterpret_cast<u32x2*>(p));
+            return;
+        }
+    } else if constexpr (N * sizeof(T) <= 4) {
+        if (nt) {
+            __builtin_nontemporal_store(raw, reinterpret_cast<V*>(p));
+            return;
+        }
+    }
     *reinterpret_cast<V*>(p) = raw;
 }
 
@@ -731,7 +745,7 @@ fast_pass(const FusedParams& p, uint32_t pass, const uint4& ra, const uint4& rb,
     for (int i = 0; i < HV; ++i)
         o[i] = reduce4<M, T>(r0[2 * i], r0[2 * i + 1], r1[2 * i], r1[2 * i + 1]);
     if (t1.p && !(p.knobs & 4u)) {
-        store_vec<T, HV>(t1.p + uint64_t(pass * 8 + rp) * trow, o);
+        store_vec<T, HV>(t1.p + uint64_t(pass * 8 + rp) * trow, o, p.nt & 4);
         t1.nz |= any_nonzero<T, HV>(o);
     }
     if (p.n_fused < 2)
@@ -752,7 +766,7 @@ fast_pass(const FusedParams& p, uint32_t pass, const uint4& ra, const uint4& rb,
             for (int j = 0; j < QV; ++j)
                 q[j] = reduce4<M, T>(o[2 * j], o[2 * j + 1], b[2 * j], b[2 * j + 1]);
             if (t2.p && !(p.knobs & 8u)) {
-                store_vec<T, QV>(t2.p + uint64_t(row2) * trow, q);
+                store_vec<T, QV>(t2.p + uint64_t(row2) * trow, q, p.nt & 4);
                 t2.nz |= any_nonzero<T, QV>(q);
             }
             if (lds_l2) {

@@ -221,6 +221,10 @@ typedef struct
     uint64_t frames_per_layer;
     uint64_t frame_bytes;      /* width*height*bpp of this level */
     uint32_t width, height;
+    uint64_t chunk_pitch;      /* device bytes from chunk c to chunk c+1 of
+                                  a resident layer (>= bytes_per_chunk; the
+                                  pad staggers chunks over HBM channels).
+                                  Host copies are packed at bytes_per_chunk. */
 } aqz_level_layout;
 
 aqz_status aqz_stage_create(const aqz_array_desc* desc,
@@ -275,7 +279,7 @@ aqz_status aqz_stage_wait_copies(aqz_stage* st);
 aqz_status aqz_host_alloc(size_t bytes, void** out);
 void aqz_host_free(void* p);
 /* Device pointers of a resident layer (for device-side consumers).  Chunk c
- * has data iff has_data[c] == layer / layer_slots + 1 (the words carry the
+ * starts at chunks + c * chunk_pitch (aqz_level_layout).  Chunk c has data iff has_data[c] == layer / layer_slots + 1 (the words carry the
  * ring-slot generation, so they are never cleared). */
 aqz_status aqz_stage_device_layer(aqz_stage* st, uint32_t level,
                                   uint64_t layer, void** chunks,

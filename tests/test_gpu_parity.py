@@ -329,12 +329,15 @@ def test_stage_z_slab_sharding(gpu):
     b.close()
 
 
-def test_stage_async_handoff_pinned_and_pageable(gpu):
+@pytest.mark.parametrize("pad", [0, 4224])
+def test_stage_async_handoff_pinned_and_pageable(gpu, pad, monkeypatch):
     """The ingestion / hand-off pipeline: pinned and pageable (multi-threaded
     staging copy) host sources, H2D on the copy stream, and every chunk layer
     handed off with copy_layer_async while the 3-slot ring wraps several
     times -- the copies must see each layer whole (a slot is not rewritten
-    before its D2H has finished)."""
+    before its D2H has finished).  pad > 0: chunks `bpc + pad` apart on the
+    device (AQZ_CHUNK_PAD), packed back to bpc by the strided D2H."""
+    monkeypatch.setenv("AQZ_CHUNK_PAD", str(pad))
     dims = [(TIME, 0, 2, 1), (SPACE, 1024, 128, 1), (SPACE, 1024, 128, 1)]
     n, B = 20, 4
     frames = synthetic_frames(U16, n, 1024, 1024, 31)
@@ -342,6 +345,7 @@ def test_stage_async_handoff_pinned_and_pageable(gpu):
     st = gpu.Stage(dims, U16, MEAN, layer_slots=2, max_batch_frames=B)
     L = st.n_levels()
     lay = [st.layout(l) for l in range(L)]
+    assert all(x["chunk_pitch"] == x["bytes_per_chunk"] + pad for x in lay)
     nbytes = [x["bytes_per_chunk"] * x["chunks_per_layer"] for x in lay]
     pinned_src = gpu.HostBuffer(B * frames[0].nbytes)
     out, handed = {}, [0] * L
@@ -385,6 +389,12 @@ def test_stage_async_handoff_pinned_and_pageable(gpu):
         got, gflags = out[key]
         assert_same_pixels(got.array.copy(), buf, U16, f"L{key[0]} layer{key[1]}")
         assert (gflags.array == flags).all(), key
+    # the synchronous copy of a still-resident layer packs the chunks too
+    for l in range(L):
+        last = (st.frames_written(l) - 1) // lay[l]["frames_per_layer"]
+        got, gflags = st.copy_layer(l, last)
+        assert_same_pixels(got, exp[(l, last)][0], U16, f"sync L{l} layer{last}")
+        assert np.array_equal(gflags, exp[(l, last)][1])
     st.close()
 
 

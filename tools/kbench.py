@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--knobs", default="")
     ap.add_argument("--depth", action="store_true")
     ap.add_argument("--nt", default="0")
+    ap.add_argument("--pads", default="")
+    ap.add_argument("--prealloc-gb", type=float, default=0)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     stream = torch.cuda.Stream(dev)
@@ -45,23 +47,26 @@ def main():
     B, H, W = 64, 2048, 2048
     fbytes = H * W * 2
     ring = torch.empty(4 * B * fbytes, dtype=torch.uint8, device=dev)
+    print(f"ring {ring.data_ptr():#x}", file=sys.stderr)
     ring.view(torch.int16).random_(-32768, 32767)
     dst = torch.empty(B * fbytes, dtype=torch.uint8, device=dev)
+    hold = torch.empty(int(args.prealloc_gb * 2**30), dtype=torch.uint8, device=dev) if args.prealloc_gb else None
     dims = [(TIME, 0, 64, 1), (SPACE, H, 256, 1), (SPACE, W, 256, 1)]
     variants = {}
     bytes_moved_extra = {}
 
     def mk(name, **kw):
         kw.setdefault("blocks_per_cu", args.bpc)
+        print(f"stage {name}", file=sys.stderr)
         st = aqz.Stage(dims, 1, 1, max_batch_frames=B, layer_slots=2, **kw)
         st.set_stream(stream.cuda_stream)
         variants[name] = st
 
     for rh in args.rh.split(","):
         os.environ["AQZ_REGION_ROWS_LOG2"] = rh
-        for nt in args.nt.split(","):
+        for j, nt in enumerate(args.nt.split(",")):
             os.environ["AQZ_NT"] = nt
-            mk(f"full5_rh{rh}_nt{nt}", force_levels=5)
+            mk(f"full5_rh{rh}_nt{nt}_{j}", force_levels=5)
         os.environ["AQZ_NT"] = "0"
         mk(f"pyr5_rh{rh}", force_levels=5, skip_level0_split=True)
     os.environ.pop("AQZ_REGION_ROWS_LOG2")
@@ -74,6 +79,12 @@ def main():
             bytes_moved_extra[f"full5_k{kn}"] = B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64 + 1 / 256))
             bytes_moved_extra[f"full4_k{kn}"] = B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64))
             os.environ.pop("AQZ_KNOBS")
+    for j, pad in enumerate(args.pads.split(",")):
+        if pad:
+            os.environ["AQZ_CHUNK_PAD"] = pad
+            mk(f"full5_pad{pad}_{j}", force_levels=5)
+            bytes_moved_extra[f"full5_pad{pad}_{j}"] = B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64 + 1 / 256))
+            os.environ.pop("AQZ_CHUNK_PAD")
     for b in args.bpcs.split(","):
         if b:
             mk(f"full5_bpc{b}", force_levels=5, blocks_per_cu=int(b))
@@ -102,7 +113,7 @@ def main():
         return ring[i * B * fbytes:(i + 1) * B * fbytes].view(torch.int64).sum()
 
     bytes_moved = {
-        **{f"full5_rh{rh}_nt{nt}": B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64 + 1 / 256)) for rh in args.rh.split(",") for nt in args.nt.split(",")},
+        **{f"full5_rh{rh}_nt{nt}_{j}": B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64 + 1 / 256)) for rh in args.rh.split(",") for j, nt in enumerate(args.nt.split(","))},
         **{f"pyr5_rh{rh}": B * fbytes * (1 + (1 / 4 + 1 / 16 + 1 / 64 + 1 / 256)) for rh in args.rh.split(",")},
         "split_only": B * fbytes * 2,
         "full4_refrule": B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64)),
@@ -119,7 +130,7 @@ def main():
     print(f"{'variant':16s} {'ms/64fr':>9s} {'in GB/s':>9s} {'bus GB/s':>9s}")
     for k, v in res.items():
         ms = min(v)
-        print(f"{k:16s} {ms:9.4f} {B * fbytes / ms / 1e6:9.1f} {bytes_moved[k] / ms / 1e6:9.1f}")
+        print(f"{k:20s} {ms:9.4f} {B * fbytes / ms / 1e6:9.1f} {bytes_moved[k] / ms / 1e6:9.1f}")
     for st in variants.values():
         st.close()
 
