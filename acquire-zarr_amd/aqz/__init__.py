@@ -143,6 +143,7 @@ def lib():
         "aqz_stage_level_dims": ([vp, u32, D, sz, C.POINTER(sz)], i32),
         "aqz_stage_level_layout": ([vp, u32, C.POINTER(LevelLayoutC)], i32),
         "aqz_stage_set_stream": ([vp, vp], i32),
+        "aqz_stage_set_tuning": ([vp, u32, u32], i32),
         "aqz_stage_append": ([vp, vp, u64, i32], i32),
         "aqz_stage_synchronize": ([vp], i32),
         "aqz_stage_frames_written": ([vp, u32], u64),
@@ -410,6 +411,9 @@ class Stage:
 
     def set_stream(self, stream_ptr):
         _check(lib().aqz_stage_set_stream(self.h, stream_ptr), "set_stream")
+
+    def set_tuning(self, knobs=0, nt=0):
+        _check(lib().aqz_stage_set_tuning(self.h, knobs, nt), "set_tuning")
 
     def append(self, frames, n_frames=None):
         p, mem = _ptr(frames)

@@ -450,6 +450,14 @@ aqz_stage_level_layout(const aqz_stage* st, uint32_t level,
 }
 
 aqz_status
+aqz_stage_set_tuning(aqz_stage* st, uint32_t knobs, uint32_t nt)
+{
+    if (!st)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard([&] { st->st->set_tuning(knobs, nt); });
+}
+
+aqz_status
 aqz_stage_set_stream(aqz_stage* st, void* stream)
 {
     return guard_sticky(

@@ -770,6 +770,9 @@ Stage::fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
     p.knobs = knobs_;
     p.nbx_in = p.fast_ok ? L0.W / RW : 0;
     p.nby_in = p.fast_ok ? L0.H >> rh_log2 : 0;
+    // XCD-contiguous region order pays on large launches (A/B: C2 -4.5%,
+    // C5 -3.5%, C3 even) and not on small ones (C1 +4%)
+    p.xcd_order = (uint64_t(n) * p.nbx_in * p.nby_in >= 8192 && !(knobs_ & 64u)) ? 1 : 0;
     p.d_nreg_in = make_fastdiv(std::max<uint32_t>(1, p.nbx_in * p.nby_in));
     p.d_nbx_in = make_fastdiv(std::max<uint32_t>(1, p.nbx_in));
     p.tw = L0.tw;

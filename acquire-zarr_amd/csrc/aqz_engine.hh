@@ -146,6 +146,7 @@ class Stage
     const std::vector<Dim>& level_dims(uint32_t level) const;
     LevelLayout layout(uint32_t level) const;
     void set_stream(hipStream_t s);
+    void set_tuning(uint32_t knobs, uint32_t nt) { knobs_ = knobs; nt_mode_ = nt & 7u; }
     void append(const void* frames, uint64_t n_frames, int mem);
     void synchronize();
     uint64_t frames_written(uint32_t level) const;

@@ -793,6 +793,20 @@ fast_pass(const FusedParams& p, uint32_t pass, const uint4& ra, const uint4& rb,
     }
 }
 
+// Workgroups are dealt round-robin over the 8 XCDs (block b -> XCD b mod 8).
+// With xcd_order, the blocks of one XCD walk one contiguous eighth of the
+// launch's regions, so horizontally adjacent regions -- whose level >= 3
+// rows share cache lines -- meet in the same L2 and leave it as whole lines.
+__device__ __forceinline__ uint32_t
+region_of_block(const FusedParams& p)
+{
+    const uint32_t b = blockIdx.x;
+    if (!p.xcd_order)
+        return b;
+    const uint32_t per = gridDim.x >> 3;
+    return b < (per << 3) ? (b & 7u) * per + (b >> 3) : b;
+}
+
 // Interior regions, one per workgroup (region r of n_frames * nby_in * nbx_in).
 // The rows of up to kPassBatch passes are loaded before any is reduced, so a
 // wave keeps its whole region in flight; then level 0 goes to its tiles,
@@ -810,7 +824,7 @@ fused_pyramid(const FusedParams p)
     __shared__ __attribute__((aligned(16))) T lds_a[(kMaxRegionRows / 2) * (RW / 2)];
     __shared__ __attribute__((aligned(16))) T lds_b[(kMaxRegionRows / 4) * (RW / 4)];
 
-    const uint32_t r = blockIdx.x;
+    const uint32_t r = region_of_block(p);
     const uint32_t f = fdiv(r, p.d_nreg_in);
     const uint32_t q = r - f * (p.nbx_in * p.nby_in);
     const uint32_t by = fdiv(q, p.d_nbx_in);
@@ -845,6 +859,177 @@ fused_pyramid(const FusedParams p)
     }
     if (!(p.knobs & 16u))
         lean_levels<T, M, RW>(p, f, y0, x0, lds_a, lds_b);
+}
+
+// ---------------------------------------------------------------------------
+// Interior regions of 64 rows with pixels of <= 4 bytes ("strip" kernel).
+// Wave w owns the region's rows [16w, 16w+16): level 1 is a 2x2 in
+// registers, level 2 meets the row below through a lane^32 swap, and levels
+// 3 and 4 combine level-2 rows that the same lane already holds (rows of
+// different passes) and columns of the same or a neighbouring lane -- so the
+// cascade down to level 4 needs no LDS and no barrier.  Only pyramids deeper
+// than 4 levels hand their one level-4 row per wave to LDS for levels 5-6.
+// ---------------------------------------------------------------------------
+template<typename T, int M>
+__global__ __launch_bounds__(256) void
+fused_pyramid_strip(const FusedParams p)
+{
+    constexpr int VEC = 16 / sizeof(T); // pixels per 16-B row vector
+    constexpr int HV = VEC / 2;         // level-1 pixels per lane
+    constexpr int QV = VEC / 4;         // level-2 pixels per lane
+    constexpr uint32_t RW = 32 * VEC;   // region width
+    static_assert(QV >= 1, "strip kernel needs <= 4-byte pixels");
+    // level 3: N3 pixels per lane, one lane in S3 holds pixels
+    constexpr int N3 = QV >= 2 ? QV / 2 : 1;
+    constexpr int S3 = QV >= 2 ? 1 : 2;
+    constexpr int N4 = N3 >= 2 ? N3 / 2 : 1;
+    constexpr int S4 = N3 >= 2 ? S3 : 2 * S3;
+    __shared__ __attribute__((aligned(16))) T lds4[4 * (RW / 16)];
+    __shared__ __attribute__((aligned(16))) T lds5[2 * (RW / 32)];
+
+    const uint32_t r = region_of_block(p);
+    const uint32_t f = fdiv(r, p.d_nreg_in);
+    const uint32_t q = r - f * (p.nbx_in * p.nby_in);
+    const uint32_t by = fdiv(q, p.d_nbx_in);
+    const uint32_t y0 = by << 6;
+    const uint32_t x0 = (q - by * p.nbx_in) * RW;
+    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t hw = (threadIdx.x >> 5) & 1u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t cv = threadIdx.x & 31u;
+    const uint32_t trow = p.tw * uint32_t(sizeof(T)); // bytes per tile row
+    const uint32_t nf = p.n_fused;
+
+    // this half-wave's rows: y0 + ry + 4i + {0, 1}, i = 0..3
+    const uint32_t ry = 16 * w + 2 * hw;
+    uint4 ra[4], rb[4];
+    {
+        const uint64_t row = uint64_t(p.W[0]) * sizeof(T);
+        const uint8_t* s = p.src + uint64_t(f) * p.src_stride + uint64_t(y0 + ry) * row +
+                           uint64_t(x0 + cv * VEC) * sizeof(T);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            ra[i] = ld16(s + uint64_t(4 * i) * row, p.nt & 1);
+            rb[i] = ld16(s + uint64_t(4 * i + 1) * row, p.nt & 1);
+        }
+    }
+    FastTile t0 = fast_tile<T>(p, 0, f, y0 + ry, x0 + cv * VEC);
+    FastTile t1{}, t2{};
+    if (nf >= 1)
+        t1 = fast_tile<T>(p, 1, f, (y0 >> 1) + 8 * w + hw, (x0 >> 1) + cv * HV);
+    if (nf >= 2)
+        t2 = fast_tile<T>(p, 2, f, (y0 >> 2) + 4 * w, (x0 >> 2) + cv * QV);
+    T q2[4][QV]; // level-2 rows 4w + i (meaningful in lanes < 32)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (t0.p) {
+            st16(t0.p + uint64_t(4 * i) * trow, ra[i], p.nt & 2);
+            st16(t0.p + uint64_t(4 * i + 1) * trow, rb[i], p.nt & 2);
+            t0.nz |= ((ra[i].x | ra[i].y | ra[i].z | ra[i].w) |
+                      (rb[i].x | rb[i].y | rb[i].z | rb[i].w)) != 0u;
+        }
+        if (nf < 1)
+            continue;
+        T r0[VEC], r1[VEC], o[HV];
+        __builtin_memcpy(r0, &ra[i], 16);
+        __builtin_memcpy(r1, &rb[i], 16);
+#pragma unroll
+        for (int j = 0; j < HV; ++j)
+            o[j] = reduce4<M, T>(r0[2 * j], r0[2 * j + 1], r1[2 * j], r1[2 * j + 1]);
+        if (t1.p) {
+            store_vec<T, HV>(t1.p + uint64_t(2 * i) * trow, o, p.nt & 4);
+            t1.nz |= any_nonzero<T, HV>(o);
+        }
+        if (nf < 2)
+            continue;
+        // the level-1 row below lives in lane ^ 32 (HV * sizeof(T) = 8 bytes)
+        uint2 mine, below;
+        __builtin_memcpy(&mine, o, 8);
+        below.x = __shfl_xor(mine.x, 32);
+        below.y = __shfl_xor(mine.y, 32);
+        T b[HV];
+        __builtin_memcpy(b, &below, 8);
+#pragma unroll
+        for (int j = 0; j < QV; ++j)
+            q2[i][j] = reduce4<M, T>(o[2 * j], o[2 * j + 1], b[2 * j], b[2 * j + 1]);
+        if (lane < 32 && t2.p) {
+            store_vec<T, QV>(t2.p + uint64_t(i) * trow, q2[i], p.nt & 4);
+            t2.nz |= any_nonzero<T, QV>(q2[i]);
+        }
+    }
+    flush_tile_flag(t0);
+    flush_tile_flag(t1);
+    flush_tile_flag(t2);
+    if (nf < 3 || (p.knobs & 8u))
+        return;
+
+    // level 3: rows 2w + r from level-2 rows 2r, 2r+1 of this lane
+    T v3[2][N3];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+        const T* a = q2[2 * rr];
+        const T* c = q2[2 * rr + 1];
+        if constexpr (QV >= 2) {
+#pragma unroll
+            for (int j = 0; j < N3; ++j)
+                v3[rr][j] = reduce4<M, T>(a[2 * j], a[2 * j + 1], c[2 * j], c[2 * j + 1]);
+        } else {
+            const T ar = shfl_down_t(a[0], 1), cr = shfl_down_t(c[0], 1);
+            v3[rr][0] = reduce4<M, T>(a[0], ar, c[0], cr);
+        }
+    }
+    {
+        const bool valid = lane < 32 && (cv % S3) == 0;
+        FastTile t3{};
+        if (valid)
+            t3 = fast_tile<T>(p, 3, f, (y0 >> 3) + 2 * w, (x0 >> 3) + (cv / S3) * N3);
+        if (t3.p) {
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr) {
+                store_vec<T, N3>(t3.p + uint64_t(rr) * trow, v3[rr]);
+                t3.nz |= any_nonzero<T, N3>(v3[rr]);
+            }
+        }
+        flush_tile_flag(t3);
+    }
+    if (nf < 4)
+        return;
+
+    // level 4: row w
+    T v4[N4];
+    if constexpr (N3 >= 2) {
+#pragma unroll
+        for (int j = 0; j < N4; ++j)
+            v4[j] = reduce4<M, T>(v3[0][2 * j], v3[0][2 * j + 1], v3[1][2 * j],
+                                  v3[1][2 * j + 1]);
+    } else {
+        const T ar = shfl_down_t(v3[0][0], S3), cr = shfl_down_t(v3[1][0], S3);
+        v4[0] = reduce4<M, T>(v3[0][0], ar, v3[1][0], cr);
+    }
+    const bool valid4 = lane < 32 && (cv % S4) == 0;
+    {
+        FastTile t4{};
+        if (valid4)
+            t4 = fast_tile<T>(p, 4, f, (y0 >> 4) + w, (x0 >> 4) + (cv / S4) * N4);
+        if (t4.p) {
+            store_vec<T, N4>(t4.p, v4);
+            t4.nz |= any_nonzero<T, N4>(v4);
+        }
+        flush_tile_flag(t4);
+    }
+    if (nf < 5)
+        return;
+    // levels 5-6 across the waves, from the level-4 rows in LDS
+    if (valid4) {
+#pragma unroll
+        for (int j = 0; j < N4; ++j)
+            lds4[w * (RW / 16) + (cv / S4) * N4 + j] = v4[j];
+    }
+    __syncthreads();
+    if (nf == 5)
+        lean_level<T, M, 5, RW>(p, f, y0, x0, lds4, lds5);
+    else
+        lean_pair<T, M, 5, RW>(p, f, y0, x0, lds4);
 }
 
 // Edge regions (right column strip, bottom row strip; or every region when
@@ -967,8 +1152,9 @@ fused_pyramid_3d(const FusedParams p)
     T lds_b[kMaxPlanes3d / 2 * (kMaxRegionRows / 4) * (RW / 4)];
 
     const uint32_t nreg = p.nbx_in * p.nby_in;
-    const uint32_t grp = fdiv(blockIdx.x, p.d_nreg_in);
-    const uint32_t r = blockIdx.x - grp * nreg;
+    const uint32_t blk = region_of_block(p);
+    const uint32_t grp = fdiv(blk, p.d_nreg_in);
+    const uint32_t r = blk - grp * nreg;
     const uint32_t by = fdiv(r, p.d_nbx_in);
     const uint32_t y0 = by << p.rh_log2;
     const uint32_t x0 = (r - by * p.nbx_in) * RW;
@@ -1203,6 +1389,23 @@ zero_frame_tiles(uint8_t* fb, uint64_t bpc, uint32_t n_tiles,
         default: return hipErrorInvalidValue;                                  \
     }
 
+// The strip kernel takes 64-row interior regions of <= 4-byte pixels when
+// no level 3-4 output goes to scratch; fused_pyramid takes the rest.
+template<typename T, int M>
+void
+launch_interior(uint32_t blocks, const FusedParams& p, hipStream_t stream)
+{
+    if constexpr (sizeof(T) <= 4) {
+        if (p.rh_log2 == 6 && p.n_fused >= 3 && !(p.knobs & 128u) &&
+            (p.scratch_level == 0 || p.scratch_level >= 5)) {
+            hipLaunchKernelGGL((fused_pyramid_strip<T, M>), dim3(blocks), dim3(256), 0,
+                               stream, p);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((fused_pyramid<T, M>), dim3(blocks), dim3(256), 0, stream, p);
+}
+
 hipError_t
 launch_fused_pyramid(int dtype, int method, const FusedParams& p,
                      hipStream_t stream)
@@ -1218,11 +1421,8 @@ launch_fused_pyramid(int dtype, int method, const FusedParams& p,
         return hipErrorInvalidValue;
 #define CALL(T, MM)                                                            \
     do {                                                                       \
-        if (interior) {                                                        \
-            const uint32_t blocks = uint32_t(interior);                        \
-            hipLaunchKernelGGL((fused_pyramid<T, MM>), dim3(blocks), dim3(256),\
-                               0, stream, p);                                  \
-        }                                                                      \
+        if (interior)                                                          \
+            launch_interior<T, MM>(uint32_t(interior), p, stream);             \
         if (edge)                                                              \
             hipLaunchKernelGGL((fused_pyramid_edge<T, MM>),                    \
                                dim3(uint32_t(edge)), dim3(256), 0, stream, p); \

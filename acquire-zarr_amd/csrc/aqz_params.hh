@@ -87,6 +87,7 @@ struct FusedParams
     uint32_t fast_ok;        // 1: tiles fit the interior fast path
     uint32_t nt;             // bit0: non-temporal input loads, bit1: nt level-0 stores
     uint32_t knobs;          // tuning A/B switches (0 = shipped defaults)
+    uint32_t xcd_order;      // 1: interior regions walk XCD-contiguous ranges
     uint32_t G;              // 2x2x2 kernel: level-0 planes per group
     uint32_t zmask;          // 2x2x2 kernel: bit k = level k halves z
     uint32_t tw, th;         // chunk tile (x, y) in pixels

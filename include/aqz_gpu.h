@@ -238,6 +238,8 @@ aqz_status aqz_stage_level_layout(const aqz_stage* st, uint32_t level,
 /* Run the stage on the HIP stream `stream` (a hipStream_t; NULL = the
  * stage's own stream).  All later work is enqueued there. */
 aqz_status aqz_stage_set_stream(aqz_stage* st, void* stream);
+/* Kernel A/B switches for tuning runs (0, 0 = the shipped kernels). */
+aqz_status aqz_stage_set_tuning(aqz_stage* st, uint32_t knobs, uint32_t nt);
 /* Append n_frames full level-0 frames (contiguous, frame after frame).
  * Equivalent to n_frames calls of MultiscaleArray::write_frame.
  *  - AQZ_MEM_HOST: copied into a pinned staging buffer by a few host threads

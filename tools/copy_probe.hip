@@ -120,6 +120,27 @@ main()
     auto s = (const u32x4*)src;
     auto d = (u32x4*)dst;
     auto d2 = (u32x4*)dst2;
+    if (getenv("PROBE_ALLOCS")) {
+        // bimodality check: the same copy into several separately
+        // allocated destinations
+        const int na = atoi(getenv("PROBE_ALLOCS"));
+        std::vector<void*> ds(na), ds2(na);
+        for (int i = 0; i < na; ++i) {
+            CK(hipMalloc(&ds[i], bytes));
+            CK(hipMalloc(&ds2[i], bytes));
+            CK(hipMemset(ds[i], 0, bytes));
+            CK(hipMemset(ds2[i], 0, bytes));
+        }
+        for (int rep = 0; rep < 2; ++rep)
+            for (int i = 0; i < na; ++i) {
+                char nm[64];
+                snprintf(nm, sizeof nm, "copy+1/3 dst%d", i);
+                run<6, false, false, 2>(nm, s, (u32x4*)ds[i], (u32x4*)ds2[i], bytes, sink, ring);
+                snprintf(nm, sizeof nm, "copy dst%d", i);
+                run<4, false, false, 1>(nm, s, (u32x4*)ds[i], (u32x4*)ds2[i], bytes, sink, ring);
+            }
+        return 0;
+    }
     for (int rep = 0; rep < 2; ++rep) {
         run<4, false, false, 0>("read", s, d, d2, bytes, sink, ring);
         run<8, false, false, 0>("read", s, d, d2, bytes, sink, ring);

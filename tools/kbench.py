@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--depth", action="store_true")
     ap.add_argument("--nt", default="0")
     ap.add_argument("--pads", default="")
+    ap.add_argument("--full4", action="store_true")
     ap.add_argument("--prealloc-gb", type=float, default=0)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -71,13 +72,14 @@ def main():
         mk(f"pyr5_rh{rh}", force_levels=5, skip_level0_split=True)
     os.environ.pop("AQZ_REGION_ROWS_LOG2")
     os.environ.pop("AQZ_NT")
-    for kn in args.knobs.split(","):
+    for j, kn in enumerate(args.knobs.split(",")):
         if kn:
             os.environ["AQZ_KNOBS"] = kn
-            mk(f"full5_k{kn}", force_levels=5)
-            mk(f"full4_k{kn}", force_levels=4)
-            bytes_moved_extra[f"full5_k{kn}"] = B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64 + 1 / 256))
-            bytes_moved_extra[f"full4_k{kn}"] = B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64))
+            mk(f"full5_k{kn}_{j}", force_levels=5)
+            bytes_moved_extra[f"full5_k{kn}_{j}"] = B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64 + 1 / 256))
+            if args.full4:
+                mk(f"full4_k{kn}_{j}", force_levels=4)
+                bytes_moved_extra[f"full4_k{kn}_{j}"] = B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64))
             os.environ.pop("AQZ_KNOBS")
     for j, pad in enumerate(args.pads.split(",")):
         if pad:
