@@ -342,8 +342,8 @@ def run_paced(torch, aqz, dev, cfg, args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -352,8 +352,8 @@ def main():
     ap.add_argument("--no-pyramid-only-line", action="store_true",
                     help="do not add the pyramid-only side measurement")
     ap.add_argument("--no-kernel-events", action="store_true",
-                    help="diagnostic: time the region without per-launch HIP events "
-                         "(roofline.achieved then uses the wall time per launch)")
+                    help="diagnostic: roofline.achieved from the wall time per launch "
+                         "instead of the HIP events bracketing the timed region")
     ap.add_argument("--fps", type=float, default=0.0,
                     help="with --e2e pinned: a simulated camera delivering frames "
                          "at this rate into a pinned ring (SURVEY 8d, C3 @ 500 fps); "
@@ -420,10 +420,16 @@ def main():
         if dist:
             dist.barrier()
         torch.cuda.synchronize(dev)
-        st.enable_kernel_timing(not args.no_kernel_events)
+        # HIP events bracket the timed region on the stage's stream (torch's
+        # current stream): per-launch event pairs would add ~10 us of gap
+        # per launch to the very wall time being measured
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        ev0.record()
         for s in range(steps):
             step(warmup + s)
+        ev1.record()
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         if dist:
@@ -433,9 +439,9 @@ def main():
             t = torch.tensor([elapsed], dtype=torch.float64, device=reduce_dev(dist, dev))
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-        kms, launches = st.kernel_timing()
+        kms, launches = ev0.elapsed_time(ev1), steps
         if args.no_kernel_events:
-            kms, launches = elapsed * 1e3, steps
+            kms = elapsed * 1e3
         kernel = st.dominant_kernel()
         st.close()
         del ring
