@@ -64,6 +64,13 @@ class StageOptionsC(C.Structure):
                 ("blocks_per_cu", C.c_uint32), ("first_frame", C.c_uint64)]
 
 
+class CompressionC(C.Structure):
+    _fields_ = [("codec", C.c_int32), ("clevel", C.c_int32), ("shuffle", C.c_int32)]
+
+
+CODEC_NONE, CODEC_BLOSC_LZ4, CODEC_BLOSC_ZSTD, CODEC_ZSTD = 0, 1, 2, 3
+
+
 class LevelLayoutC(C.Structure):
     _fields_ = [("bytes_per_chunk", C.c_uint64),
                 ("chunks_per_layer", C.c_uint32), ("layer_slots", C.c_uint32),
@@ -158,6 +165,14 @@ def lib():
         "aqz_stage_enable_kernel_timing": ([vp, i32], i32),
         "aqz_stage_kernel_timing": ([vp, C.POINTER(C.c_double), C.POINTER(u64)], i32),
         "aqz_stage_dominant_kernel": ([vp], C.c_char_p),
+        "aqz_stage_compress_layer": ([vp, u32, u64, C.POINTER(CompressionC)], i32),
+        "aqz_stage_compressed_offsets": ([vp, u32, u64, C.POINTER(u64), sz], i32),
+        "aqz_stage_copy_compressed_async": ([vp, u32, u64, vp, sz], i32),
+        "aqz_compressor_create": ([u64, u32, C.POINTER(CompressionC), C.POINTER(vp)], i32),
+        "aqz_compressor_destroy": ([vp], None),
+        "aqz_compressor_max_bytes": ([u64, u32], u64),
+        "aqz_compressor_run": ([vp, vp, u64, u32, vp, sz, vp, vp], i32),
+        "aqz_compressor_blocksize": ([vp], u32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -468,3 +483,62 @@ class Stage:
 
     def dominant_kernel(self):
         return lib().aqz_stage_dominant_kernel(self.h).decode()
+
+    # ---- device compression of resident layers ----------------------------
+    def compress_layer(self, level, layer, codec=CODEC_BLOSC_LZ4, clevel=5, shuffle=1):
+        c = CompressionC(codec, clevel, shuffle)
+        _check(lib().aqz_stage_compress_layer(self.h, level, layer, C.byref(c)),
+               "compress_layer")
+
+    def compressed_offsets(self, level, layer):
+        n = self.layout(level)["chunks_per_layer"] + 1
+        off = np.empty(n, dtype=np.uint64)
+        _check(lib().aqz_stage_compressed_offsets(
+            self.h, level, layer, off.ctypes.data_as(C.POINTER(C.c_uint64)), n),
+            "compressed_offsets")
+        return off
+
+    def copy_compressed_async(self, level, layer, dst_ptr, cap):
+        _check(lib().aqz_stage_copy_compressed_async(self.h, level, layer, dst_ptr, cap),
+               "copy_compressed_async")
+
+    def copy_compressed(self, level, layer):
+        """(frames bytes, offsets) of a compressed layer, synchronously."""
+        off = self.compressed_offsets(level, layer)
+        out = np.empty(max(1, int(off[-1])), dtype=np.uint8)
+        self.copy_compressed_async(level, layer, out.ctypes.data, out.nbytes)
+        self.wait_copies()
+        return out[:int(off[-1])], off
+
+
+class Compressor:
+    """blosc1/LZ4 frames of device-resident chunks (aqz_compressor_*)."""
+
+    def __init__(self, chunk_bytes, typesize, codec=CODEC_BLOSC_LZ4, clevel=5, shuffle=1):
+        c = CompressionC(codec, clevel, shuffle)
+        h = C.c_void_p()
+        _check(lib().aqz_compressor_create(chunk_bytes, typesize, C.byref(c), C.byref(h)),
+               "aqz_compressor_create")
+        self.h = h
+        self.chunk_bytes = chunk_bytes
+
+    def close(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.aqz_compressor_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    @property
+    def blocksize(self):
+        return lib().aqz_compressor_blocksize(self.h)
+
+    def max_bytes(self, n_chunks):
+        return lib().aqz_compressor_max_bytes(self.chunk_bytes, n_chunks)
+
+    def run_ptr(self, chunks_ptr, pitch, n_chunks, dst_ptr, dst_cap, offsets_ptr,
+                stream_ptr=None):
+        _check(lib().aqz_compressor_run(self.h, chunks_ptr, pitch, n_chunks, dst_ptr,
+                                        dst_cap, offsets_ptr, stream_ptr),
+               "aqz_compressor_run")

@@ -23,6 +23,11 @@ struct aqz_stage
     std::unique_ptr<Stage> st;
     int32_t sticky = AQZ_STATUS_SUCCESS;
 };
+struct aqz_compressor
+{
+    std::unique_ptr<Compressor> c;
+    int32_t sticky = AQZ_STATUS_SUCCESS;
+};
 
 namespace {
 
@@ -576,3 +581,94 @@ aqz_stage_dominant_kernel(const aqz_stage* st)
 }
 
 } // extern "C"
+
+// ---- chunk compression ----------------------------------------------------
+static Compression
+to_compression(const aqz_compression* c)
+{
+    Compression k;
+    k.codec = c->codec;
+    k.clevel = c->clevel;
+    k.shuffle = c->shuffle;
+    return k;
+}
+
+aqz_status
+aqz_stage_compress_layer(aqz_stage* st, uint32_t level, uint64_t layer,
+                         const aqz_compression* comp)
+{
+    if (!comp)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard_sticky(
+      st, [&] { st->st->compress_layer(level, layer, to_compression(comp)); });
+}
+
+aqz_status
+aqz_stage_compressed_offsets(aqz_stage* st, uint32_t level, uint64_t layer,
+                             uint64_t* offsets, size_t n)
+{
+    if (!offsets)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard_sticky(
+      st, [&] { st->st->compressed_offsets(level, layer, offsets, n); });
+}
+
+aqz_status
+aqz_stage_copy_compressed_async(aqz_stage* st, uint32_t level, uint64_t layer,
+                                void* dst, size_t cap)
+{
+    if (!dst)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard_sticky(
+      st, [&] { st->st->copy_compressed_async(level, layer, dst, cap); });
+}
+
+aqz_status
+aqz_compressor_create(uint64_t chunk_bytes, uint32_t typesize,
+                      const aqz_compression* comp, aqz_compressor** out)
+{
+    if (!comp || !out)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    *out = nullptr;
+    return guard([&] {
+        auto h = std::make_unique<aqz_compressor>();
+        h->c = std::make_unique<Compressor>(chunk_bytes, typesize, to_compression(comp));
+        *out = h.release();
+    });
+}
+
+void
+aqz_compressor_destroy(aqz_compressor* c)
+{
+    delete c;
+}
+
+uint64_t
+aqz_compressor_max_bytes(uint64_t chunk_bytes, uint32_t n_chunks)
+{
+    return Compressor::max_bytes(chunk_bytes, n_chunks);
+}
+
+uint32_t
+aqz_compressor_blocksize(const aqz_compressor* c)
+{
+    return c && c->c ? c->c->geom().blocksize : 0;
+}
+
+aqz_status
+aqz_compressor_run(aqz_compressor* c, const void* chunks, uint64_t pitch,
+                   uint32_t n_chunks, void* dst, size_t dst_cap, uint64_t* offsets,
+                   void* stream)
+{
+    if (!c || !chunks || !dst || !offsets)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard_sticky(c, [&] {
+        const uint64_t nb = c->c->geom().nbytes;
+        if (pitch < nb)
+            throw Error(1, "chunk pitch below the chunk size");
+        if (dst_cap < Compressor::max_bytes(nb, n_chunks))
+            throw Error(2, "destination below aqz_compressor_max_bytes");
+        c->c->run(static_cast<const uint8_t*>(chunks), pitch, n_chunks, nullptr, 0,
+                  static_cast<uint8_t*>(dst), offsets, static_cast<hipStream_t>(stream));
+    });
+}

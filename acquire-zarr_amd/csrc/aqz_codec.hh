@@ -1,0 +1,65 @@
+// aqz_codec.hh -- device chunk compression: the blosc1
+// frame of Chunk::compress_and_take_buffer (chunk.cpp:78-106) ->
+// zarr::compress_in_place (zarr.common.cpp:106-140) ->
+// blosc_compress_ctx(clevel, shuffle, typesize, ..., "lz4", blocksize 0, 1
+// thread), produced on the GPU for a whole resident chunk layer at once.
+//
+// Output parity is at the decoded level: any blosc1 decoder returns the
+// chunk bytes.  The frame differs from c-blosc's own in two documented
+// choices -- the block size (kLz4StreamMax bytes per split stream, so a
+// stream fits in LDS; the header records it, and zarr.json says blocksize
+// 0 = "whatever the frame says") and the LZ4 match finder (parallel hash
+// probing instead of LZ4_compress_fast's sequential scan) -- so the
+// compressed bytes differ while every decoded byte is identical.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace aqz {
+
+// bytes of one LZ4-compressed stream (resident in LDS while it is encoded)
+constexpr uint32_t kLz4StreamMax = 16384;
+constexpr int kLz4HashLog = 12;
+
+// The blosc1 frame geometry shared by every chunk of a layer.
+struct BloscGeom
+{
+    uint32_t nbytes;    // chunk bytes (blosc nbytes)
+    uint32_t typesize;  // bytes per pixel
+    uint32_t shuffle;   // 0 none, 1 byte shuffle, 2 bit shuffle
+    uint32_t blocksize;
+    uint32_t nfull;     // full blocks
+    uint32_t left;      // bytes of the trailing (leftover) block, 0 = none
+    uint32_t ns_full;   // streams per full block: typesize (split) or 1
+    uint32_t spc;       // streams per chunk
+    uint32_t slot;      // scratch bytes per stream (>= its length)
+    uint32_t nblocks;
+};
+
+// Block size and split rule; throws nothing (callers validate inputs).
+BloscGeom make_blosc_geom(uint32_t nbytes, uint32_t typesize, uint32_t shuffle);
+
+struct BloscParams
+{
+    BloscGeom g;
+    const uint8_t* chunks;  // chunk c at chunks + c * pitch
+    uint64_t pitch;
+    uint32_t n_chunks;
+    const uint32_t* flags;  // has_data words (nullptr: every chunk has data)
+    uint32_t tag;           // a chunk has data iff flags[c] == tag
+    uint8_t* scratch;       // [n_chunks * spc] stream slots of g.slot bytes
+    uint32_t* ssize;        // [n_chunks * spc] bytes stored per stream
+    uint32_t* spos;         // [n_chunks * spc] record offset inside the frame
+    uint32_t* fsize;        // [n_chunks] frame bytes (0: chunk skipped)
+    uint8_t* mode;          // [n_chunks] 1: memcpyed frame
+    uint64_t* offsets;      // [n_chunks + 1] frame offsets in out; [n] = total
+    uint8_t* out;           // frames, back to back in chunk order
+    uint32_t store_only;    // clevel 0: every frame memcpyed, no LZ4
+};
+
+// Enqueue the whole layer: streams -> per-chunk layout -> offsets -> frames.
+hipError_t launch_blosc_lz4(const BloscParams& p, hipStream_t stream);
+
+} // namespace aqz

@@ -437,6 +437,9 @@ Stage::~Stage()
         for (hipEvent_t e : L.copy_ev)
             if (e)
                 (void)hipEventDestroy(e);
+        for (hipEvent_t e : L.comp_ev)
+            if (e)
+                (void)hipEventDestroy(e);
     }
 
     for (auto& pr : ev_pairs_) {
@@ -1106,6 +1109,129 @@ Stage::device_layer(uint32_t level, uint64_t layer, void** chunks,
         *chunks = L.ring.p + slot * L.slot_bytes;
     if (flags)
         *flags = reinterpret_cast<uint32_t*>(L.flags.p) + size_t(slot) * L.n_chunks;
+}
+
+// ---- device compression of resident layers ----------
+Compressor::Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compression& c)
+{
+    if (c.codec != 1)
+        throw Error(4, "only blosc-lz4 compresses on the device");
+    if (c.shuffle < 0 || c.shuffle > 2 || c.clevel < 0 || c.clevel > 9)
+        throw Error(1, "invalid compression settings");
+    if (chunk_bytes == 0 || chunk_bytes > 0x7fffffefull || typesize == 0 ||
+        typesize > 255)
+        throw Error(1, "chunk size outside the blosc1 limits");
+    g_ = make_blosc_geom(uint32_t(chunk_bytes), typesize, uint32_t(c.shuffle));
+    store_only_ = c.clevel == 0;
+}
+
+void
+Compressor::run(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
+                const uint32_t* flags, uint32_t tag, uint8_t* out, uint64_t* offsets,
+                hipStream_t stream)
+{
+    const uint64_t ns = uint64_t(n_chunks) * g_.spc;
+    scratch_.alloc(store_only_ ? 1 : ns * g_.slot);
+    ssize_.alloc(ns * 4);
+    spos_.alloc(ns * 4);
+    fsize_.alloc(size_t(n_chunks) * 4);
+    mode_.alloc(n_chunks);
+    BloscParams p{};
+    p.g = g_;
+    p.chunks = chunks;
+    p.pitch = pitch;
+    p.n_chunks = n_chunks;
+    p.flags = flags;
+    p.tag = tag;
+    p.scratch = scratch_.p;
+    p.ssize = reinterpret_cast<uint32_t*>(ssize_.p);
+    p.spos = reinterpret_cast<uint32_t*>(spos_.p);
+    p.fsize = reinterpret_cast<uint32_t*>(fsize_.p);
+    p.mode = mode_.p;
+    p.offsets = offsets;
+    p.out = out;
+    p.store_only = store_only_ ? 1 : 0;
+    hip_check(launch_blosc_lz4(p, stream), "blosc-lz4 launch");
+}
+
+void
+Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
+{
+    if (level >= lv_.size())
+        throw Error(3, "level out of range");
+    StageLevel& L = lv_[level];
+    if (!L.ring.p)
+        throw Error(1, "level 0 split disabled for this stage");
+    const uint32_t slot = uint32_t(layer % L.n_slots);
+    if (L.slot_layer[slot] != int64_t(layer))
+        throw Error(3, "chunk layer not resident");
+    if (!L.comp || L.comp_cfg.codec != c.codec || L.comp_cfg.clevel != c.clevel ||
+        L.comp_cfg.shuffle != c.shuffle) {
+        hip_check(hipStreamSynchronize(d2h_), "hipStreamSynchronize");
+        L.comp = std::make_unique<Compressor>(L.bpc, uint32_t(bpp_), c);
+        L.comp_cfg = c;
+    }
+    if (L.cframes.empty()) {
+        L.cframes.resize(L.n_slots);
+        L.coffsets.resize(L.n_slots);
+        L.h_coffsets.resize(L.n_slots);
+        L.comp_ev.assign(L.n_slots, nullptr);
+        L.comp_layer.assign(L.n_slots, -1);
+        for (uint32_t s = 0; s < L.n_slots; ++s)
+            hip_check(hipEventCreateWithFlags(&L.comp_ev[s], hipEventDisableTiming),
+                      "hipEventCreate");
+    }
+    L.cframes[slot].alloc(Compressor::max_bytes(L.bpc, L.n_chunks));
+    L.coffsets[slot].alloc((size_t(L.n_chunks) + 1) * 8);
+    L.h_coffsets[slot].alloc((size_t(L.n_chunks) + 1) * 8);
+    // after every kernel enqueued so far; the slot's next layer waits for it
+    hip_check(hipEventRecord(L.ready_ev[slot], stream_), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(d2h_, L.ready_ev[slot], 0), "hipStreamWaitEvent");
+    L.comp->run(L.ring.p + slot * L.slot_bytes, L.pitch, L.n_chunks,
+                reinterpret_cast<const uint32_t*>(L.flags.p) + size_t(slot) * L.n_chunks,
+                uint32_t(layer / L.n_slots + 1), L.cframes[slot].p,
+                reinterpret_cast<uint64_t*>(L.coffsets[slot].p), d2h_);
+    hip_check(hipMemcpyAsync(L.h_coffsets[slot].p, L.coffsets[slot].p,
+                             (size_t(L.n_chunks) + 1) * 8, hipMemcpyDeviceToHost, d2h_),
+              "hipMemcpyAsync");
+    hip_check(hipEventRecord(L.comp_ev[slot], d2h_), "hipEventRecord");
+    hip_check(hipEventRecord(L.copy_ev[slot], d2h_), "hipEventRecord");
+    L.copy_pending[slot] = 1;
+    L.comp_layer[slot] = int64_t(layer);
+}
+
+void
+Stage::compressed_offsets(uint32_t level, uint64_t layer, uint64_t* offsets, size_t n)
+{
+    if (level >= lv_.size())
+        throw Error(3, "level out of range");
+    StageLevel& L = lv_[level];
+    const uint32_t slot = L.n_slots ? uint32_t(layer % L.n_slots) : 0;
+    if (L.comp_layer.empty() || L.comp_layer[slot] != int64_t(layer))
+        throw Error(3, "layer was not compressed (or its slot was reused)");
+    if (n < size_t(L.n_chunks) + 1)
+        throw Error(2, "offsets too small");
+    hip_check(hipEventSynchronize(L.comp_ev[slot]), "hipEventSynchronize");
+    std::memcpy(offsets, L.h_coffsets[slot].p, (size_t(L.n_chunks) + 1) * 8);
+}
+
+void
+Stage::copy_compressed_async(uint32_t level, uint64_t layer, void* dst, size_t cap)
+{
+    if (level >= lv_.size())
+        throw Error(3, "level out of range");
+    StageLevel& L = lv_[level];
+    const uint32_t slot = L.n_slots ? uint32_t(layer % L.n_slots) : 0;
+    if (L.comp_layer.empty() || L.comp_layer[slot] != int64_t(layer))
+        throw Error(3, "layer was not compressed (or its slot was reused)");
+    hip_check(hipEventSynchronize(L.comp_ev[slot]), "hipEventSynchronize");
+    const uint64_t total =
+      reinterpret_cast<const uint64_t*>(L.h_coffsets[slot].p)[L.n_chunks];
+    if (cap < total)
+        throw Error(2, "destination too small for the compressed layer");
+    memcpy_pieces(dst, L.cframes[slot].p, total, hipMemcpyDefault, d2h_);
+    hip_check(hipEventRecord(L.copy_ev[slot], d2h_), "hipEventRecord");
+    L.copy_pending[slot] = 1;
 }
 
 void

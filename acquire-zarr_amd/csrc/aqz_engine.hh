@@ -8,6 +8,7 @@
 //                     same add_frame/take_frame contract.
 #pragma once
 
+#include "aqz_codec.hh"
 #include "aqz_copy.hh"
 #include "aqz_geometry.hh"
 #include "aqz_params.hh"
@@ -69,6 +70,39 @@ struct PinnedBuf
         o.n = 0;
     }
     void alloc(size_t bytes);
+};
+
+// Chunk compression settings (ZarrCompressionSettings, zarr.types.h:112-122;
+// codec values of ZarrCompressionCodec).
+struct Compression
+{
+    int32_t codec = 0;   // 0 none, 1 blosc-lz4 (2 blosc-zstd, 3 zstd: not on device)
+    int32_t clevel = 1;  // blosc clevel; 0 stores every chunk uncompressed
+    int32_t shuffle = 1; // 0 none, 1 byte, 2 bit
+};
+
+// blosc1/LZ4 frames of arrays of equally sized device chunks (aqz_codec.hip).
+class Compressor
+{
+  public:
+    Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compression& c);
+    static uint64_t max_bytes(uint64_t chunk_bytes, uint32_t n_chunks)
+    {
+        return uint64_t(n_chunks) * (chunk_bytes + 16);
+    }
+    // Enqueue on `stream`: the frames of n_chunks chunks (chunk i at
+    // chunks + i * pitch; skipped unless flags[i] == tag when flags is
+    // given) back to back into out; offsets (device, n_chunks + 1 words)
+    // gets each frame's start and the total.
+    void run(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
+             const uint32_t* flags, uint32_t tag, uint8_t* out, uint64_t* offsets,
+             hipStream_t stream);
+    const BloscGeom& geom() const { return g_; }
+
+  private:
+    BloscGeom g_;
+    bool store_only_;
+    DevBuf scratch_, ssize_, spos_, fsize_, mode_;
 };
 
 struct ArrayDesc
@@ -134,6 +168,14 @@ struct StageLevel
     std::vector<hipEvent_t> ready_ev, copy_ev;
     std::vector<uint8_t> copy_pending;
     DevBuf flag_bytes;                     // per slot: has_data as 0/1 bytes
+    // device compression of resident layers (compress_layer): per slot the
+    // frames, their offsets (device and pinned host copy) and an event
+    std::unique_ptr<Compressor> comp;
+    Compression comp_cfg;
+    std::vector<DevBuf> cframes, coffsets;
+    std::vector<PinnedBuf> h_coffsets;
+    std::vector<hipEvent_t> comp_ev;
+    std::vector<int64_t> comp_layer;       // layer compressed in each slot
 };
 
 class Stage
@@ -159,6 +201,13 @@ class Stage
     void copy_layer_async(uint32_t level, uint64_t layer, void* dst, size_t cap,
                           uint8_t* has_data, size_t has_data_cap);
     void wait_copies();
+    // device compression of a resident layer, on the hand-off stream
+    void compress_layer(uint32_t level, uint64_t layer, const Compression& c);
+    // waits for that compression; offsets[0..n_chunks] (frame starts + total)
+    void compressed_offsets(uint32_t level, uint64_t layer, uint64_t* offsets,
+                            size_t n);
+    // D2H of the frames (offsets[n_chunks] bytes) on the hand-off stream
+    void copy_compressed_async(uint32_t level, uint64_t layer, void* dst, size_t cap);
     void finalize();
     void enable_timing(bool on);
     void timing(double* total_ms, uint64_t* launches);

@@ -286,6 +286,58 @@ void aqz_host_free(void* p);
 aqz_status aqz_stage_device_layer(aqz_stage* st, uint32_t level,
                                   uint64_t layer, void** chunks,
                                   uint32_t** has_data);
+/* ---- chunk compression on the device ----------------
+ * ZarrCompressionSettings (zarr.types.h:112-122) as applied by
+ * Chunk::compress_and_take_buffer (chunk.cpp:78-106) ->
+ * zarr::compress_in_place (zarr.common.cpp:106-140) -> blosc_compress_ctx.
+ * codec: ZarrCompressionCodec values; only AQZ_CODEC_BLOSC_LZ4 runs on the
+ * device (others -> AQZ_STATUS_NOT_YET_IMPLEMENTED).  clevel 0 stores every
+ * chunk as a memcpyed frame; levels 1-9 run the same GPU match finder.
+ * Frames decode (any blosc1 decoder) to the chunk bytes exactly; their
+ * compressed bytes differ from c-blosc's (block size, match finder). */
+#define AQZ_CODEC_NONE 0
+#define AQZ_CODEC_BLOSC_LZ4 1
+#define AQZ_CODEC_BLOSC_ZSTD 2
+#define AQZ_CODEC_ZSTD 3
+typedef struct
+{
+    int32_t codec;   /* ZarrCompressionCodec */
+    int32_t clevel;  /* 0-9 */
+    int32_t shuffle; /* 0 none, 1 byte (BLOSC_SHUFFLE), 2 bit (BLOSC_BITSHUFFLE) */
+} aqz_compression;
+
+/* Compress resident layer `layer` of `level` into blosc1 frames, one per
+ * chunk with data (chunks without data are skipped, like the reference's
+ * skip_chunk), back to back in chunk order.  Runs on the hand-off stream
+ * after the kernels that wrote the layer; the slot is not reused until it
+ * has been read. */
+aqz_status aqz_stage_compress_layer(aqz_stage* st, uint32_t level, uint64_t layer,
+                                    const aqz_compression* comp);
+/* Waits for that compression.  offsets[c] = start of chunk c's frame,
+ * offsets[c+1] - offsets[c] its size (0: skipped), offsets[chunks_per_layer]
+ * = total bytes.  n >= chunks_per_layer + 1. */
+aqz_status aqz_stage_compressed_offsets(aqz_stage* st, uint32_t level,
+                                        uint64_t layer, uint64_t* offsets, size_t n);
+/* Asynchronous copy of the layer's frames (total bytes) to dst (host or
+ * device); complete after aqz_stage_wait_copies. */
+aqz_status aqz_stage_copy_compressed_async(aqz_stage* st, uint32_t level,
+                                           uint64_t layer, void* dst, size_t cap);
+
+/* Stand-alone compressor for device-resident chunk arrays: chunk i of
+ * n_chunks at chunks + i * pitch, chunk_bytes each; frames back to back at
+ * dst (device, >= aqz_compressor_max_bytes), offsets (device, n_chunks + 1
+ * uint64) as above.  Enqueued on `stream` (hipStream_t; NULL = default). */
+typedef struct aqz_compressor aqz_compressor;
+aqz_status aqz_compressor_create(uint64_t chunk_bytes, uint32_t typesize,
+                                 const aqz_compression* comp, aqz_compressor** out);
+void aqz_compressor_destroy(aqz_compressor* c);
+uint64_t aqz_compressor_max_bytes(uint64_t chunk_bytes, uint32_t n_chunks);
+aqz_status aqz_compressor_run(aqz_compressor* c, const void* chunks, uint64_t pitch,
+                              uint32_t n_chunks, void* dst, size_t dst_cap,
+                              uint64_t* offsets, void* stream);
+/* The block size of the frames (recorded in each frame header). */
+uint32_t aqz_compressor_blocksize(const aqz_compressor* c);
+
 /* Zero the not-yet-written frames of every level's last partial layer so
  * it can be flushed (the reference's lazily zeroed chunks, chunk.cpp:8-15).
  * The unpaired trailing z plane is dropped, as in the reference. */

@@ -103,6 +103,26 @@ int or_ds_take_frame(or_downsampler* ds, int level, void* dst, size_t cap,
 uint64_t or_splitmix64(uint64_t* state);
 void or_fill_splitmix(void* dst, size_t nbytes, uint64_t seed);
 
+/* ---- chunk compression / shard index (aqz_codec_oracle.c) ------------- */
+typedef struct
+{
+    uint32_t version, versionlz, flags, typesize;
+    uint32_t nbytes, blocksize, cbytes;
+} or_blosc_info;
+
+void or_shuffle(size_t ts, size_t n, const uint8_t* src, uint8_t* dst);
+void or_unshuffle(size_t ts, size_t n, const uint8_t* src, uint8_t* dst);
+void or_bitshuffle(size_t ts, size_t n, const uint8_t* src, uint8_t* dst);
+void or_bitunshuffle(size_t ts, size_t n, const uint8_t* src, uint8_t* dst);
+/* decoded bytes (== dsize) or -1 */
+long or_lz4_decompress(const uint8_t* src, size_t csize, uint8_t* dst,
+                       size_t dsize);
+int or_blosc_frame_info(const uint8_t* src, size_t srcsize, or_blosc_info* info);
+/* nbytes or < 0; tmp holds one block */
+long or_blosc_decompress(const uint8_t* src, size_t srcsize, uint8_t* dst,
+                         size_t dstcap, uint8_t* tmp);
+uint32_t or_crc32c(const uint8_t* p, size_t n);
+
 #ifdef __cplusplus
 }
 #endif
