@@ -137,6 +137,7 @@ gather_stream(const BloscGeom& g, const StreamRef& r, const uint8_t* blk, uint8_
     if (g.shuffle == 1 && ts > 1 && r.ns == ts && aligned && (ts == 2 || ts == 4 || ts == 8)) {
         // byte r.s of elements 4w .. 4w+3 -> word w
         uint32_t* sw = reinterpret_cast<uint32_t*>(sb);
+#pragma unroll 8
         for (uint32_t w = lane; w < ne / 4; w += 64) {
             uint8_t e[32];
             if (ts == 2) {
@@ -161,6 +162,7 @@ gather_stream(const BloscGeom& g, const StreamRef& r, const uint8_t* blk, uint8_
     if (g.shuffle == 2 && r.ns == ts && ne % 8 == 0 && ne * ts == r.bsize) {
         // stream r.s = the 8 bit-planes of byte r.s of every element
         const uint32_t row = ne / 8;
+#pragma unroll 4
         for (uint32_t m = lane; m < row; m += 64) {
             uint64_t x = 0;
             for (uint32_t k = 0; k < 8; ++k)
@@ -176,54 +178,68 @@ gather_stream(const BloscGeom& g, const StreamRef& r, const uint8_t* blk, uint8_
         sb[k] = shuffled_byte(blk, r.bsize, ts, g.shuffle, x0 + k);
 }
 
-// ---- LZ4 sequence emission (uniform control; lanes share the byte work) --
-__device__ __forceinline__ void
-put_len_ext(uint8_t* d, uint32_t n_ext, uint32_t rest)
+// ---- LZ4 encoder: one wave per stream -----------------------------------
+// Wave-wide inclusive prefix sum.
+__device__ __forceinline__ uint32_t
+wave_incl_scan(uint32_t x)
 {
-    // n_ext bytes: 255 ... 255, then rest - 255 * (n_ext - 1)
-    for (uint32_t k = threadIdx.x; k < n_ext; k += 64)
-        d[k] = k + 1 < n_ext ? 255 : uint8_t(rest - 255 * (n_ext - 1));
+    const uint32_t lane = threadIdx.x & 63u;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (int(lane) >= d)
+            x += y;
+    }
+    return x;
 }
 
-__device__ __forceinline__ bool
-emit_sequence(uint8_t* dst, uint32_t& op, uint32_t cap, const uint8_t* sb, uint32_t lit0,
-              uint32_t litlen, uint32_t off, uint32_t mlen, bool last)
+// value of lane i (wave-uniform i): v_readlane, no LDS round trip
+__device__ __forceinline__ uint32_t
+rdlane(uint32_t v, uint32_t i)
 {
-    const uint32_t ml = last ? 0 : mlen - 4;
-    const uint32_t le = litlen >= 15 ? (litlen - 15) / 255 + 1 : 0;
-    const uint32_t me = (!last && ml >= 15) ? (ml - 15) / 255 + 1 : 0;
-    const uint32_t need = 1 + le + litlen + (last ? 0 : 2 + me);
-    if (op + need > cap)
-        return false;
-    uint8_t* d = dst + op;
-    if (threadIdx.x == 0)
-        d[0] = uint8_t((litlen < 15 ? litlen : 15) << 4 |
-                       (last ? 0 : (ml < 15 ? ml : 15)));
-    put_len_ext(d + 1, le, litlen - 15);
-    uint8_t* lit = d + 1 + le;
-    for (uint32_t k = threadIdx.x; k < litlen; k += 64)
-        lit[k] = sb[lit0 + k];
-    if (!last) {
-        uint8_t* o = lit + litlen;
-        if (threadIdx.x == 0) {
-            o[0] = uint8_t(off & 255u);
-            o[1] = uint8_t(off >> 8);
-        }
-        put_len_ext(o + 2, me, ml - 15);
-    }
-    op += need;
-    return true;
+    return uint32_t(__builtin_amdgcn_readlane(int(v), int(i)));
 }
+
+// Length-extension bytes: n_ext bytes 255 ... 255, then the remainder.
+__device__ __forceinline__ void
+put_len_ext_lane(uint8_t* d, uint32_t n_ext, uint32_t rest)
+{
+    for (uint32_t k = 0; k + 1 < n_ext; ++k)
+        d[k] = 255;
+    if (n_ext)
+        d[n_ext - 1] = uint8_t(rest - 255 * (n_ext - 1));
+}
+
+// Copies n stream bytes sb[s0..) to d with the whole wave.
+__device__ __forceinline__ void
+copy_lits(uint8_t* d, const uint8_t* sb, uint32_t s0, uint32_t n)
+{
+    for (uint32_t k = threadIdx.x; k < n; k += 64)
+        d[k] = sb[s0 + k];
+}
+
+constexpr uint32_t kLenCap = 32; // match bytes measured per position up front
+constexpr uint32_t kWin = 4;     // 64-position windows probed per batch
+constexpr uint32_t kShortLits = 16; // literal runs copied by one lane
 
 // LZ4 block of sb[0, L) -> dst; returns the compressed size, or 0 when it
 // would not be smaller than L - 1 bytes (the caller then stores the stream
 // raw, which blosc signals by csize == L).
+//
+// Per 64-position window: (A) every lane hashes its position, probes the
+// table (any earlier position with the same hash is a valid candidate, so
+// concurrent table stores may land in any order), verifies 4 bytes and
+// measures the match up to kLenCap bytes with word compares; (B) the wave
+// walks the ballot of match starts greedily with scalar steps, extending
+// only matches that reached kLenCap (64 bytes per ballot), and records the
+// window's sequences one per lane; (C) the sequences are encoded in
+// parallel: a wave scan places them, each lane writes its token, lengths
+// and offset, and the wave copies the literal runs.
 __device__ uint32_t
-lz4_wave(const uint8_t* sb, const uint32_t* sw, uint32_t L, uint32_t* table, uint8_t* dst)
+lz4_wave(const uint8_t* sb, const uint32_t* sw, uint32_t L, uint16_t* table, uint8_t* dst)
 {
     const uint32_t lane = threadIdx.x;
-    for (uint32_t i = lane; i < kHashSize; i += 64)
-        table[i] = 0;
+    for (uint32_t i = lane; i < kHashSize / 2; i += 64)
+        reinterpret_cast<uint32_t*>(table)[i] = 0;
     __syncthreads();
     if (L < 13)
         return 0;
@@ -231,62 +247,149 @@ lz4_wave(const uint8_t* sb, const uint32_t* sw, uint32_t L, uint32_t* table, uin
     const uint32_t matchlimit = L - 5; // a match ends at or before here
     const uint32_t cap = L - 1;
     uint32_t anchor = 0, p = 0, op = 0;
+    uint32_t misses = 0; // consecutive batches without a match
     for (uint32_t base = 0; base <= mflimit;) {
-        const uint32_t q = base + lane;
-        uint32_t cand = 0;
-        bool m = false;
-        if (q <= mflimit) {
-            const uint32_t v = lds_rd32(sw, q);
-            const uint32_t h = (v * 2654435761u) >> (32 - kLz4HashLog);
-            const uint32_t e = table[h];
-            atomicMax(&table[h], q + 1);
-            if (e != 0) {
-                cand = e - 1;
-                m = lds_rd32(sw, cand) == v;
-            }
-        }
-        const uint64_t M = __ballot(m);
-        while (p < base + 64) {
-            const uint32_t sh = p > base ? p - base : 0;
-            const uint64_t mm = M & (~0ull << sh);
-            if (mm == 0)
-                break;
-            const uint32_t i = uint32_t(__ffsll(static_cast<long long>(mm))) - 1;
-            uint32_t qq = base + i;
-            uint32_t cc = __shfl(cand, int(i));
-            while (qq > anchor && cc > 0 && sb[qq - 1] == sb[cc - 1]) {
-                --qq;
-                --cc;
-            }
-            uint32_t len = base + i - qq + 4;
-            for (;;) {
-                const uint32_t a = qq + len + lane;
-                const bool eq = a < matchlimit && sb[a] == sb[cc + len + lane];
-                const uint64_t miss = __ballot(!eq);
-                if (miss == 0) {
-                    len += 64;
-                    continue;
+        // (A) four 64-position windows at once: four independent probe
+        // chains per lane (a batch does not see its own table stores)
+        uint32_t cand[kWin], mlen[kWin];
+        uint64_t M[kWin];
+#pragma unroll
+        for (uint32_t k = 0; k < kWin; ++k) {
+            const uint32_t q = base + 64 * k + lane;
+            cand[k] = 0;
+            mlen[k] = 0;
+            if (q <= mflimit) {
+                const uint32_t v = lds_rd32(sw, q);
+                const uint32_t h = (v * 2654435761u) >> (32 - kLz4HashLog);
+                const uint32_t e = table[h];
+                table[h] = uint16_t(q + 1);
+                if (e != 0 && lds_rd32(sw, e - 1) == v) {
+                    const uint32_t c = e - 1;
+                    const uint32_t lim = min(matchlimit - q, kLenCap);
+                    uint32_t len = 4;
+                    bool done = false;
+                    while (len + 4 <= lim) {
+                        const uint32_t x = lds_rd32(sw, q + len) ^ lds_rd32(sw, c + len);
+                        if (x) {
+                            len += uint32_t(__builtin_ctz(x)) >> 3;
+                            done = true;
+                            break;
+                        }
+                        len += 4;
+                    }
+                    if (!done) // the last < 4 bytes up to the limit
+                        while (len < lim && sb[q + len] == sb[c + len])
+                            ++len;
+                    cand[k] = c;
+                    mlen[k] = len;
                 }
-                len += uint32_t(__ffsll(static_cast<long long>(miss))) - 1;
-                break;
             }
-            if (!emit_sequence(dst, op, cap, sb, anchor, qq - anchor, qq - cc, len, false))
-                return 0;
-            p = qq + len;
-            anchor = p;
         }
-        base = max(base + 64, p & ~63u);
+#pragma unroll
+        for (uint32_t k = 0; k < kWin; ++k)
+            M[k] = __ballot(mlen[k] != 0);
+        // (B)
+        uint32_t s_lit0 = 0, s_lit = 0, s_off = 0, s_len = 4; // lane k: sequence k
+        uint32_t nseq = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kWin; ++k) {
+            const uint32_t wb = base + 64 * k;
+            while (p < wb + 64) {
+                const uint32_t sh = p > wb ? p - wb : 0;
+                const uint64_t mm = M[k] & (~0ull << sh);
+                if (mm == 0)
+                    break;
+                const uint32_t i = uint32_t(__ffsll(static_cast<long long>(mm))) - 1;
+                const uint32_t qq = wb + i;
+                const uint32_t cc = rdlane(cand[k], i);
+                uint32_t len = rdlane(mlen[k], i);
+                if (len == kLenCap) {
+                    for (;;) {
+                        const uint32_t a = qq + len + lane;
+                        const bool eq = a < matchlimit && sb[a] == sb[cc + len + lane];
+                        const uint64_t miss = __ballot(!eq);
+                        if (miss == 0) {
+                            len += 64;
+                            continue;
+                        }
+                        len += uint32_t(__ffsll(static_cast<long long>(miss))) - 1;
+                        break;
+                    }
+                }
+                if (lane == nseq) {
+                    s_lit0 = anchor;
+                    s_lit = qq - anchor;
+                    s_off = qq - cc;
+                    s_len = len;
+                }
+                ++nseq;
+                p = qq + len;
+                anchor = p;
+            }
+        }
+        // (C)
+        if (nseq) {
+            const bool mine = lane < nseq;
+            const uint32_t ml = s_len - 4;
+            const uint32_t le = s_lit >= 15 ? (s_lit - 15) / 255 + 1 : 0;
+            const uint32_t me = ml >= 15 ? (ml - 15) / 255 + 1 : 0;
+            const uint32_t sz = mine ? 1 + le + s_lit + 2 + me : 0;
+            const uint32_t incl = wave_incl_scan(sz);
+            const uint32_t total = rdlane(incl, nseq - 1);
+            if (op + total > cap)
+                return 0;
+            if (mine) {
+                uint8_t* d = dst + op + incl - sz;
+                d[0] = uint8_t((s_lit < 15 ? s_lit : 15) << 4 | (ml < 15 ? ml : 15));
+                put_len_ext_lane(d + 1, le, s_lit - 15);
+                uint8_t* o = d + 1 + le + s_lit;
+                o[0] = uint8_t(s_off & 255u);
+                o[1] = uint8_t(s_off >> 8);
+                put_len_ext_lane(o + 2, me, ml - 15);
+            }
+            // literal runs: short ones by their own lane, long ones by the wave
+            if (mine && s_lit <= kShortLits) {
+                uint8_t* d = dst + op + incl - sz + 1 + le;
+                for (uint32_t k = 0; k < s_lit; ++k)
+                    d[k] = sb[s_lit0 + k];
+            }
+            uint64_t longs = __ballot(mine && s_lit > kShortLits);
+            while (longs) {
+                const uint32_t k = uint32_t(__ffsll(static_cast<long long>(longs))) - 1;
+                longs &= longs - 1;
+                const uint32_t n = rdlane(s_lit, k);
+                const uint32_t start = rdlane(incl - sz, k);
+                const uint32_t lel = (n - 15) / 255 + 1;
+                copy_lits(dst + op + start + 1 + lel, sb, rdlane(s_lit0, k), n);
+            }
+            op += total;
+            misses = 0;
+        } else {
+            ++misses;
+        }
+        // incompressible runs are probed ever more sparsely (LZ4's
+        // acceleration): after m batches without a match, m-1 are skipped
+        const uint32_t skip = misses > 1 ? (misses - 1) * 64 * kWin : 0;
+        base = max(base + 64 * kWin + skip, p & ~63u);
     }
-    if (!emit_sequence(dst, op, cap, sb, anchor, L - anchor, 0, 0, true))
+    // the last literals
+    const uint32_t n = L - anchor;
+    const uint32_t le = n >= 15 ? (n - 15) / 255 + 1 : 0;
+    if (op + 1 + le + n > cap)
         return 0;
-    return op;
+    if (lane == 0) {
+        dst[op] = uint8_t((n < 15 ? n : 15) << 4);
+        put_len_ext_lane(dst + op + 1, le, n - 15);
+    }
+    copy_lits(dst + op + 1 + le, sb, anchor, n);
+    return op + 1 + le + n;
 }
 
 __global__ __launch_bounds__(64) void
 lz4_streams(const BloscParams p)
 {
     __shared__ __attribute__((aligned(16))) uint32_t sw[kLz4StreamMax / 4 + 4];
-    __shared__ uint32_t table[kHashSize];
+    __shared__ __attribute__((aligned(16))) uint16_t table[kHashSize];
     const uint32_t gid = blockIdx.x;
     const uint32_t c = gid / p.g.spc, q = gid - c * p.g.spc;
     if (p.flags && p.flags[c] != p.tag) {
@@ -317,13 +420,18 @@ lz4_streams(const BloscParams p)
     __syncthreads();
     uint32_t n = lz4_wave(sb, sw, r.len, table, dst);
     if (n == 0) {
-        for (uint32_t k = threadIdx.x; k < r.len; k += 64)
+        // raw: words when the slot is 4-B aligned (slots are), bytes for the tail
+        const uint32_t nw = (reinterpret_cast<uintptr_t>(dst) & 3u) ? 0 : r.len / 4;
+        for (uint32_t k = threadIdx.x; k < nw; k += 64)
+            reinterpret_cast<uint32_t*>(dst)[k] = sw[k];
+        for (uint32_t k = nw * 4 + threadIdx.x; k < r.len; k += 64)
             dst[k] = sb[k];
         n = r.len;
     }
     if (threadIdx.x == 0)
         p.ssize[gid] = n;
 }
+
 
 // Exclusive block-wide scan of one value per thread (256 threads); returns
 // the prefix, *total = the sum over the block.
