@@ -20,8 +20,8 @@
 namespace aqz {
 
 // bytes of one LZ4-compressed stream (resident in LDS while it is encoded)
-constexpr uint32_t kLz4StreamMax = 16384;
-constexpr int kLz4HashLog = 12;
+constexpr uint32_t kLz4StreamMax = 8192;
+constexpr int kLz4HashLog = 11;
 
 // The blosc1 frame geometry shared by every chunk of a layer.
 struct BloscGeom

@@ -263,8 +263,13 @@ lz4_wave(const uint8_t* sb, const uint32_t* sw, uint32_t L, uint16_t* table, uin
                 const uint32_t h = (v * 2654435761u) >> (32 - kLz4HashLog);
                 const uint32_t e = table[h];
                 table[h] = uint16_t(q + 1);
-                if (e != 0 && lds_rd32(sw, e - 1) == v) {
-                    const uint32_t c = e - 1;
+                // the hash candidate, else the byte before (a run: offset 1)
+                uint32_t c = ~0u;
+                if (e != 0 && lds_rd32(sw, e - 1) == v)
+                    c = e - 1;
+                else if (q > 0 && lds_rd32(sw, q - 1) == v)
+                    c = q - 1;
+                if (c != ~0u) {
                     const uint32_t lim = min(matchlimit - q, kLenCap);
                     uint32_t len = 4;
                     bool done = false;

@@ -195,20 +195,45 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
         src_arr = np.empty(src_frames * fbytes, dtype=np.uint8)
         src_ptr, mem = src_arr.ctypes.data, aqz.MEM_HOST
     rng = np.random.default_rng(7 + rank)
-    src_arr[...] = rng.integers(0, 256, size=src_arr.size, dtype=np.uint8)
-    dst = [[aqz.HostBuffer(lbytes[l]) for _ in range(4)] for l in range(L)]
+    if args.compress:
+        # compressible camera-like frames (smooth background + noise)
+        n_px = src_arr.size // bpp
+        v = 1000.0 + 200.0 * np.sin(np.arange(n_px) / 977.0) + rng.normal(0, 30.0, n_px)
+        npdt = {U8: np.uint8, U16: np.uint16, F32: np.float32}[dt]
+        if dt == U8:
+            v = v / 8.0
+        src_arr[...] = v.clip(0, 65535).astype(npdt).view(np.uint8)
+    else:
+        src_arr[...] = rng.integers(0, 256, size=src_arr.size, dtype=np.uint8)
+    cap = [lbytes[l] + 16 * lay[l]["chunks_per_layer"] for l in range(L)]
+    dst = [[aqz.HostBuffer(cap[l]) for _ in range(4)] for l in range(L)]
     hd = [[aqz.HostBuffer(lay[l]["chunks_per_layer"]) for _ in range(4)] for l in range(L)]
     handed = [0] * L
     d2h = [0]
+    pending = []  # compressed layers whose frames are not copied yet
+
+    def drain_compressed():
+        while pending:
+            l, layer = pending.pop(0)
+            i = layer % 4
+            off = st.compressed_offsets(l, layer)
+            st.copy_compressed_async(l, layer, dst[l][i].ptr, cap[l])
+            d2h[0] += int(off[-1])
 
     def hand_off():
+        if args.compress:
+            drain_compressed()  # last step's layers: their kernels are done by now
         for l in range(L):
             done = st.frames_written(l) // lay[l]["frames_per_layer"]
             while handed[l] < done:
                 i = handed[l] % 4
-                st.copy_layer_async(l, handed[l], dst[l][i].ptr, lbytes[l], hd[l][i].ptr,
-                                    hd[l][i].nbytes)
-                d2h[0] += lbytes[l]
+                if args.compress:
+                    st.compress_layer(l, handed[l], clevel=5, shuffle=args.compress)
+                    pending.append((l, handed[l]))
+                else:
+                    st.copy_layer_async(l, handed[l], dst[l][i].ptr, lbytes[l],
+                                        hd[l][i].ptr, hd[l][i].nbytes)
+                    d2h[0] += lbytes[l]
                 handed[l] += 1
 
     def step(s):
@@ -217,6 +242,8 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
 
     for s in range(args.warmup):
         step(s)
+    drain_compressed()
+    st.wait_copies()
     st.synchronize()
     if dist:
         dist.barrier()
@@ -224,6 +251,8 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
     t0 = time.perf_counter()
     for s in range(args.steps):
         step(args.warmup + s)
+    drain_compressed()
+    st.wait_copies()
     st.synchronize()
     el = time.perf_counter() - t0
     if dist:
@@ -235,19 +264,22 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
     in_bytes = args.steps * B * fbytes
     return {
         "metric": "end-to-end input GB/s, host frames -> H2D -> multiscale stage -> "
-                  "D2H of every chunk layer",
+                  + ("device blosc-lz4 compression (shuffle %d) -> D2H of every "
+                     "compressed chunk layer" % args.compress if args.compress
+                     else "D2H of every chunk layer"),
         "value": round(world * in_bytes / el / 1e9, 3), "unit": "GB/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el * 1e3 / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
         "dtype": {U8: "u8", U16: "u16", F32: "f32"}[dt],
-        "data": f"synthetic, host {args.e2e} source ring of {src_frames} frames",
+        "data": f"synthetic{' camera-like' if args.compress else ' random'}, host {args.e2e} source ring of {src_frames} frames",
         "config": {"workload": cfg["workload"].replace("device-resident", "host-resident") +
                    f" [e2e, {args.e2e} source]", "frames_per_step_per_gpu": B,
                    "levels": L},
         "h2d_gbs_per_gpu": round(in_bytes / el / 1e9, 3),
         "d2h_gbs_per_gpu": round(d2h[0] / el / 1e9, 3),
         "frames_per_s_per_gpu": round(args.steps * B / el, 1),
+        "d2h_bytes_per_input_byte": round(d2h[0] / in_bytes, 4),
     }
 
 
@@ -362,6 +394,9 @@ def main():
                     help="duration of the --fps run")
     ap.add_argument("--batch", type=int, default=0,
                     help="frames per append (default: the config's batch)")
+    ap.add_argument("--compress", type=int, default=0, choices=[0, 1, 2],
+                    help="e2e: compress every chunk layer on the device (blosc-lz4, "
+                         "1 = byte shuffle, 2 = bitshuffle) and hand off the frames")
     ap.add_argument("--e2e", choices=["pinned", "pageable"], default=None,
                     help="end-to-end mode: frames start in host memory (pinned or "
                          "pageable), every completed chunk layer is handed back to "
