@@ -71,6 +71,14 @@ class CompressionC(C.Structure):
 CODEC_NONE, CODEC_BLOSC_LZ4, CODEC_BLOSC_ZSTD, CODEC_ZSTD = 0, 1, 2, 3
 
 
+class ChunkEntryC(C.Structure):
+    _fields_ = [("chunk", C.c_uint32), ("shard", C.c_uint32), ("internal", C.c_uint32),
+                ("reserved", C.c_uint32), ("offset", C.c_uint64), ("nbytes", C.c_uint64)]
+
+
+SHARD_UNWRITTEN = (1 << 64) - 1
+
+
 class LevelLayoutC(C.Structure):
     _fields_ = [("bytes_per_chunk", C.c_uint64),
                 ("chunks_per_layer", C.c_uint32), ("layer_slots", C.c_uint32),
@@ -173,6 +181,12 @@ def lib():
         "aqz_compressor_max_bytes": ([u64, u32], u64),
         "aqz_compressor_run": ([vp, vp, u64, u32, vp, sz, vp, vp], i32),
         "aqz_compressor_blocksize": ([vp], u32),
+        "aqz_stage_compressed_entries": ([vp, u32, u64, C.POINTER(ChunkEntryC), sz], i32),
+        "aqz_stage_shard_geometry": ([vp, u32, C.POINTER(u32), C.POINTER(u32),
+                                      C.POINTER(u32)], i32),
+        "aqz_shard_table_bytes": ([u32], sz),
+        "aqz_shard_table": ([vp, vp, u32, vp, sz], i32),
+        "aqz_crc32c": ([vp, sz], u32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -502,6 +516,20 @@ class Stage:
         _check(lib().aqz_stage_copy_compressed_async(self.h, level, layer, dst_ptr, cap),
                "copy_compressed_async")
 
+    def compressed_entries(self, level, layer):
+        """[(chunk, shard, internal, offset, nbytes)] in output (shard-major) order."""
+        n = self.layout(level)["chunks_per_layer"]
+        arr = (ChunkEntryC * n)()
+        _check(lib().aqz_stage_compressed_entries(self.h, level, layer, arr, n),
+               "compressed_entries")
+        return [(e.chunk, e.shard, e.internal, e.offset, e.nbytes) for e in arr]
+
+    def shard_geometry(self, level):
+        a, b, c = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        _check(lib().aqz_stage_shard_geometry(self.h, level, C.byref(a), C.byref(b),
+                                              C.byref(c)), "shard_geometry")
+        return a.value, b.value, c.value
+
     def copy_compressed(self, level, layer):
         """(frames bytes, offsets) of a compressed layer, synchronously."""
         off = self.compressed_offsets(level, layer)
@@ -542,3 +570,44 @@ class Compressor:
         _check(lib().aqz_compressor_run(self.h, chunks_ptr, pitch, n_chunks, dst_ptr,
                                         dst_cap, offsets_ptr, stream_ptr),
                "aqz_compressor_run")
+
+
+def shard_table(offsets, extents) -> bytes:
+    """Shard::write_table_ bytes (aqz_shard_table)."""
+    n = len(offsets)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ext = np.ascontiguousarray(extents, dtype=np.uint64)
+    out = np.empty(lib().aqz_shard_table_bytes(n), dtype=np.uint8)
+    _check(lib().aqz_shard_table(off.ctypes.data, ext.ctypes.data, n, out.ctypes.data,
+                                 out.nbytes), "aqz_shard_table")
+    return out.tobytes()
+
+
+def crc32c(data: bytes) -> int:
+    return lib().aqz_crc32c(data, len(data))
+
+
+class ShardAssembler:
+    """zarr::Shard bookkeeping for one append-dimension shard row of a level
+    (shard.cpp:55-166): each compressed layer's shard runs are appended at
+    the shard's running offset, unwritten chunks keep the UINT64_MAX
+    sentinel, and finalize() appends the index table + CRC-32C.  Host-side
+    helper over the C ABI; the byte sink (file / S3) is the caller's."""
+
+    def __init__(self, stage, level):
+        self.cps, self.n_shards, self.lps = stage.shard_geometry(level)
+        self.data = [bytearray() for _ in range(self.n_shards)]
+        self.off = [[SHARD_UNWRITTEN] * self.cps for _ in range(self.n_shards)]
+        self.ext = [[SHARD_UNWRITTEN] * self.cps for _ in range(self.n_shards)]
+
+    def add_layer(self, frames, entries):
+        for chunk, shard, internal, offset, nbytes in entries:
+            if nbytes == 0:
+                continue
+            self.off[shard][internal] = len(self.data[shard])
+            self.ext[shard][internal] = nbytes
+            self.data[shard] += bytes(frames[offset:offset + nbytes])
+
+    def finalize(self):
+        return [bytes(self.data[s]) + shard_table(self.off[s], self.ext[s])
+                for s in range(self.n_shards)]

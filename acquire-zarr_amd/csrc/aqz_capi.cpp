@@ -672,3 +672,51 @@ aqz_compressor_run(aqz_compressor* c, const void* chunks, uint64_t pitch,
                   static_cast<uint8_t*>(dst), offsets, static_cast<hipStream_t>(stream));
     });
 }
+
+// ---- shard packing ---------------------------------------------------------
+aqz_status
+aqz_stage_compressed_entries(aqz_stage* st, uint32_t level, uint64_t layer,
+                             aqz_chunk_entry* out, size_t n)
+{
+    if (!out)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    static_assert(sizeof(aqz_chunk_entry) == sizeof(ChunkEntry), "entry layout");
+    return guard_sticky(st, [&] {
+        st->st->compressed_entries(level, layer, reinterpret_cast<ChunkEntry*>(out), n);
+    });
+}
+
+aqz_status
+aqz_stage_shard_geometry(const aqz_stage* st, uint32_t level, uint32_t* chunks_per_shard,
+                         uint32_t* number_of_shards, uint32_t* layers_per_shard)
+{
+    if (!st)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard([&] {
+        st->st->shard_geometry(level, chunks_per_shard, number_of_shards, layers_per_shard);
+    });
+}
+
+size_t
+aqz_shard_table_bytes(uint32_t chunks_per_shard)
+{
+    return size_t(chunks_per_shard) * 16 + 4;
+}
+
+aqz_status
+aqz_shard_table(const uint64_t* offsets, const uint64_t* extents, uint32_t chunks_per_shard,
+                void* out, size_t cap)
+{
+    if (!offsets || !extents || !out)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    if (cap < aqz_shard_table_bytes(chunks_per_shard))
+        return AQZ_STATUS_OVERFLOW;
+    shard_table(offsets, extents, chunks_per_shard, static_cast<uint8_t*>(out));
+    return AQZ_STATUS_SUCCESS;
+}
+
+uint32_t
+aqz_crc32c(const void* data, size_t n)
+{
+    return data ? crc32c(static_cast<const uint8_t*>(data), n) : 0;
+}

@@ -54,8 +54,12 @@ struct BloscParams
     uint32_t* spos;         // [n_chunks * spc] record offset inside the frame
     uint32_t* fsize;        // [n_chunks] frame bytes (0: chunk skipped)
     uint8_t* mode;          // [n_chunks] 1: memcpyed frame
-    uint64_t* offsets;      // [n_chunks + 1] frame offsets in out; [n] = total
-    uint8_t* out;           // frames, back to back in chunk order
+    const uint32_t* order;  // [n_chunks] output position -> chunk (nullptr:
+                            // chunk order); shard-major for shard packing
+    uint64_t* offsets;      // [n_chunks + 1] frame offsets in out, in output
+                            // order; [n] = total
+    uint64_t* cstart;       // [n_chunks] frame offset of each chunk
+    uint8_t* out;           // frames, back to back in output order
     uint32_t store_only;    // clevel 0: every frame memcpyed, no LZ4
 };
 

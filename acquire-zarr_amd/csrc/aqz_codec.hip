@@ -489,20 +489,24 @@ chunk_layout(const BloscParams p)
 }
 
 __global__ __launch_bounds__(256) void
-scan_offsets(const uint32_t* fsize, uint64_t* offsets, uint32_t n)
+scan_offsets(const uint32_t* fsize, const uint32_t* order, uint64_t* offsets,
+             uint64_t* cstart, uint32_t n)
 {
     __shared__ uint64_t carry_s;
     if (threadIdx.x == 0)
         carry_s = 0;
     __syncthreads();
-    for (uint32_t c0 = 0; c0 < n; c0 += 256) {
-        const uint32_t c = c0 + threadIdx.x;
-        const uint32_t v = c < n ? fsize[c] : 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += 256) {
+        const uint32_t i = i0 + threadIdx.x;
+        const uint32_t c = i < n ? (order ? order[i] : i) : 0;
+        const uint32_t v = i < n ? fsize[c] : 0;
         uint32_t tot;
         const uint32_t pre = block_scan256(v, &tot);
         const uint64_t carry = carry_s;
-        if (c < n)
-            offsets[c] = carry + pre;
+        if (i < n) {
+            offsets[i] = carry + pre;
+            cstart[c] = carry + pre;
+        }
         __syncthreads();
         if (threadIdx.x == 0)
             carry_s = carry + tot;
@@ -529,7 +533,7 @@ write_frames(const BloscParams p)
     const uint32_t fs = p.fsize[c];
     if (fs == 0)
         return;
-    uint8_t* o = p.out + p.offsets[c];
+    uint8_t* o = p.out + p.cstart[c];
     const bool memcpyed = p.mode[c] != 0;
     if (q == 0 && threadIdx.x == 0) {
         o[0] = 2; // BLOSC_VERSION_FORMAT
@@ -575,8 +579,8 @@ launch_blosc_lz4(const BloscParams& p, hipStream_t stream)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(lz4_streams, dim3(uint32_t(ns)), dim3(64), 0, stream, p);
     hipLaunchKernelGGL(chunk_layout, dim3(p.n_chunks), dim3(256), 0, stream, p);
-    hipLaunchKernelGGL(scan_offsets, dim3(1), dim3(256), 0, stream, p.fsize, p.offsets,
-                       p.n_chunks);
+    hipLaunchKernelGGL(scan_offsets, dim3(1), dim3(256), 0, stream, p.fsize, p.order,
+                       p.offsets, p.cstart, p.n_chunks);
     hipLaunchKernelGGL(write_frames, dim3(uint32_t(ns)), dim3(256), 0, stream, p);
     return hipGetLastError();
 }

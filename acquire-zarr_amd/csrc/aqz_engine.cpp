@@ -295,6 +295,7 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
                                 hipMemcpyHostToDevice),
                       "hipMemcpy");
         }
+        build_shard_order(L);
         L.tab_off.alloc(size_t(L.F) * 8);
         L.tab_grp.alloc(size_t(L.F) * 4);
         hip_check(hipMemcpy(L.tab_off.p, L.h_tab_off.data(), size_t(L.F) * 8,
@@ -1111,6 +1112,118 @@ Stage::device_layer(uint32_t level, uint64_t layer, void** chunks,
         *flags = reinterpret_cast<uint32_t*>(L.flags.p) + size_t(slot) * L.n_chunks;
 }
 
+// ---- shard packing ------------------------------------
+uint32_t
+crc32c(const uint8_t* p, size_t n)
+{
+    static const auto table = [] {
+        std::vector<uint32_t> t(256);
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t c = i;
+            for (int k = 0; k < 8; ++k)
+                c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+            t[i] = c;
+        }
+        return t;
+    }();
+    uint32_t c = 0xFFFFFFFFu;
+    for (size_t i = 0; i < n; ++i)
+        c = table[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
+    return c ^ 0xFFFFFFFFu;
+}
+
+void
+shard_table(const uint64_t* offsets, const uint64_t* extents, uint32_t n, uint8_t* out)
+{
+    for (uint32_t i = 0; i < n; ++i)
+        for (int b = 0; b < 8; ++b) {
+            out[16 * i + b] = uint8_t(offsets[i] >> (8 * b));
+            out[16 * i + 8 + b] = uint8_t(extents[i] >> (8 * b));
+        }
+    const uint32_t crc = crc32c(out, size_t(n) * 16);
+    for (int b = 0; b < 4; ++b)
+        out[size_t(n) * 16 + b] = uint8_t(crc >> (8 * b));
+}
+
+// Shard-major order of a level's chunks (Array::compress_and_flush_data_
+// walks shards, array.cpp:777-803; Shard::write_chunk appends each chunk at
+// the shard's running file offset, shard.cpp:55-112).  Without sharding
+// (a shard size of 0) the order is the chunk order.
+void
+Stage::build_shard_order(StageLevel& L)
+{
+    const uint32_t n = L.n_chunks;
+    L.h_order.resize(n);
+    L.h_shard.assign(n, 0);
+    L.h_internal0.assign(n, 0);
+    for (uint32_t c = 0; c < n; ++c)
+        L.h_order[c] = c;
+    bool sharded = true;
+    for (const Dim& d : L.ad->dims())
+        sharded = sharded && d.shard_size_chunks > 0;
+    if (sharded) {
+        L.chunks_per_shard = L.ad->chunks_per_shard();
+        L.n_shards = L.ad->number_of_shards();
+        L.layers_per_shard = std::max<uint32_t>(1, L.ad->chunk_layers_per_shard());
+        L.internal_stride = L.chunks_per_shard / L.layers_per_shard;
+        for (uint32_t c = 0; c < n; ++c) {
+            L.h_shard[c] = L.ad->shard_index_for_chunk(c);
+            L.h_internal0[c] = L.ad->shard_internal_index(c);
+        }
+        std::stable_sort(L.h_order.begin(), L.h_order.end(), [&](uint32_t a, uint32_t b) {
+            return L.h_shard[a] != L.h_shard[b] ? L.h_shard[a] < L.h_shard[b]
+                                                : L.h_internal0[a] < L.h_internal0[b];
+        });
+    } else {
+        L.chunks_per_shard = 1;
+        L.n_shards = n;
+        L.layers_per_shard = 1;
+        L.internal_stride = 0;
+        for (uint32_t c = 0; c < n; ++c)
+            L.h_shard[c] = c;
+    }
+    L.shard_order.alloc(size_t(n) * 4);
+    hip_check(hipMemcpy(L.shard_order.p, L.h_order.data(), size_t(n) * 4,
+                        hipMemcpyHostToDevice),
+              "hipMemcpy");
+}
+
+void
+Stage::compressed_entries(uint32_t level, uint64_t layer, ChunkEntry* out, size_t n)
+{
+    if (level >= lv_.size())
+        throw Error(3, "level out of range");
+    StageLevel& L = lv_[level];
+    const uint32_t slot = L.n_slots ? uint32_t(layer % L.n_slots) : 0;
+    if (L.comp_layer.empty() || L.comp_layer[slot] != int64_t(layer))
+        throw Error(3, "layer was not compressed (or its slot was reused)");
+    if (n < L.n_chunks)
+        throw Error(2, "entries too small");
+    hip_check(hipEventSynchronize(L.comp_ev[slot]), "hipEventSynchronize");
+    const uint64_t* off = reinterpret_cast<const uint64_t*>(L.h_coffsets[slot].p);
+    const uint32_t cl = uint32_t(layer % L.layers_per_shard);
+    for (uint32_t i = 0; i < L.n_chunks; ++i) {
+        const uint32_t c = L.h_order[i];
+        out[i] = ChunkEntry{ c, L.h_shard[c], L.h_internal0[c] + cl * L.internal_stride, 0,
+                             off[i], off[i + 1] - off[i] };
+    }
+}
+
+void
+Stage::shard_geometry(uint32_t level, uint32_t* chunks_per_shard, uint32_t* n_shards,
+                      uint32_t* layers_per_shard) const
+{
+    if (level >= lv_.size())
+        throw Error(3, "level out of range");
+    const StageLevel& L = lv_[level];
+    if (chunks_per_shard)
+        *chunks_per_shard = L.chunks_per_shard;
+    if (n_shards)
+        *n_shards = L.n_shards;
+    if (layers_per_shard)
+        *layers_per_shard = L.layers_per_shard;
+}
+
 // ---- device compression of resident layers ----------
 Compressor::Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compression& c)
 {
@@ -1128,7 +1241,7 @@ Compressor::Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compressio
 void
 Compressor::run(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
                 const uint32_t* flags, uint32_t tag, uint8_t* out, uint64_t* offsets,
-                hipStream_t stream)
+                hipStream_t stream, const uint32_t* order)
 {
     const uint64_t ns = uint64_t(n_chunks) * g_.spc;
     scratch_.alloc(store_only_ ? 1 : ns * g_.slot);
@@ -1136,6 +1249,7 @@ Compressor::run(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
     spos_.alloc(ns * 4);
     fsize_.alloc(size_t(n_chunks) * 4);
     mode_.alloc(n_chunks);
+    cstart_.alloc(size_t(n_chunks) * 8);
     BloscParams p{};
     p.g = g_;
     p.chunks = chunks;
@@ -1149,6 +1263,8 @@ Compressor::run(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
     p.fsize = reinterpret_cast<uint32_t*>(fsize_.p);
     p.mode = mode_.p;
     p.offsets = offsets;
+    p.cstart = reinterpret_cast<uint64_t*>(cstart_.p);
+    p.order = order;
     p.out = out;
     p.store_only = store_only_ ? 1 : 0;
     hip_check(launch_blosc_lz4(p, stream), "blosc-lz4 launch");
@@ -1190,7 +1306,8 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
     L.comp->run(L.ring.p + slot * L.slot_bytes, L.pitch, L.n_chunks,
                 reinterpret_cast<const uint32_t*>(L.flags.p) + size_t(slot) * L.n_chunks,
                 uint32_t(layer / L.n_slots + 1), L.cframes[slot].p,
-                reinterpret_cast<uint64_t*>(L.coffsets[slot].p), d2h_);
+                reinterpret_cast<uint64_t*>(L.coffsets[slot].p), d2h_,
+                reinterpret_cast<const uint32_t*>(L.shard_order.p));
     hip_check(hipMemcpyAsync(L.h_coffsets[slot].p, L.coffsets[slot].p,
                              (size_t(L.n_chunks) + 1) * 8, hipMemcpyDeviceToHost, d2h_),
               "hipMemcpyAsync");

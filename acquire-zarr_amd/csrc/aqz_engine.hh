@@ -94,15 +94,16 @@ class Compressor
     // chunks + i * pitch; skipped unless flags[i] == tag when flags is
     // given) back to back into out; offsets (device, n_chunks + 1 words)
     // gets each frame's start and the total.
+    // order (device, optional): output position -> chunk.
     void run(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
              const uint32_t* flags, uint32_t tag, uint8_t* out, uint64_t* offsets,
-             hipStream_t stream);
+             hipStream_t stream, const uint32_t* order = nullptr);
     const BloscGeom& geom() const { return g_; }
 
   private:
     BloscGeom g_;
     bool store_only_;
-    DevBuf scratch_, ssize_, spos_, fsize_, mode_;
+    DevBuf scratch_, ssize_, spos_, fsize_, mode_, cstart_;
 };
 
 struct ArrayDesc
@@ -176,7 +177,27 @@ struct StageLevel
     std::vector<PinnedBuf> h_coffsets;
     std::vector<hipEvent_t> comp_ev;
     std::vector<int64_t> comp_layer;       // layer compressed in each slot
+    // shard packing: compressed frames leave in shard-major order
+    // (shard_index_for_chunk, then shard_internal_index); internal indices
+    // of a layer = h_internal0 + (layer mod layers_per_shard) * stride
+    DevBuf shard_order;
+    std::vector<uint32_t> h_order, h_shard, h_internal0;
+    uint32_t chunks_per_shard = 0, n_shards = 0, layers_per_shard = 1;
+    uint32_t internal_stride = 0;
 };
+
+// One chunk of a compressed layer, in output (shard-major) order.
+struct ChunkEntry
+{
+    uint32_t chunk, shard, internal, reserved;
+    uint64_t offset, nbytes;
+};
+
+// Shard::write_table_ (shard.cpp:145-166): offsets/extents as little-endian
+// uint64 pairs, then the CRC-32C of those bytes.
+uint32_t crc32c(const uint8_t* p, size_t n);
+void shard_table(const uint64_t* offsets, const uint64_t* extents, uint32_t n,
+                 uint8_t* out);
 
 class Stage
 {
@@ -208,6 +229,10 @@ class Stage
                             size_t n);
     // D2H of the frames (offsets[n_chunks] bytes) on the hand-off stream
     void copy_compressed_async(uint32_t level, uint64_t layer, void* dst, size_t cap);
+    // waits; one entry per chunk in output order
+    void compressed_entries(uint32_t level, uint64_t layer, ChunkEntry* out, size_t n);
+    void shard_geometry(uint32_t level, uint32_t* chunks_per_shard, uint32_t* n_shards,
+                        uint32_t* layers_per_shard) const;
     void finalize();
     void enable_timing(bool on);
     void timing(double* total_ms, uint64_t* launches);
@@ -223,6 +248,7 @@ class Stage
     };
 
     void run_batch(const uint8_t* dsrc, uint32_t n);
+    void build_shard_order(StageLevel& L);
     FusedParams fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
                              uint32_t rh_log2, bool tail);
     void run_fused(const uint8_t* dsrc, uint32_t n);

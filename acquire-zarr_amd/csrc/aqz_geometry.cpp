@@ -256,6 +256,26 @@ ArrayDimensions::shard_index_for_chunk(uint32_t chunk_index) const
 }
 
 uint32_t
+ArrayDimensions::chunks_per_shard() const
+{
+    uint64_t n = 1;
+    for (const Dim& d : dims_)
+        n *= d.shard_size_chunks;
+    if (n > 0xffffffffull)
+        throw Error(1, "too many chunks per shard");
+    return uint32_t(n);
+}
+
+uint32_t
+ArrayDimensions::number_of_shards() const
+{
+    uint64_t n = 1;
+    for (size_t i = 1; i < dims_.size(); ++i)
+        n *= shards_along(dims_[i]);
+    return uint32_t(n);
+}
+
+uint32_t
 ArrayDimensions::shard_internal_index(uint32_t chunk_index) const
 {
     // array.dimensions.cpp:504-548

@@ -88,6 +88,10 @@ class ArrayDimensions
     uint64_t frames_per_chunk_layer() const;
     uint32_t shard_index_for_chunk(uint32_t chunk_index) const;
     uint32_t shard_internal_index(uint32_t chunk_index) const;
+    // array.dimensions.cpp:168-178, 376-397
+    uint32_t chunks_per_shard() const;
+    uint32_t number_of_shards() const;
+    uint32_t chunk_layers_per_shard() const { return dims_[0].shard_size_chunks; }
 
   private:
     bool is_2d_;

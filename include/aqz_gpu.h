@@ -308,20 +308,56 @@ typedef struct
 
 /* Compress resident layer `layer` of `level` into blosc1 frames, one per
  * chunk with data (chunks without data are skipped, like the reference's
- * skip_chunk), back to back in chunk order.  Runs on the hand-off stream
+ * skip_chunk), back to back in SHARD-MAJOR order: the chunks of shard 0 by
+ * shard_internal_index, then shard 1, ... (aqz_stage_compressed_entries
+ * lists them), so each shard's frames of the layer are one contiguous run
+ * that Shard::write_chunk would append at the shard's file offset.  Runs on the hand-off stream
  * after the kernels that wrote the layer; the slot is not reused until it
  * has been read. */
 aqz_status aqz_stage_compress_layer(aqz_stage* st, uint32_t level, uint64_t layer,
                                     const aqz_compression* comp);
-/* Waits for that compression.  offsets[c] = start of chunk c's frame,
- * offsets[c+1] - offsets[c] its size (0: skipped), offsets[chunks_per_layer]
- * = total bytes.  n >= chunks_per_layer + 1. */
+/* Waits for that compression.  offsets[i] = start of the i-th frame in
+ * output order, offsets[i+1] - offsets[i] its size (0: skipped),
+ * offsets[chunks_per_layer] = total bytes.  n >= chunks_per_layer + 1. */
 aqz_status aqz_stage_compressed_offsets(aqz_stage* st, uint32_t level,
                                         uint64_t layer, uint64_t* offsets, size_t n);
 /* Asynchronous copy of the layer's frames (total bytes) to dst (host or
  * device); complete after aqz_stage_wait_copies. */
 aqz_status aqz_stage_copy_compressed_async(aqz_stage* st, uint32_t level,
                                            uint64_t layer, void* dst, size_t cap);
+
+/* ---- shard packing -----------------------------------
+ * The frames of a compressed layer in output order, with their place in
+ * the shards (ArrayDimensions::shard_index_for_chunk / shard_internal_index,
+ * array.dimensions.cpp:396-548; the internal index includes the layer's
+ * position along the append dimension inside its shard). */
+typedef struct
+{
+    uint32_t chunk;    /* chunk index inside the layer (Array::chunks_ slot) */
+    uint32_t shard;    /* shard of the current append-dimension shard row */
+    uint32_t internal; /* shard_internal_index */
+    uint32_t reserved;
+    uint64_t offset;   /* frame start inside the compressed layer */
+    uint64_t nbytes;   /* frame bytes; 0 = no data (Shard::skip_chunk) */
+} aqz_chunk_entry;
+aqz_status aqz_stage_compressed_entries(aqz_stage* st, uint32_t level,
+                                        uint64_t layer, aqz_chunk_entry* out,
+                                        size_t n);
+/* chunks_per_shard, number_of_shards (one append-dimension shard row) and
+ * chunk layers per shard (array.dimensions.cpp:376-397) of a level. */
+aqz_status aqz_stage_shard_geometry(const aqz_stage* st, uint32_t level,
+                                    uint32_t* chunks_per_shard,
+                                    uint32_t* number_of_shards,
+                                    uint32_t* layers_per_shard);
+/* Shard::write_table_ (shard.cpp:145-166): chunks_per_shard (offset,
+ * extent) little-endian uint64 pairs -- UINT64_MAX for both when a chunk
+ * was never written -- followed by the CRC-32C of those bytes; out holds
+ * aqz_shard_table_bytes(chunks_per_shard) bytes.  The table goes at the end
+ * of the shard (index_location "end"). */
+size_t aqz_shard_table_bytes(uint32_t chunks_per_shard);
+aqz_status aqz_shard_table(const uint64_t* offsets, const uint64_t* extents,
+                           uint32_t chunks_per_shard, void* out, size_t cap);
+uint32_t aqz_crc32c(const void* data, size_t n);
 
 /* Stand-alone compressor for device-resident chunk arrays: chunk i of
  * n_chunks at chunks + i * pitch, chunk_bytes each; frames back to back at

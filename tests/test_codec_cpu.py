@@ -81,3 +81,22 @@ def test_shuffles_invert():
             d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
             assert shuffle("unshuffle", ts, shuffle("shuffle", ts, d)) == d
             assert shuffle("bitunshuffle", ts, shuffle("bitshuffle", ts, d)) == d
+
+
+def test_shard_table_layout_and_crc():
+    """aqz_shard_table (C ABI, host code) == Shard::write_table_ restated:
+    (offset, extent) little-endian u64 pairs, UINT64_MAX for unwritten
+    chunks, then CRC-32C of the pairs (shard.cpp:145-166)."""
+    import aqz
+    U = (1 << 64) - 1
+    offsets = [0, U, 1000, 17, U]
+    extents = [1000, U, 5, 983, U]
+    t = aqz.shard_table(offsets, extents)
+    body = b"".join(struct.pack("<QQ", o, e) for o, e in zip(offsets, extents))
+    assert t[:-4] == body
+    assert struct.unpack("<I", t[-4:])[0] == crc32c(body)
+    assert aqz.crc32c(b"123456789") == 0xE3069283
+    rng = np.random.default_rng(0)
+    for n in (0, 1, 31, 1000):
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert aqz.crc32c(d) == crc32c(d)

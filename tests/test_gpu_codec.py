@@ -130,16 +130,94 @@ def test_stage_compress_layer(gpu):
             layer = st.frames_written(l) // lay[l]["frames_per_layer"] - 1
             if layer >= 0 and (l, layer) not in got:
                 st.compress_layer(l, layer, clevel=5, shuffle=1)
-                got[(l, layer)] = st.copy_compressed(l, layer)
+                got[(l, layer)] = (st.copy_compressed(l, layer)[0],
+                                   st.compressed_entries(l, layer))
     assert sorted(got) == sorted(exp)
     for (l, layer), (buf, flags) in exp.items():
-        data, off = got[(l, layer)]
+        data, ent = got[(l, layer)]
         bpc = lay[l]["bytes_per_chunk"]
-        for c in range(lay[l]["chunks_per_layer"]):
-            fr = data[int(off[c]):int(off[c + 1])].tobytes()
+        assert sorted(e[0] for e in ent) == list(range(lay[l]["chunks_per_layer"]))
+        for c, _, _, o, nb in ent:
+            fr = data[o:o + nb].tobytes()
             if not flags[c]:
                 assert len(fr) == 0, (l, layer, c)
                 continue
             chunk = buf[c * bpc:(c + 1) * bpc].tobytes()
             assert oracle_decode(fr) == chunk, (l, layer, c)
     st.close()
+
+
+def parse_shard(blob: bytes, cps: int):
+    """(offsets, extents) of a shard file; checks the index CRC-32C."""
+    import struct
+    from codec_helpers import crc32c
+    tbl = blob[len(blob) - 16 * cps - 4:]
+    body, crc = tbl[:-4], struct.unpack("<I", tbl[-4:])[0]
+    assert crc32c(body) == crc, "shard index checksum"
+    pairs = [struct.unpack("<QQ", body[16 * i:16 * i + 16]) for i in range(cps)]
+    return [p[0] for p in pairs], [p[1] for p in pairs]
+
+
+def test_stage_shards_from_device_frames(gpu):
+    """Shard packing: compressed layers leave the device
+    shard-major; ShardAssembler appends each shard's run at its running
+    offset over the layers of one append-dimension shard row and writes the
+    index + CRC-32C.  Every written (offset, extent) decodes to the oracle's
+    chunk at that internal index; chunks without data and the ragged edge
+    shard's missing chunks carry the UINT64_MAX sentinel."""
+    from oracle_bindings import OracleDims, OracleDownsampler
+    # y: 4 chunks -> 2 shards; x: 3 chunks -> 2 shards (one ragged);
+    # t: 2 layers per shard row
+    dims = [(TIME, 0, 2, 2), (SPACE, 512, 128, 2), (SPACE, 384, 128, 2)]
+    n = 8
+    frames = synthetic_frames(U16, n, 512, 384, 21)
+    frames[:, 128:256, :] = 0
+    exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
+    ods = OracleDownsampler(dims, U16, MEAN, 0)
+    st = gpu.Stage(dims, U16, MEAN, layer_slots=2, max_batch_frames=2)
+    L = st.n_levels()
+    lay = [st.layout(l) for l in range(L)]
+    rows = {}   # (level, shard row) -> ShardAssembler
+    done = {l: 0 for l in range(L)}
+    for b in range(0, n, 2):
+        st.append(np.ascontiguousarray(frames[b:b + 2]))
+        for l in range(L):
+            while done[l] < st.frames_written(l) // lay[l]["frames_per_layer"]:
+                layer = done[l]
+                st.compress_layer(l, layer, clevel=5, shuffle=2)
+                data, _ = st.copy_compressed(l, layer)
+                ent = st.compressed_entries(l, layer)
+                lps = st.shard_geometry(l)[2]
+                key = (l, layer // lps)
+                if key not in rows:
+                    rows[key] = gpu.ShardAssembler(st, l)
+                rows[key].add_layer(data, ent)
+                done[l] += 1
+    st.close()
+    checked = 0
+    for (l, row), asm in rows.items():
+        od = OracleDims(ods.level_dims(l), U16)
+        cim = od.number_of_chunks_in_memory()
+        bpc = od.bytes_per_chunk()
+        blobs = asm.finalize()
+        want = {}  # (shard, internal) -> chunk bytes or None (no data)
+        for cl in range(asm.lps):
+            layer = row * asm.lps + cl
+            if (l, layer) not in exp:
+                continue
+            buf, flags = exp[(l, layer)]
+            for c in range(cim):
+                idx = cl * cim + c
+                key = (od.shard_index_for_chunk(idx), od.shard_internal_index(idx))
+                want[key] = buf[c * bpc:(c + 1) * bpc].tobytes() if flags[c] else None
+        for s, blob in enumerate(blobs):
+            offs, exts = parse_shard(blob, asm.cps)
+            for i in range(asm.cps):
+                w = want.get((s, i))
+                if w is None:
+                    assert offs[i] == gpu.SHARD_UNWRITTEN and exts[i] == gpu.SHARD_UNWRITTEN
+                    continue
+                fr = blob[offs[i]:offs[i] + exts[i]]
+                assert oracle_decode(fr) == w, (l, row, s, i)
+                checked += 1
+    assert checked > 0
