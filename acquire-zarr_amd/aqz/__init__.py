@@ -172,6 +172,8 @@ def lib():
         "aqz_stage_finalize": ([vp], i32),
         "aqz_stage_enable_kernel_timing": ([vp, i32], i32),
         "aqz_stage_kernel_timing": ([vp, C.POINTER(C.c_double), C.POINTER(u64)], i32),
+        "aqz_stage_timing_mark": ([vp, i32], i32),
+        "aqz_stage_timing_elapsed": ([vp, C.POINTER(C.c_double)], i32),
         "aqz_stage_dominant_kernel": ([vp], C.c_char_p),
         "aqz_stage_compress_layer": ([vp, u32, u64, C.POINTER(CompressionC)], i32),
         "aqz_stage_compressed_offsets": ([vp, u32, u64, C.POINTER(u64), sz], i32),
@@ -494,6 +496,17 @@ class Stage:
         n = C.c_uint64(0)
         _check(lib().aqz_stage_kernel_timing(self.h, C.byref(ms), C.byref(n)), "timing")
         return ms.value, n.value
+
+    def timing_mark(self, which):
+        """Record timing event `which` (0 = begin, 1 = end) on the stage's
+        stream, after everything enqueued so far."""
+        _check(lib().aqz_stage_timing_mark(self.h, which), "timing_mark")
+
+    def timing_elapsed(self):
+        """ms between the begin and end marks (waits for the end mark)."""
+        ms = C.c_double(0)
+        _check(lib().aqz_stage_timing_elapsed(self.h, C.byref(ms)), "timing_elapsed")
+        return ms.value
 
     def dominant_kernel(self):
         return lib().aqz_stage_dominant_kernel(self.h).decode()

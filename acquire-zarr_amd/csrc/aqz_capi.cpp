@@ -574,6 +574,22 @@ aqz_stage_kernel_timing(aqz_stage* st, double* total_ms, uint64_t* launches)
     return guard_sticky(st, [&] { st->st->timing(total_ms, launches); });
 }
 
+aqz_status
+aqz_stage_timing_mark(aqz_stage* st, int32_t which)
+{
+    return guard_sticky(st, [&] { st->st->mark(which); });
+}
+
+aqz_status
+aqz_stage_timing_elapsed(aqz_stage* st, double* ms)
+{
+    return guard_sticky(st, [&] {
+        const double v = st->st->marked_ms();
+        if (ms)
+            *ms = v;
+    });
+}
+
 const char*
 aqz_stage_dominant_kernel(const aqz_stage* st)
 {

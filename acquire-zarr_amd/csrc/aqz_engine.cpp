@@ -447,6 +447,9 @@ Stage::~Stage()
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
     }
+    for (hipEvent_t e : mark_ev_)
+        if (e)
+            (void)hipEventDestroy(e);
     if (own_stream_)
         (void)hipStreamDestroy(own_stream_);
 }
@@ -1404,10 +1407,40 @@ Stage::timing(double* total_ms, uint64_t* launches)
         *launches = timed_launches_;
 }
 
+// One timing event pair on the stream the kernels are launched on: the bench
+// brackets its whole timed region with it (a pair per launch adds gaps).
+void
+Stage::mark(int which)
+{
+    if (which != 0 && which != 1)
+        throw Error(1, "timing mark must be 0 (begin) or 1 (end)");
+    if (!mark_ev_[which])
+        hip_check(hipEventCreate(&mark_ev_[which]), "hipEventCreate");
+    hip_check(hipEventRecord(mark_ev_[which], stream_), "hipEventRecord");
+}
+
+double
+Stage::marked_ms()
+{
+    if (!mark_ev_[0] || !mark_ev_[1])
+        throw Error(1, "timing marks not recorded");
+    hip_check(hipEventSynchronize(mark_ev_[1]), "hipEventSynchronize");
+    float ms = 0;
+    hip_check(hipEventElapsedTime(&ms, mark_ev_[0], mark_ev_[1]), "hipEventElapsedTime");
+    return ms;
+}
+
 const char*
 Stage::dominant_kernel() const
 {
-    return fused_2d_ ? "fused_pyramid" : fused_3d_ ? "fused_pyramid_3d" : "level_kernel";
+    if (fused_2d_) {
+        // launch_interior's choice (aqz_kernels.hip) for this stage's launches
+        const bool tail = n_levels() - 1 > n_fused_;
+        const bool strip = bpp_ <= 4 && rh_log2_ == 6 && n_fused_ >= 3 &&
+                           !(knobs_ & 128u) && (!tail || n_fused_ >= 5);
+        return strip ? "fused_pyramid_strip" : "fused_pyramid";
+    }
+    return fused_3d_ ? "fused_pyramid_3d" : "level_kernel";
 }
 
 // ===========================================================================

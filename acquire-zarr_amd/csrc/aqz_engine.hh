@@ -236,6 +236,9 @@ class Stage
     void finalize();
     void enable_timing(bool on);
     void timing(double* total_ms, uint64_t* launches);
+    // timing events on the stage's stream bracketing a region of appends
+    void mark(int which);
+    double marked_ms();
     const char* dominant_kernel() const;
 
   private:
@@ -307,6 +310,7 @@ class Stage
     size_t ev_used_ = 0;
     double timed_ms_ = 0;
     uint64_t timed_launches_ = 0;
+    hipEvent_t mark_ev_[2] = { nullptr, nullptr };
 };
 
 class GpuDownsampler

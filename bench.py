@@ -437,12 +437,14 @@ def main():
         st = aqz.Stage(cfg["dims"], dt, cfg["method"], force_levels=cfg["force_levels"],
                        max_batch_frames=B, layer_slots=2, device=dev.index,
                        skip_level0_split=pyramid_only, first_frame=first)
-        st.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        # the stage runs on its own HIP stream; the timing marks below are
+        # recorded by the library on that same stream
         sizes = level_sizes(st)
         fbytes = sizes[0][0] * sizes[0][1] * bpp
         ring_frames = cfg["ring"]
         ring = torch.empty(ring_frames * fbytes, dtype=torch.uint8, device=dev)
         fill_ring(torch, ring, dt, 1234 + rank)
+        torch.cuda.synchronize(dev)  # torch's stream filled it; the stage's reads it
         nb = ring_frames // B
         base = ring.data_ptr()
 
@@ -451,20 +453,20 @@ def main():
 
         for s in range(warmup):
             step(s)
+        st.synchronize()
         torch.cuda.synchronize(dev)
         if dist:
             dist.barrier()
         torch.cuda.synchronize(dev)
-        # HIP events bracket the timed region on the stage's stream (torch's
-        # current stream): per-launch event pairs would add ~10 us of gap
-        # per launch to the very wall time being measured
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
+        # one HIP event pair, recorded by the library on the stream the
+        # kernels are launched on, brackets the timed region (a pair per
+        # launch would add ~10 us of gap per launch to the wall time)
         t0 = time.perf_counter()
-        ev0.record()
+        st.timing_mark(0)
         for s in range(steps):
             step(warmup + s)
-        ev1.record()
+        st.timing_mark(1)
+        st.synchronize()
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         if dist:
@@ -474,7 +476,7 @@ def main():
             t = torch.tensor([elapsed], dtype=torch.float64, device=reduce_dev(dist, dev))
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-        kms, launches = ev0.elapsed_time(ev1), steps
+        kms, launches = st.timing_elapsed(), steps
         if args.no_kernel_events:
             kms = elapsed * 1e3
         kernel = st.dominant_kernel()

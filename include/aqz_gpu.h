@@ -387,6 +387,12 @@ aqz_status aqz_stage_enable_kernel_timing(aqz_stage* st, int32_t enable);
  * synchronizes. */
 aqz_status aqz_stage_kernel_timing(aqz_stage* st, double* total_ms,
                                    uint64_t* launches);
+/* One timing event pair on the stage's stream (the stream its kernels run
+ * on): which = 0 records the begin mark, 1 the end mark, after all work
+ * enqueued so far.  aqz_stage_timing_elapsed waits for the end mark and
+ * returns the milliseconds between the two. */
+aqz_status aqz_stage_timing_mark(aqz_stage* st, int32_t which);
+aqz_status aqz_stage_timing_elapsed(aqz_stage* st, double* ms);
 /* Name of the dominant kernel symbol (for matching rocprof output). */
 const char* aqz_stage_dominant_kernel(const aqz_stage* st);
 
