@@ -461,6 +461,7 @@ def main():
         # one HIP event pair, recorded by the library on the stream the
         # kernels are launched on, brackets the timed region (a pair per
         # launch would add ~10 us of gap per launch to the wall time)
+        fw0 = [st.frames_written(l) for l in range(len(sizes))]
         t0 = time.perf_counter()
         st.timing_mark(0)
         for s in range(steps):
@@ -480,10 +481,14 @@ def main():
         if args.no_kernel_events:
             kms = elapsed * 1e3
         kernel = st.dominant_kernel()
+        # algorithmic bytes per launch: every input frame read once, plus
+        # every frame each level emitted in the timed region written once
+        # (a z-halving level emits half as many frames as its parent)
+        emitted = [st.frames_written(l) - fw0[l] for l in range(len(sizes))]
         st.close()
         del ring
-        out_bytes = sum(h * w * bpp for (h, w) in sizes[1:])
-        alg = B * (fbytes + (0 if pyramid_only else fbytes) + out_bytes)
+        out_bytes = sum(n * h * w * bpp for n, (h, w) in zip(emitted[1:], sizes[1:]))
+        alg = (emitted[0] * fbytes * (1 if pyramid_only else 2) + out_bytes) // max(1, steps)
         avg_ms = kms / max(1, launches)
         return dict(elapsed=elapsed, sizes=sizes, fbytes=fbytes, kernel=kernel,
                     avg_ms=avg_ms, alg=alg,
