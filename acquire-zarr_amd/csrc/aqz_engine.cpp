@@ -391,6 +391,7 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
     }
     hip_check(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking), "hipStreamCreate");
     hip_check(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking), "hipStreamCreate");
+    hip_check(hipStreamCreateWithFlags(&comp_, hipStreamNonBlocking), "hipStreamCreate");
     for (auto& L : lv_) {
         hip_check(hipEventCreateWithFlags(&L.ops_ev, hipEventDisableTiming),
                   "hipEventCreate");
@@ -415,7 +416,7 @@ Stage::~Stage()
 {
     if (stream_)
         (void)hipStreamSynchronize(stream_);
-    for (hipStream_t s : { h2d_, d2h_ })
+    for (hipStream_t s : { h2d_, comp_, d2h_ })
         if (s) {
             (void)hipStreamSynchronize(s);
             (void)hipStreamDestroy(s);
@@ -439,6 +440,9 @@ Stage::~Stage()
             if (e)
                 (void)hipEventDestroy(e);
         for (hipEvent_t e : L.comp_ev)
+            if (e)
+                (void)hipEventDestroy(e);
+        for (hipEvent_t e : L.cdone_ev)
             if (e)
                 (void)hipEventDestroy(e);
     }
@@ -494,6 +498,7 @@ Stage::synchronize()
 {
     hip_check(hipStreamSynchronize(h2d_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    hip_check(hipStreamSynchronize(comp_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(d2h_), "hipStreamSynchronize");
     retire_consumed(true);
 }
@@ -557,6 +562,7 @@ Stage::frames_consumed()
 void
 Stage::wait_copies()
 {
+    hip_check(hipStreamSynchronize(comp_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(d2h_), "hipStreamSynchronize");
 }
 
@@ -1286,6 +1292,7 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
         throw Error(3, "chunk layer not resident");
     if (!L.comp || L.comp_cfg.codec != c.codec || L.comp_cfg.clevel != c.clevel ||
         L.comp_cfg.shuffle != c.shuffle) {
+        hip_check(hipStreamSynchronize(comp_), "hipStreamSynchronize");
         hip_check(hipStreamSynchronize(d2h_), "hipStreamSynchronize");
         L.comp = std::make_unique<Compressor>(L.bpc, uint32_t(bpp_), c);
         L.comp_cfg = c;
@@ -1295,27 +1302,42 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
         L.coffsets.resize(L.n_slots);
         L.h_coffsets.resize(L.n_slots);
         L.comp_ev.assign(L.n_slots, nullptr);
+        L.cdone_ev.assign(L.n_slots, nullptr);
+        L.cdone_pending.assign(L.n_slots, 0);
         L.comp_layer.assign(L.n_slots, -1);
-        for (uint32_t s = 0; s < L.n_slots; ++s)
+        for (uint32_t s = 0; s < L.n_slots; ++s) {
             hip_check(hipEventCreateWithFlags(&L.comp_ev[s], hipEventDisableTiming),
                       "hipEventCreate");
+            hip_check(hipEventCreateWithFlags(&L.cdone_ev[s], hipEventDisableTiming),
+                      "hipEventCreate");
+        }
     }
-    L.cframes[slot].alloc(Compressor::max_bytes(L.bpc, L.n_chunks));
+    // the slot's previous frames may still be on their way to the host
+    if (L.cdone_pending[slot]) {
+        hip_check(hipStreamWaitEvent(comp_, L.cdone_ev[slot], 0), "hipStreamWaitEvent");
+        L.cdone_pending[slot] = 0;
+    }
+    const uint64_t cap = Compressor::max_bytes(L.bpc, L.n_chunks);
+    if (L.cframes[slot].n < cap)
+        hip_check(hipStreamSynchronize(comp_), "hipStreamSynchronize"); // realloc below
+    L.cframes[slot].alloc(cap);
     L.coffsets[slot].alloc((size_t(L.n_chunks) + 1) * 8);
     L.h_coffsets[slot].alloc((size_t(L.n_chunks) + 1) * 8);
-    // after every kernel enqueued so far; the slot's next layer waits for it
+    // after every kernel enqueued so far; the slot's next layer waits for it.
+    // Compression runs on its own stream: it overlaps the D2H of the frames
+    // of earlier layers on the hand-off stream.
     hip_check(hipEventRecord(L.ready_ev[slot], stream_), "hipEventRecord");
-    hip_check(hipStreamWaitEvent(d2h_, L.ready_ev[slot], 0), "hipStreamWaitEvent");
+    hip_check(hipStreamWaitEvent(comp_, L.ready_ev[slot], 0), "hipStreamWaitEvent");
     L.comp->run(L.ring.p + slot * L.slot_bytes, L.pitch, L.n_chunks,
                 reinterpret_cast<const uint32_t*>(L.flags.p) + size_t(slot) * L.n_chunks,
                 uint32_t(layer / L.n_slots + 1), L.cframes[slot].p,
-                reinterpret_cast<uint64_t*>(L.coffsets[slot].p), d2h_,
+                reinterpret_cast<uint64_t*>(L.coffsets[slot].p), comp_,
                 reinterpret_cast<const uint32_t*>(L.shard_order.p));
     hip_check(hipMemcpyAsync(L.h_coffsets[slot].p, L.coffsets[slot].p,
-                             (size_t(L.n_chunks) + 1) * 8, hipMemcpyDeviceToHost, d2h_),
+                             (size_t(L.n_chunks) + 1) * 8, hipMemcpyDeviceToHost, comp_),
               "hipMemcpyAsync");
-    hip_check(hipEventRecord(L.comp_ev[slot], d2h_), "hipEventRecord");
-    hip_check(hipEventRecord(L.copy_ev[slot], d2h_), "hipEventRecord");
+    hip_check(hipEventRecord(L.comp_ev[slot], comp_), "hipEventRecord");
+    hip_check(hipEventRecord(L.copy_ev[slot], comp_), "hipEventRecord");
     L.copy_pending[slot] = 1;
     L.comp_layer[slot] = int64_t(layer);
 }
@@ -1351,7 +1373,9 @@ Stage::copy_compressed_async(uint32_t level, uint64_t layer, void* dst, size_t c
         throw Error(2, "destination too small for the compressed layer");
     memcpy_pieces(dst, L.cframes[slot].p, total, hipMemcpyDefault, d2h_);
     hip_check(hipEventRecord(L.copy_ev[slot], d2h_), "hipEventRecord");
+    hip_check(hipEventRecord(L.cdone_ev[slot], d2h_), "hipEventRecord");
     L.copy_pending[slot] = 1;
+    L.cdone_pending[slot] = 1;
 }
 
 void

@@ -176,6 +176,8 @@ struct StageLevel
     std::vector<DevBuf> cframes, coffsets;
     std::vector<PinnedBuf> h_coffsets;
     std::vector<hipEvent_t> comp_ev;
+    std::vector<hipEvent_t> cdone_ev;      // the slot's frames were copied out
+    std::vector<uint8_t> cdone_pending;
     std::vector<int64_t> comp_layer;       // layer compressed in each slot
     // shard packing: compressed frames leave in shard-major order
     // (shard_index_for_chunk, then shard_internal_index); internal indices
@@ -288,6 +290,9 @@ class Stage
     bool consume_rec_[2] = { false, false };
     int stage_idx_ = 0;
     hipStream_t h2d_ = nullptr, d2h_ = nullptr;
+    // device compression of handed-off layers runs on comp_, so layer i+1
+    // compresses while layer i's frames go D2H on d2h_
+    hipStream_t comp_ = nullptr;
     std::unique_ptr<CopyPool> pool_;
     // XY-transposed storage order: level-0 frames are transposed into xbuf_
     // (acquisition rows x cols -> storage rows x cols) before the pipeline

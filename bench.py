@@ -39,7 +39,7 @@ CONFIGS = {
                         "256x256 chunks (t-chunk 64), mean, level-0 split + pyramid + "
                         "tile split of all levels, device-resident",
                dims=[(TIME, 0, 64, 1), (SPACE, 2048, 256, 1), (SPACE, 2048, 256, 1)],
-               dtype=U16, method=MEAN, force_levels=5, batch=64, ring=256),
+               dtype=U16, method=MEAN, force_levels=5, batch=128, ring=256),
     # same, reference level rule (4 levels)
     "c2-ref4": dict(workload="uint16 2048x2048 frames, 4-level pyramid (reference rule "
                              "at 256-px chunks), t-chunk 64, mean, device-resident",
@@ -423,7 +423,7 @@ def main():
     import aqz
     cfg = CONFIGS[args.config]
     dt = cfg["dtype"]
-    B = cfg["batch"]
+    B = args.batch or cfg["batch"]
     bpp = BPP[dt]
     first = 0
     if args.config == "c4" and world > 1:
