@@ -19,7 +19,8 @@ import subprocess
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libaqz_gpu.so")
+# AQZ_LIB: dev A/B of two builds in separate processes (tools/); default in-tree
+LIB_PATH = os.environ.get("AQZ_LIB") or os.path.join(PKG_DIR, "libaqz_gpu.so")
 
 UINT8, UINT16, UINT32, UINT64, INT8, INT16, INT32, INT64, FLOAT32, FLOAT64 = range(10)
 DECIMATE, MEAN, MIN, MAX = range(4)

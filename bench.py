@@ -57,7 +57,7 @@ CONFIGS = {
                         "pyramid, 256x256x64 chunks, mean, device-resident",
                dims=[(TIME, 0, 1, 1), (SPACE, 256, 64, 1), (SPACE, 2048, 256, 1),
                      (SPACE, 2048, 256, 1)],
-               dtype=U16, method=MEAN, force_levels=0, batch=64, ring=256),
+               dtype=U16, method=MEAN, force_levels=0, batch=128, ring=256),
     "c5": dict(workload="float32 8192x8192 frames, 7-level pyramid, 128x128 chunks, mean, "
                         "device-resident (one camera stream per GPU)",
                dims=[(TIME, 0, 4, 1), (SPACE, 8192, 128, 1), (SPACE, 8192, 128, 1)],
