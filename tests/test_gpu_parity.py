@@ -274,6 +274,31 @@ def test_stage_device_resident_input(gpu):
         assert (gflags == flags).all()
 
 
+def test_stage_timing_marks(gpu):
+    """The bench's timing pair (aqz_stage_timing_mark/_elapsed) brackets the
+    kernels of the appends between the marks on the stage's own stream."""
+    import torch
+    dims = [(TIME, 0, 8, 1), (SPACE, 1024, 256, 1), (SPACE, 1024, 256, 1)]
+    st = gpu.Stage(dims, U16, MEAN, max_batch_frames=8)
+    with pytest.raises(gpu.AqzError):
+        st.timing_elapsed()  # no marks yet
+    with pytest.raises(gpu.AqzError):
+        st.timing_mark(2)
+    t = torch.zeros(8 * 1024 * 1024, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    st.timing_mark(0)
+    st.timing_mark(1)
+    empty = st.timing_elapsed()
+    st.timing_mark(0)
+    for _ in range(20):
+        st.append_ptr(t.data_ptr(), 8)
+    st.timing_mark(1)
+    busy = st.timing_elapsed()
+    st.synchronize()
+    assert 0 <= empty < busy, (empty, busy)
+    st.close()
+
+
 # ---------------------------------------------------------------------------
 # 2x2x2 fused path (regular z schedule) and z-slab sharding
 # ---------------------------------------------------------------------------
