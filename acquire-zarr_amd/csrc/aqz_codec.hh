@@ -20,8 +20,13 @@
 namespace aqz {
 
 // bytes of one LZ4-compressed stream (resident in LDS while it is encoded)
-constexpr uint32_t kLz4StreamMax = 8192;
-constexpr int kLz4HashLog = 11;
+// and the hash table size.  The encoder is latency-bound, so occupancy
+// rules: 4 KiB streams + a 1024-entry table (6 KiB of LDS, 77 VGPRs: 24
+// waves/CU) ran camera-like u16 chunks 1.4x (byte shuffle) and 1.3x
+// (bitshuffle) faster than 8 KiB + 2048 entries (12 KiB, 103 VGPRs: 13
+// waves/CU) for a ratio 0.3-1.2% lower; 2 KiB streams were no faster.
+constexpr uint32_t kLz4StreamMax = 4096;
+constexpr int kLz4HashLog = 10;
 
 // The blosc1 frame geometry shared by every chunk of a layer.
 struct BloscGeom
