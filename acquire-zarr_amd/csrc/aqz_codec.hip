@@ -525,6 +525,43 @@ put32(uint8_t* d, uint32_t v)
     d[3] = uint8_t(v >> 24);
 }
 
+// n bytes s -> d for any alignment of either, by the whole workgroup:
+// dword stores at dword-aligned destinations, each assembled from two
+// aligned source dwords (v_alignbyte); only the head and tail go by byte.
+// Never reads past s + n.
+__device__ __forceinline__ void
+copy_bytes(uint8_t* d, const uint8_t* s, uint32_t n)
+{
+    const uint32_t t = threadIdx.x, nt = blockDim.x;
+    uint32_t head = (4u - uint32_t(reinterpret_cast<uintptr_t>(d) & 3u)) & 3u;
+    if (head > n)
+        head = n;
+    for (uint32_t k = t; k < head; k += nt)
+        d[k] = s[k];
+    d += head;
+    s += head;
+    n -= head;
+    const uint32_t nw = n / 4;
+    uint32_t* dw = reinterpret_cast<uint32_t*>(d);
+    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(s) & 3u);
+    if (sh == 0) {
+        const uint32_t* sw = reinterpret_cast<const uint32_t*>(s);
+        for (uint32_t i = t; i < nw; i += nt)
+            dw[i] = sw[i];
+    } else {
+        // source dwords i and i+1 cover destination dword i; the last one
+        // would read up to 3 bytes past the end, so it goes by byte
+        const uint32_t* sw = reinterpret_cast<const uint32_t*>(s - sh);
+        for (uint32_t i = t; i + 1 < nw; i += nt)
+            dw[i] = __builtin_amdgcn_alignbyte(sw[i + 1], sw[i], sh);
+        if (nw > 0 && t == 0)
+            for (uint32_t k = 4 * (nw - 1); k < 4 * nw; ++k)
+                d[k] = s[k];
+    }
+    for (uint32_t k = 4 * nw + t; k < n; k += nt)
+        d[k] = s[k];
+}
+
 __global__ __launch_bounds__(256) void
 write_frames(const BloscParams p)
 {
@@ -548,9 +585,8 @@ write_frames(const BloscParams p)
     const uint8_t* chunk = p.chunks + c * p.pitch;
     if (memcpyed) {
         const uint32_t per = (p.g.nbytes + p.g.spc - 1) / p.g.spc;
-        const uint32_t x0 = q * per, x1 = min(p.g.nbytes, x0 + per);
-        for (uint32_t x = x0 + threadIdx.x; x < x1; x += 256)
-            o[16 + x] = chunk[x];
+        const uint32_t x0 = min(p.g.nbytes, q * per), x1 = min(p.g.nbytes, x0 + per);
+        copy_bytes(o + 16 + x0, chunk + x0, x1 - x0);
         return;
     }
     const uint64_t sidx = uint64_t(c) * p.g.spc;
@@ -562,9 +598,7 @@ write_frames(const BloscParams p)
     uint8_t* rec = o + p.spos[gid];
     if (threadIdx.x == 0)
         put32(rec, n);
-    const uint8_t* s = p.scratch + uint64_t(gid) * p.g.slot;
-    for (uint32_t k = threadIdx.x; k < n; k += 256)
-        rec[4 + k] = s[k];
+    copy_bytes(rec + 4, p.scratch + uint64_t(gid) * p.g.slot, n);
 }
 
 } // namespace
