@@ -104,8 +104,9 @@ def pmc_traffic(config, pyramid_only, kernel):
 def cpu_baseline(cfg, seconds):
     """The reference's CPU path timed on this host's cores (rank 0 only):
     the compiled reference (oracle/_ref) when present, else the C port.
-    Single thread (Downsampler::add_frame runs on the one frame-consumer
-    thread, zarr.stream.cpp:1683-1684)."""
+    Downsampler::add_frame runs on the one frame-consumer thread
+    (zarr.stream.cpp:1683-1684); the reference's tile split is OpenMP over
+    tiles (array.cpp:575), so its restated loop runs on OMP_NUM_THREADS."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_bindings as ob
     dims = list(cfg["dims"])
@@ -161,10 +162,16 @@ def cpu_baseline(cfg, seconds):
         for s in sp:
             R.ref_split_destroy(s)
     gbs = n * frames[0].nbytes / el / 1e9
-    return {"value": round(gbs, 4), "unit": "GB/s", "cores": 1, "kind": kind,
-            "sample": f"{n} frames of {h}x{w} {ob.DTYPE_NAMES[dt]} ({el:.1f} s): "
-                      f"Downsampler::add_frame+take_frame ({L} levels) + tile split of "
-                      f"every level, single thread"}
+    if kind == "reference":
+        threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+        how = (f"Downsampler::add_frame+take_frame ({L} levels) on the one consumer "
+               f"thread + the tile split of every level with OpenMP over tiles "
+               f"(array.cpp:575) on {threads} threads")
+    else:
+        threads = 1
+        how = f"C port: downsample ({L} levels) + tile split of every level, single thread"
+    return {"value": round(gbs, 4), "unit": "GB/s", "cores": threads, "kind": kind,
+            "sample": f"{n} frames of {h}x{w} {ob.DTYPE_NAMES[dt]} ({el:.1f} s): {how}"}
 
 
 def reduce_dev(dist, dev):

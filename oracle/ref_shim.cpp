@@ -310,6 +310,9 @@ ref_split_write(void* h, uint64_t fid, const void* frame)
     const uint64_t internal = dims->chunk_internal_offset(fid);
     const auto* src = static_cast<const uint8_t*>(frame);
     size_t written = 0;
+    // the reference's tile loop is OpenMP-parallel (array.cpp:575); each
+    // tile owns its chunk, so the lazy allocation below needs no lock here
+#pragma omp parallel for schedule(static) reduction(+ : written)
     for (uint32_t t = 0; t < ntx * nty; ++t) {
         auto& chunk = s->chunks[t + group];
         if (!chunk)
