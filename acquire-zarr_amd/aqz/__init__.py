@@ -61,8 +61,16 @@ class ArrayDescC(C.Structure):
 
 class StageOptionsC(C.Structure):
     _fields_ = [("layer_slots", C.c_uint32), ("max_batch_frames", C.c_uint32),
-                ("force_levels", C.c_uint32), ("skip_level0_split", C.c_int32),
-                ("blocks_per_cu", C.c_uint32), ("first_frame", C.c_uint64)]
+                ("first_frame", C.c_uint64)]
+
+
+class StageBenchOptionsC(C.Structure):
+    """aqz_stage_bench_options (include/aqz_gpu_bench.h): not drop-in ABI."""
+    _fields_ = [("force_levels", C.c_uint32), ("skip_level0_split", C.c_int32)]
+
+
+class MemoryUsageC(C.Structure):
+    _fields_ = [("device_bytes", C.c_uint64), ("pinned_bytes", C.c_uint64)]
 
 
 class CompressionC(C.Structure):
@@ -145,6 +153,10 @@ def lib():
         "aqz_dims_shard_index_for_chunk": ([vp, u32], u32),
         "aqz_dims_shard_internal_index": ([vp, u32], u32),
         "aqz_pyramid_levels": ([D, sz, u32, C.POINTER(u32), D, sz], i32),
+        "aqz_dims_dim1_banding": ([vp, C.POINTER(i32), C.POINTER(u32), C.POINTER(u64),
+                                   C.POINTER(u32)], i32),
+        "aqz_downsampling_method_name": ([i32], C.c_char_p),
+        "aqz_downsampling_metadata_json": ([i32, C.c_char_p, sz, C.POINTER(sz)], i32),
         "aqz_downsampler_create": ([C.POINTER(ArrayDescC), C.POINTER(vp)], i32),
         "aqz_downsampler_destroy": ([vp], None),
         "aqz_downsampler_n_levels": ([vp], u32),
@@ -154,6 +166,15 @@ def lib():
         "aqz_downsampler_method_name": ([vp], C.c_char_p),
         "aqz_downsampler_metadata_json": ([vp, C.c_char_p, sz, C.POINTER(sz)], i32),
         "aqz_stage_create": ([C.POINTER(ArrayDescC), C.POINTER(StageOptionsC), C.POINTER(vp)], i32),
+        "aqz_stage_create_bench": ([C.POINTER(ArrayDescC), C.POINTER(StageOptionsC),
+                                    C.POINTER(StageBenchOptionsC), C.POINTER(vp)], i32),
+        "aqz_stage_wait_stream": ([vp, vp], i32),
+        "aqz_stage_band_geometry": ([vp, u32, C.POINTER(i32), C.POINTER(u32), C.POINTER(u64),
+                                     C.POINTER(u32)], i32),
+        "aqz_stage_copy_band_async": ([vp, u32, u64, u32, vp, sz, vp, sz], i32),
+        "aqz_stage_memory_usage": ([vp, C.POINTER(MemoryUsageC)], i32),
+        "aqz_stage_estimate_memory": ([C.POINTER(ArrayDescC), C.POINTER(StageOptionsC),
+                                       C.POINTER(MemoryUsageC)], i32),
         "aqz_stage_destroy": ([vp], None),
         "aqz_stage_n_levels": ([vp], u32),
         "aqz_stage_level_dims": ([vp, u32, D, sz, C.POINTER(sz)], i32),
@@ -277,6 +298,39 @@ class Dims:
 
     def shard_internal_index(self, c):
         return lib().aqz_dims_shard_internal_index(self.h, c)
+
+    def dim1_banding(self):
+        """(supported, n_bands, frames_per_band, chunks_per_band)"""
+        a, b, c, d = C.c_int32(), C.c_uint32(), C.c_uint64(), C.c_uint32()
+        _check(lib().aqz_dims_dim1_banding(self.h, C.byref(a), C.byref(b), C.byref(c),
+                                           C.byref(d)), "aqz_dims_dim1_banding")
+        return bool(a.value), b.value, c.value, d.value
+
+
+def downsampling_method_name(method):
+    """Downsampler::downsampling_method for a method value (no GPU)."""
+    return lib().aqz_downsampling_method_name(method).decode()
+
+
+def downsampling_metadata_json(method):
+    """Downsampler::get_metadata().dump() for a method value (no GPU)."""
+    n = C.c_size_t(0)
+    _check(lib().aqz_downsampling_metadata_json(method, None, 0, C.byref(n)), "metadata")
+    buf = C.create_string_buffer(n.value + 1)
+    _check(lib().aqz_downsampling_metadata_json(method, buf, n.value + 1, C.byref(n)),
+           "metadata")
+    return buf.value.decode()
+
+
+def estimate_memory(dims, dtype, method, max_levels=0, layer_slots=0,
+                    max_batch_frames=0, storage_order=None):
+    """aqz_stage_estimate_memory: upper bound of a stage's footprint (no GPU)."""
+    d, keep = _desc(dims, dtype, method, max_levels, True, storage_order, 0)
+    o = StageOptionsC(layer_slots, max_batch_frames, 0)
+    m = MemoryUsageC()
+    _check(lib().aqz_stage_estimate_memory(C.byref(d), C.byref(o), C.byref(m)),
+           "aqz_stage_estimate_memory")
+    return {"device_bytes": m.device_bytes, "pinned_bytes": m.pinned_bytes}
 
 
 def pyramid_levels(dims, max_levels=0):
@@ -402,21 +456,30 @@ class Downsampler:
 
 
 class Stage:
-    """Device-resident multiscale stage: tile split + pyramid of every level."""
+    """Device-resident multiscale stage: tile split + pyramid of every level.
+
+    force_levels / skip_level0_split are the bench-only extensions of
+    include/aqz_gpu_bench.h (aqz_stage_create_bench); everything else is the
+    drop-in ABI of include/aqz_gpu.h."""
 
     def __init__(self, dims, dtype, method, max_levels=0, multiscale=True,
                  storage_order=None, device=0, layer_slots=0,
                  max_batch_frames=0, force_levels=0, skip_level0_split=False,
-                 blocks_per_cu=0, first_frame=0):
+                 first_frame=0):
         self.dtype = dtype
         d, self._keep = _desc(dims, dtype, method, max_levels, multiscale,
                               storage_order, device)
-        o = StageOptionsC(layer_slots, max_batch_frames, force_levels,
-                          1 if skip_level0_split else 0, blocks_per_cu, first_frame)
+        o = StageOptionsC(layer_slots, max_batch_frames, first_frame)
         h = C.c_void_p()
-        _check(lib().aqz_stage_create(C.byref(d), C.byref(o), C.byref(h)),
-               "aqz_stage_create")
+        if force_levels or skip_level0_split:
+            b = StageBenchOptionsC(force_levels, 1 if skip_level0_split else 0)
+            rc = lib().aqz_stage_create_bench(C.byref(d), C.byref(o), C.byref(b), C.byref(h))
+        else:
+            rc = lib().aqz_stage_create(C.byref(d), C.byref(o), C.byref(h))
+        _check(rc, "aqz_stage_create")
         self.h = h
+        self._held = []  # (appended count, CUDA tensor) still being read
+        self._appended = 0
 
     def close(self):
         if getattr(self, "h", None) and _lib is not None:
@@ -448,16 +511,61 @@ class Stage:
         _check(lib().aqz_stage_set_tuning(self.h, knobs, nt), "set_tuning")
 
     def append(self, frames, n_frames=None):
+        """Append frames from a numpy array (pageable), a HostBuffer (pinned)
+        or a torch tensor.  A CUDA tensor is read on the stage's own stream:
+        that stream first waits for the work torch has queued on the
+        tensor's current stream (no host sync), and the tensor is kept
+        alive until the stage reports its frames consumed."""
         p, mem = _ptr(frames)
         if n_frames is None:
             n_frames = frames.shape[0] if frames.ndim == 3 else 1
+        cuda = mem == MEM_DEVICE and hasattr(frames, "data_ptr")
+        if cuda:
+            import torch
+            s = torch.cuda.current_stream(frames.device).cuda_stream
+            _check(lib().aqz_stage_wait_stream(self.h, s), "wait_stream")
         _check(lib().aqz_stage_append(self.h, p, n_frames, mem), "append")
+        self._appended += n_frames
+        if cuda:
+            self._held.append((self._appended, frames))
+        self._release_consumed()
 
     def append_ptr(self, ptr, n_frames, mem=MEM_DEVICE):
+        """Append from a raw pointer; the caller orders and keeps its
+        memory (see frames_consumed)."""
         _check(lib().aqz_stage_append(self.h, ptr, n_frames, mem), "append")
+        self._appended += n_frames
+
+    def wait_stream(self, stream_ptr):
+        _check(lib().aqz_stage_wait_stream(self.h, stream_ptr), "wait_stream")
+
+    def _release_consumed(self):
+        if self._held:
+            done = self.frames_consumed()
+            self._held = [(n, t) for n, t in self._held if n > done]
+
+    def band_geometry(self, level):
+        """(supported, n_bands, frames_per_band, chunks_per_band) of dim-1
+        banding (Array::flush_completed_bands_)."""
+        a, b, c, d = C.c_int32(), C.c_uint32(), C.c_uint64(), C.c_uint32()
+        _check(lib().aqz_stage_band_geometry(self.h, level, C.byref(a), C.byref(b),
+                                             C.byref(c), C.byref(d)), "band_geometry")
+        return bool(a.value), b.value, c.value, d.value
+
+    def copy_band_async(self, level, layer, band, dst_ptr, cap, has_data_ptr=None,
+                        has_data_cap=0):
+        _check(lib().aqz_stage_copy_band_async(self.h, level, layer, band, dst_ptr, cap,
+                                               has_data_ptr, has_data_cap),
+               "copy_band_async")
+
+    def memory_usage(self):
+        m = MemoryUsageC()
+        _check(lib().aqz_stage_memory_usage(self.h, C.byref(m)), "memory_usage")
+        return {"device_bytes": m.device_bytes, "pinned_bytes": m.pinned_bytes}
 
     def synchronize(self):
         _check(lib().aqz_stage_synchronize(self.h), "synchronize")
+        self._release_consumed()
 
     def frames_written(self, level):
         return lib().aqz_stage_frames_written(self.h, level)
@@ -488,6 +596,7 @@ class Stage:
 
     def finalize(self):
         _check(lib().aqz_stage_finalize(self.h), "finalize")
+        self._release_consumed()
 
     def enable_kernel_timing(self, on=True):
         _check(lib().aqz_stage_enable_kernel_timing(self.h, 1 if on else 0), "timing")

@@ -1,6 +1,7 @@
 // aqz_capi.cpp -- extern "C" boundary (include/aqz_gpu.h).  No exception or
 // HIP error crosses it: everything maps to a ZarrStatusCode value.
 #include "aqz_gpu.h"
+#include "aqz_gpu_bench.h"
 
 #include "aqz_engine.hh"
 
@@ -275,6 +276,24 @@ aqz_dims_shard_internal_index(const aqz_dims* d, uint32_t c)
 }
 
 aqz_status
+aqz_dims_dim1_banding(const aqz_dims* d, int32_t* supported, uint32_t* n_bands,
+                      uint64_t* frames_per_band, uint32_t* chunks_per_band)
+{
+    if (!d)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    const ArrayDimensions& a = *d->ad;
+    if (supported)
+        *supported = a.supports_dim1_banding() ? 1 : 0;
+    if (n_bands)
+        *n_bands = a.dim1_band_count();
+    if (frames_per_band)
+        *frames_per_band = a.frames_per_dim1_band();
+    if (chunks_per_band)
+        *chunks_per_band = a.chunks_per_dim1_band();
+    return AQZ_STATUS_SUCCESS;
+}
+
+aqz_status
 aqz_pyramid_levels(const aqz_dimension* dims, size_t ndims, uint32_t max_levels,
                    uint32_t* n_levels, aqz_dimension* out_dims, size_t out_cap)
 {
@@ -367,28 +386,47 @@ aqz_downsampler_method_name(const aqz_downsampler* ds)
     return ds ? ds->ds->method_name() : "";
 }
 
+static void
+put_string(const std::string& s, char* buf, size_t cap, size_t* len)
+{
+    if (len)
+        *len = s.size();
+    if (buf) {
+        if (cap < s.size() + 1)
+            throw Error(AQZ_STATUS_OVERFLOW, "buffer too small");
+        std::memcpy(buf, s.c_str(), s.size() + 1);
+    }
+}
+
 aqz_status
 aqz_downsampler_metadata_json(const aqz_downsampler* ds, char* buf, size_t cap,
                               size_t* len)
 {
     if (!ds)
         return AQZ_STATUS_INVALID_ARGUMENT;
-    return guard([&] {
-        const std::string s = ds->ds->metadata_json();
-        if (len)
-            *len = s.size();
-        if (buf) {
-            if (cap < s.size() + 1)
-                throw Error(AQZ_STATUS_OVERFLOW, "buffer too small");
-            std::memcpy(buf, s.c_str(), s.size() + 1);
-        }
-    });
+    return guard([&] { put_string(ds->ds->metadata_json(), buf, cap, len); });
+}
+
+const char*
+aqz_downsampling_method_name(int32_t method)
+{
+    try {
+        return downsampling_method_name(method);
+    } catch (...) {
+        return "";
+    }
+}
+
+aqz_status
+aqz_downsampling_metadata_json(int32_t method, char* buf, size_t cap, size_t* len)
+{
+    return guard([&] { put_string(downsampling_metadata_json(method), buf, cap, len); });
 }
 
 // ---- stage ---------------------------------------------------------------------
-aqz_status
-aqz_stage_create(const aqz_array_desc* desc, const aqz_stage_options* opt,
-                 aqz_stage** out)
+static aqz_status
+create_stage(const aqz_array_desc* desc, const aqz_stage_options* opt,
+             const aqz_stage_bench_options* bench, aqz_stage** out)
 {
     if (!out)
         return AQZ_STATUS_INVALID_ARGUMENT;
@@ -399,10 +437,11 @@ aqz_stage_create(const aqz_array_desc* desc, const aqz_stage_options* opt,
         if (opt) {
             o.layer_slots = opt->layer_slots;
             o.max_batch_frames = opt->max_batch_frames;
-            o.force_levels = opt->force_levels;
-            o.skip_level0_split = opt->skip_level0_split != 0;
-            o.blocks_per_cu = opt->blocks_per_cu;
             o.first_frame = opt->first_frame;
+        }
+        if (bench) {
+            o.force_levels = bench->force_levels;
+            o.skip_level0_split = bench->skip_level0_split != 0;
         }
         auto* s = new aqz_stage;
         try {
@@ -412,6 +451,78 @@ aqz_stage_create(const aqz_array_desc* desc, const aqz_stage_options* opt,
             throw;
         }
         *out = s;
+    });
+}
+
+aqz_status
+aqz_stage_create(const aqz_array_desc* desc, const aqz_stage_options* opt,
+                 aqz_stage** out)
+{
+    return create_stage(desc, opt, nullptr, out);
+}
+
+aqz_status
+aqz_stage_create_bench(const aqz_array_desc* desc, const aqz_stage_options* opt,
+                       const aqz_stage_bench_options* bench, aqz_stage** out)
+{
+    return create_stage(desc, opt, bench, out);
+}
+
+aqz_status
+aqz_stage_estimate_memory(const aqz_array_desc* desc, const aqz_stage_options* opt,
+                          aqz_memory_usage* out)
+{
+    if (!out)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard([&] {
+        const ArrayDesc a = to_desc(desc);
+        StageOptions o;
+        if (opt) {
+            o.layer_slots = opt->layer_slots;
+            o.max_batch_frames = opt->max_batch_frames;
+            o.first_frame = opt->first_frame;
+        }
+        const Footprint f = Stage::estimate_memory(a, o);
+        *out = aqz_memory_usage{ f.device, f.pinned };
+    });
+}
+
+aqz_status
+aqz_stage_memory_usage(const aqz_stage* st, aqz_memory_usage* out)
+{
+    if (!st || !out)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard([&] {
+        const Footprint f = st->st->memory_usage();
+        *out = aqz_memory_usage{ f.device, f.pinned };
+    });
+}
+
+aqz_status
+aqz_stage_wait_stream(aqz_stage* st, void* stream)
+{
+    return guard_sticky(
+      st, [&] { st->st->wait_stream(static_cast<hipStream_t>(stream)); });
+}
+
+aqz_status
+aqz_stage_band_geometry(const aqz_stage* st, uint32_t level, int32_t* supported,
+                        uint32_t* n_bands, uint64_t* frames_per_band,
+                        uint32_t* chunks_per_band)
+{
+    if (!st)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard([&] {
+        st->st->band_geometry(level, supported, n_bands, frames_per_band, chunks_per_band);
+    });
+}
+
+aqz_status
+aqz_stage_copy_band_async(aqz_stage* st, uint32_t level, uint64_t layer, uint32_t band,
+                          void* dst, size_t cap, uint8_t* has_data, size_t has_data_cap)
+{
+    return guard_sticky(st, [&] {
+        st->st->copy_band_async(level, layer, band, dst, cap, has_data, has_data_cap);
     });
 }
 

@@ -454,6 +454,8 @@ Stage::~Stage()
     for (hipEvent_t e : mark_ev_)
         if (e)
             (void)hipEventDestroy(e);
+    if (ext_ev_)
+        (void)hipEventDestroy(ext_ev_);
     if (own_stream_)
         (void)hipStreamDestroy(own_stream_);
 }
@@ -573,6 +575,7 @@ Stage::append(const void* frames, uint64_t n_frames, int mem)
         return;
     if (!frames)
         throw Error(1, "null frames");
+    finalized_ = false;
     const uint64_t fbytes = uint64_t(lv_[0].W) * lv_[0].H * bpp_;
     uint64_t n_ok = n_frames;
     if (max_frames_ > 0) {
@@ -590,8 +593,9 @@ Stage::append(const void* frames, uint64_t n_frames, int mem)
             // Double buffer: batch i+1's host copy and H2D (on h2d_) overlap
             // batch i's kernels.  A pageable source is first copied into the
             // pinned staging buffer (the one copy ZarrStream_append makes,
-            // frame.queue.cpp:37-39); a pinned source is DMA'd directly and
-            // append waits for that DMA so the caller may reuse its buffer.
+            // frame.queue.cpp:37-39) and may be reused once append returns.
+            // A pinned source is DMA'd directly and read asynchronously:
+            // frames_consumed() says when its bytes may be overwritten.
             const int j = stage_idx_;
             stage_idx_ ^= 1;
             const size_t nbytes = size_t(b) * fbytes;
@@ -1106,6 +1110,158 @@ Stage::copy_layer_async(uint32_t level, uint64_t layer, void* dst, size_t cap,
 }
 
 void
+Stage::band_geometry(uint32_t level, int32_t* supported, uint32_t* n_bands,
+                     uint64_t* frames_per_band, uint32_t* chunks_per_band) const
+{
+    if (level >= lv_.size())
+        throw Error(3, "level out of range");
+    const ArrayDimensions& ad = *lv_[level].ad;
+    const bool ok = ad.supports_dim1_banding();
+    if (supported)
+        *supported = ok ? 1 : 0;
+    if (n_bands)
+        *n_bands = ok ? ad.dim1_band_count() : 1;
+    if (frames_per_band)
+        *frames_per_band = ok ? ad.frames_per_dim1_band() : lv_[level].F;
+    if (chunks_per_band)
+        *chunks_per_band = ok ? ad.chunks_per_dim1_band() : lv_[level].n_chunks;
+}
+
+// Array::flush_completed_bands_ (array.cpp:873-908) hands band b of a layer
+// -- the chunk slots [b*cpb, (b+1)*cpb), dim 1 being the slowest chunk index
+// of a layer -- to compression once frames [b*fpb, (b+1)*fpb) of the layer
+// are written.  Same ordering rules as copy_layer_async.
+void
+Stage::copy_band_async(uint32_t level, uint64_t layer, uint32_t band, void* dst,
+                       size_t cap, uint8_t* has_data, size_t has_data_cap)
+{
+    if (level >= lv_.size())
+        throw Error(3, "level out of range");
+    StageLevel& L = lv_[level];
+    if (!L.ring.p)
+        throw Error(1, "level 0 split disabled for this stage");
+    int32_t ok = 0;
+    uint32_t nb = 1, cpb = L.n_chunks;
+    uint64_t fpb = L.F;
+    band_geometry(level, &ok, &nb, &fpb, &cpb);
+    if (band >= nb)
+        throw Error(3, "band out of range");
+    const uint32_t slot = uint32_t(layer % L.n_slots);
+    if (L.slot_layer[slot] != int64_t(layer))
+        throw Error(3, "chunk layer not resident");
+    if (!finalized_ && L.frames_written < layer * L.F + (uint64_t(band) + 1) * fpb)
+        throw Error(3, "band not complete");
+    if (dst && cap < L.bpc * cpb)
+        throw Error(2, "destination too small for a band");
+    if (has_data && has_data_cap < cpb)
+        throw Error(2, "has_data too small");
+    const uint32_t c0 = band * cpb;
+    hip_check(hipEventRecord(L.ready_ev[slot], stream_), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(d2h_, L.ready_ev[slot], 0), "hipStreamWaitEvent");
+    if (dst)
+        copy_chunks(dst, L.ring.p + slot * L.slot_bytes + uint64_t(c0) * L.pitch, L.bpc,
+                    L.pitch, cpb, hipMemcpyDefault, d2h_);
+    if (has_data) {
+        uint8_t* fb = L.flag_bytes.p + size_t(slot) * L.n_chunks + c0;
+        hip_check(launch_flags_to_bytes(reinterpret_cast<const uint32_t*>(L.flags.p) +
+                                          size_t(slot) * L.n_chunks + c0,
+                                        fb, cpb, uint32_t(layer / L.n_slots + 1), d2h_),
+                  "flags launch");
+        hip_check(hipMemcpyAsync(has_data, fb, cpb, hipMemcpyDefault, d2h_),
+                  "hipMemcpyAsync");
+    }
+    hip_check(hipEventRecord(L.copy_ev[slot], d2h_), "hipEventRecord");
+    L.copy_pending[slot] = 1;
+}
+
+void
+Stage::wait_stream(hipStream_t s)
+{
+    if (!ext_ev_)
+        hip_check(hipEventCreateWithFlags(&ext_ev_, hipEventDisableTiming),
+                  "hipEventCreate");
+    hip_check(hipEventRecord(ext_ev_, s), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(stream_, ext_ev_, 0), "hipStreamWaitEvent");
+}
+
+Footprint
+Stage::memory_usage() const
+{
+    Footprint f;
+    for (const StageLevel& L : lv_) {
+        f.device += L.ring.n + L.flags.n + L.tab_off.n + L.tab_grp.n + L.ref_table.n +
+                    L.scratch.n + L.partial[0].n + L.partial[1].n + L.d_ops.n +
+                    L.flag_bytes.n + L.shard_order.n;
+        f.pinned += L.h_ops.n;
+        for (const DevBuf& b : L.cframes)
+            f.device += b.n;
+        for (const DevBuf& b : L.coffsets)
+            f.device += b.n;
+        for (const PinnedBuf& b : L.h_coffsets)
+            f.pinned += b.n;
+        if (L.comp)
+            f.device += L.comp->device_bytes();
+    }
+    for (int j = 0; j < 2; ++j) {
+        f.device += d_stage_[j].n;
+        f.pinned += h_stage_[j].n;
+    }
+    f.device += xbuf_.n;
+    return f;
+}
+
+// The constructor's geometry without allocating: every buffer at the size
+// the stage may grow it to (staging for a host source, per-level scratch and
+// z partials for the generic cascade, the transposition buffer).
+Footprint
+Stage::estimate_memory(const ArrayDesc& desc, const StageOptions& opt_in)
+{
+    StageOptions opt = opt_in;
+    if (opt.layer_slots == 0)
+        opt.layer_slots = 2;
+    if (opt.max_batch_frames == 0)
+        opt.max_batch_frames = 64;
+    const size_t bpp = bytes_of_type(desc.dtype);
+    ArrayDimensions base(desc.dims, desc.dtype, desc.storage_order);
+    const auto levels = desc.multiscale
+                          ? make_pyramid_levels(base.dims(), desc.max_levels,
+                                                opt.force_levels)
+                          : std::vector<std::vector<Dim>>{ base.dims() };
+    const size_t n = base.ndims();
+    const uint64_t B = opt.max_batch_frames;
+    Footprint f;
+    for (size_t k = 0; k < levels.size(); ++k) {
+        ArrayDimensions ad(levels[k], desc.dtype);
+        const uint64_t W = levels[k][n - 1].array_size_px;
+        const uint64_t H = levels[k][n - 2].array_size_px;
+        const uint64_t bpc = ad.bytes_per_chunk();
+        const uint64_t nc = ad.number_of_chunks_in_memory();
+        const uint64_t F = std::max<uint64_t>(1, ad.frames_per_chunk_layer());
+        const uint64_t slots = std::max<uint64_t>(opt.layer_slots, (B - 1 + F - 1) / F + 1);
+        const uint64_t lfb = W * H * bpp;
+        if (!(k == 0 && opt.skip_level0_split)) {
+            f.device += chunk_pitch(bpc, uint32_t(nc)) * nc * slots; // ring
+            f.device += nc * slots * 4;                              // has_data words
+            f.device += slots * F * sizeof(FrameRef);                // frame table
+            f.device += nc * slots;                                  // has_data bytes
+        }
+        f.device += F * 12 + nc * 4; // tab_off + tab_grp, shard order
+        if (k > 0) {
+            f.device += B * lfb + 2 * lfb;                       // scratch, z partials
+            f.device += (B + 1) * sizeof(LevelOp);               // d_ops
+            f.pinned += (B + 1) * sizeof(LevelOp);               // h_ops
+        }
+    }
+    const uint64_t fb0 = uint64_t(levels[0][n - 1].array_size_px) *
+                         levels[0][n - 2].array_size_px * bpp;
+    f.device += 2 * B * fb0; // H2D staging (host sources)
+    f.pinned += 2 * B * fb0; // pageable -> pinned staging
+    if (base.needs_xy_transposition())
+        f.device += B * fb0;
+    return f;
+}
+
+void
 Stage::device_layer(uint32_t level, uint64_t layer, void** chunks,
                     uint32_t** flags)
 {
@@ -1399,6 +1555,7 @@ Stage::finalize()
                       "zero launch");
         }
     }
+    finalized_ = true;
     synchronize();
 }
 
@@ -1618,24 +1775,40 @@ GpuDownsampler::take_frame(uint32_t level, void* dst, size_t cap, int mem,
 const char*
 GpuDownsampler::method_name() const
 {
-    // downsampler.cpp:422-438
-    switch (method_) {
+    return downsampling_method_name(method_);
+}
+
+std::string
+GpuDownsampler::metadata_json() const
+{
+    return downsampling_metadata_json(method_);
+}
+
+// Downsampler::downsampling_method (downsampler.cpp:422-438)
+const char*
+downsampling_method_name(int32_t method)
+{
+    switch (method) {
         case 0:
             return "decimate";
         case 1:
             return "local_mean";
         case 2:
             return "local_min";
-        default:
+        case 3:
             return "local_max";
+        default:
+            throw Error(1, "Invalid downsampling method: " + std::to_string(method));
     }
 }
 
+// Downsampler::get_metadata (downsampler.cpp:440-485) as nlohmann's
+// json::dump() serialises it: compact, object keys sorted.  Byte-compared
+// with the compiled reference (tests/test_metadata_cpu.py).
 std::string
-GpuDownsampler::metadata_json() const
+downsampling_metadata_json(int32_t method)
 {
-    // downsampler.cpp:440-485, serialised with sorted keys as nlohmann does
-    switch (method_) {
+    switch (method) {
         case 1:
             return "{\"description\":\"The fields in the metadata describe how "
                    "to reproduce this multiscaling in scikit-image. The method "
@@ -1655,12 +1828,14 @@ GpuDownsampler::metadata_json() const
                    "along block dimensions.\",\"kwargs\":{\"func\":\"np.min\"},"
                    "\"method\":\"skimage.measure.block_reduce\",\"version\":"
                    "\"0.25.2\"}";
-        default:
+        case 3:
             return "{\"description\":\"Maximum pooling over 2x2 blocks. "
                    "Equivalent to reshaping into blocks and taking numpy.max "
                    "along block dimensions.\",\"kwargs\":{\"func\":\"np.max\"},"
                    "\"method\":\"skimage.measure.block_reduce\",\"version\":"
                    "\"0.25.2\"}";
+        default:
+            throw Error(1, "Invalid downsampling method: " + std::to_string(method));
     }
 }
 

@@ -99,6 +99,11 @@ class Compressor
              const uint32_t* flags, uint32_t tag, uint8_t* out, uint64_t* offsets,
              hipStream_t stream, const uint32_t* order = nullptr);
     const BloscGeom& geom() const { return g_; }
+    // device bytes of the scratch buffers allocated so far
+    uint64_t device_bytes() const
+    {
+        return scratch_.n + ssize_.n + spos_.n + fsize_.n + mode_.n + cstart_.n;
+    }
 
   private:
     BloscGeom g_;
@@ -123,7 +128,6 @@ struct StageOptions
     uint32_t max_batch_frames = 64;
     uint32_t force_levels = 0;
     bool skip_level0_split = false;
-    uint32_t blocks_per_cu = 0;
     uint64_t first_frame = 0;
 };
 
@@ -188,6 +192,12 @@ struct StageLevel
     uint32_t internal_stride = 0;
 };
 
+// What a stage holds (aqz_memory_usage).
+struct Footprint
+{
+    uint64_t device = 0, pinned = 0;
+};
+
 // One chunk of a compressed layer, in output (shard-major) order.
 struct ChunkEntry
 {
@@ -211,6 +221,8 @@ class Stage
     const std::vector<Dim>& level_dims(uint32_t level) const;
     LevelLayout layout(uint32_t level) const;
     void set_stream(hipStream_t s);
+    // the stage's stream waits for the work enqueued so far on s
+    void wait_stream(hipStream_t s);
     void set_tuning(uint32_t knobs, uint32_t nt) { knobs_ = knobs; nt_mode_ = nt & 7u; }
     void append(const void* frames, uint64_t n_frames, int mem);
     void synchronize();
@@ -224,6 +236,14 @@ class Stage
     void copy_layer_async(uint32_t level, uint64_t layer, void* dst, size_t cap,
                           uint8_t* has_data, size_t has_data_cap);
     void wait_copies();
+    // dim-1 banding: geometry and the hand-off of one complete band
+    void band_geometry(uint32_t level, int32_t* supported, uint32_t* n_bands,
+                       uint64_t* frames_per_band, uint32_t* chunks_per_band) const;
+    void copy_band_async(uint32_t level, uint64_t layer, uint32_t band, void* dst,
+                         size_t cap, uint8_t* has_data, size_t has_data_cap);
+    Footprint memory_usage() const;
+    // upper bound of what Stage(desc, opt) allocates (no compressed hand-off)
+    static Footprint estimate_memory(const ArrayDesc& desc, const StageOptions& opt);
     // device compression of a resident layer, on the hand-off stream
     void compress_layer(uint32_t level, uint64_t layer, const Compression& c);
     // waits for that compression; offsets[0..n_chunks] (frame starts + total)
@@ -316,7 +336,14 @@ class Stage
     double timed_ms_ = 0;
     uint64_t timed_launches_ = 0;
     hipEvent_t mark_ev_[2] = { nullptr, nullptr };
+    hipEvent_t ext_ev_ = nullptr;  // wait_stream
+    bool finalized_ = false;
 };
+
+// Downsampler::downsampling_method / get_metadata().dump() (downsampler.cpp:
+// 422-485) for a method value; throw Error(1) on an invalid method.
+const char* downsampling_method_name(int32_t method);
+std::string downsampling_metadata_json(int32_t method);
 
 class GpuDownsampler
 {

@@ -92,6 +92,27 @@ class ArrayDimensions
     uint32_t chunks_per_shard() const;
     uint32_t number_of_shards() const;
     uint32_t chunk_layers_per_shard() const { return dims_[0].shard_size_chunks; }
+    // dim-1 banding (array.dimensions.cpp:344-373): append chunk 1 plus an
+    // intermediate dim, no transposition; a band is one chunk row of dim 1
+    bool supports_dim1_banding() const
+    {
+        return dims_[0].chunk_size_px == 1 && ndims() >= 4 && !transposed_;
+    }
+    uint32_t dim1_band_count() const
+    {
+        return parts_along(dims_[1].array_size_px, dims_[1].chunk_size_px);
+    }
+    uint64_t frames_per_dim1_band() const
+    {
+        uint64_t f = dims_[1].chunk_size_px;
+        for (size_t i = 2; i + 2 < ndims(); ++i)
+            f *= dims_[i].array_size_px;
+        return f;
+    }
+    uint32_t chunks_per_dim1_band() const
+    {
+        return chunks_in_memory_ / dim1_band_count();
+    }
 
   private:
     bool is_2d_;

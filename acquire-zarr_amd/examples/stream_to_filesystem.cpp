@@ -24,6 +24,7 @@
 // appended cyclically.  Prints
 // one JSON line with the end-to-end rate.
 #include "aqz_gpu.h"
+#include "aqz_gpu_bench.h"
 
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -293,12 +294,20 @@ main(int argc, char** argv)
     }
     const bool compress = codec == "lz4";
     aqz_array_desc desc{ dims.data(), dims.size(), dtype, 1, AQZ_METHOD_MEAN, 0, nullptr, 0 };
+    // this writer emits sharded Zarr v3 arrays only (every dimension has a
+    // shard size); an unsharded array stores each chunk as its own file with
+    // no index table, which is not implemented here
+    for (const aqz_dimension& d : dims)
+        if (d.shard_size_chunks == 0)
+            die("unsharded arrays are not supported by this example");
     aqz_stage_options opt{};
     opt.layer_slots = 3;
     opt.max_batch_frames = batch;
-    opt.force_levels = force_levels;
+    // c2: BASELINE's 5 levels at 256-px chunks (the bench-only extension)
+    aqz_stage_bench_options bopt{};
+    bopt.force_levels = force_levels;
     aqz_stage* st = nullptr;
-    check(aqz_stage_create(&desc, &opt, &st), "aqz_stage_create");
+    check(aqz_stage_create_bench(&desc, &opt, &bopt, &st), "aqz_stage_create");
 
     const uint32_t nl = aqz_stage_n_levels(st);
     std::vector<Level> lv(nl);
@@ -534,6 +543,16 @@ main(int argc, char** argv)
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t f = 0; f < n_frames;) {
         const uint64_t n = std::min<uint64_t>({ uint64_t(batch), n_frames - f, ring - f % ring });
+        // Back-pressure of a camera DMA ring: frames f..f+n-1 go into ring
+        // slots last used by frames f-ring..f+n-1-ring, which a pinned source
+        // hands to the stage asynchronously.  The camera may write those
+        // slots only once the stage has read them (aqz_stage_frames_consumed);
+        // here the slots keep their synthetic contents, but the wait is the
+        // one a real producer needs.  (A pageable source is copied before
+        // aqz_stage_append returns.)
+        if (mem == AQZ_MEM_HOST_PINNED && f + n > ring)
+            while (aqz_stage_frames_consumed(st) < f + n - ring)
+                std::this_thread::yield();
         check(aqz_stage_append(st, src + (f % ring) * fbytes, n, mem), "append");
         f += n;
         advance(false);

@@ -378,6 +378,22 @@ def run_paced(torch, aqz, dev, cfg, args):
     }
 
 
+def self_launch(n):
+    """`bench.py --gpus N` without a launcher: run this same command under
+    torch.distributed.run with N ranks on 127.0.0.1 (one process per GPU)
+    as a child process; rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -408,10 +424,29 @@ def main():
                     help="end-to-end mode: frames start in host memory (pinned or "
                          "pageable), every completed chunk layer is handed back to "
                          "pinned host buffers (DESIGN.md 'End to end')")
+    ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
-    import torch
+    if args.gpus < 1:
+        sys.exit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # No launcher: start one rank per GPU ourselves, before this process
+        # has touched the GPU, and exit with the launcher's status.
+        sys.exit(self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU required")
+    if args.launch_probe:
+        # CPU test hook: report the rank layout and stop before any GPU work
+        # one write() per line: ranks share the pipe
+        sys.stdout.write(json.dumps({"rank": int(os.environ.get("RANK", "0")),
+                                     "world": world,
+                                     "local_rank": int(os.environ.get("LOCAL_RANK", "0"))})
+                         + "\n")
+        sys.stdout.flush()
+        return
+
+    import torch
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None

@@ -135,6 +135,11 @@ uint64_t aqz_dims_frames_per_chunk_layer(const aqz_dims* d);
 /* array.dimensions.cpp:393-548 */
 uint32_t aqz_dims_shard_index_for_chunk(const aqz_dims* d, uint32_t chunk);
 uint32_t aqz_dims_shard_internal_index(const aqz_dims* d, uint32_t chunk);
+/* supports_dim1_banding, dim1_band_count, frames_per_dim1_band,
+ * chunks_per_dim1_band (array.dimensions.cpp:344-373) */
+aqz_status aqz_dims_dim1_banding(const aqz_dims* d, int32_t* supported,
+                                 uint32_t* n_bands, uint64_t* frames_per_band,
+                                 uint32_t* chunks_per_band);
 
 /* Level geometry of the pyramid: Downsampler::make_writer_configurations_
  * (src/streaming/downsampler.cpp:494-597).  dims in storage order; writes the
@@ -174,9 +179,17 @@ aqz_status aqz_downsampler_take_frame(aqz_downsampler* ds, uint32_t level,
 /* Downsampler::downsampling_method (downsampler.cpp:422-438):
  * "decimate" | "local_mean" | "local_min" | "local_max" */
 const char* aqz_downsampler_method_name(const aqz_downsampler* ds);
-/* Downsampler::get_metadata (downsampler.cpp:440-485) as JSON text. */
+/* Downsampler::get_metadata (downsampler.cpp:440-485) as JSON text:
+ * byte-identical to the reference's get_metadata().dump(), the block
+ * MultiscaleArray embeds in zarr.json (multiscale.array.cpp:271).  With
+ * buf == NULL only *len is set; cap must hold *len + 1 bytes. */
 aqz_status aqz_downsampler_metadata_json(const aqz_downsampler* ds, char* buf,
                                          size_t cap, size_t* len);
+/* The same two, from the method value alone (pure host, no GPU):
+ * "" / AQZ_STATUS_INVALID_ARGUMENT for a method outside AQZ_METHOD_*. */
+const char* aqz_downsampling_method_name(int32_t method);
+aqz_status aqz_downsampling_metadata_json(int32_t method, char* buf, size_t cap,
+                                          size_t* len);
 
 /* ======================================================================
  * Stage -- the device-resident hot path of MultiscaleArray::write_frame
@@ -198,14 +211,6 @@ typedef struct
 {
     uint32_t layer_slots;      /* resident chunk layers per level (>=1; 0 = 2) */
     uint32_t max_batch_frames; /* frames per internal launch (0 = 64) */
-    uint32_t force_levels;     /* 0 = reference level rule.  >0: extension
-                                  used only by bench.py for the BASELINE
-                                  "5-level @ 256-px chunks" config: keep
-                                  halving XY until this many levels exist. */
-    int32_t skip_level0_split; /* 1 = do not tile-split level 0 (pyramid
-                                  only); default 0 = full stage */
-    uint32_t blocks_per_cu;    /* reserved, ignored: the fused kernels run
-                                  one region per workgroup */
     uint64_t first_frame;      /* level-0 frame id of this stage's first
                                   frame (z-slab sharding across GPUs: the
                                   slab's first plane); level k starts at
@@ -238,8 +243,10 @@ aqz_status aqz_stage_level_layout(const aqz_stage* st, uint32_t level,
 /* Run the stage on the HIP stream `stream` (a hipStream_t; NULL = the
  * stage's own stream).  All later work is enqueued there. */
 aqz_status aqz_stage_set_stream(aqz_stage* st, void* stream);
-/* Kernel A/B switches for tuning runs (0, 0 = the shipped kernels). */
-aqz_status aqz_stage_set_tuning(aqz_stage* st, uint32_t knobs, uint32_t nt);
+/* Make the stage's stream wait for all work enqueued so far on `stream`
+ * (a hipStream_t): append device frames produced there without a host
+ * synchronisation (e.g. a torch stream that filled them). */
+aqz_status aqz_stage_wait_stream(aqz_stage* st, void* stream);
 /* Append n_frames full level-0 frames (contiguous, frame after frame).
  * Equivalent to n_frames calls of MultiscaleArray::write_frame.
  *  - AQZ_MEM_HOST: copied into a pinned staging buffer by a few host threads
@@ -277,6 +284,48 @@ aqz_status aqz_stage_copy_layer_async(aqz_stage* st, uint32_t level,
                                       uint64_t layer, void* dst, size_t cap,
                                       uint8_t* has_data, size_t has_data_cap);
 aqz_status aqz_stage_wait_copies(aqz_stage* st);
+
+/* ---- dim-1 banding ---------------------------------------------------------
+ * Array::flush_completed_bands_ (array.cpp:873-908) flushes the chunks of a
+ * band of dimension 1 as soon as its frames are written, before the whole
+ * chunk layer is: ArrayDimensions::supports_dim1_banding, dim1_band_count,
+ * frames_per_dim1_band, chunks_per_dim1_band (array.dimensions.cpp:344-373).
+ * Band b of a layer is the contiguous chunk range
+ * [b * chunks_per_band, (b + 1) * chunks_per_band). */
+aqz_status aqz_stage_band_geometry(const aqz_stage* st, uint32_t level,
+                                   int32_t* supported, uint32_t* n_bands,
+                                   uint64_t* frames_per_band,
+                                   uint32_t* chunks_per_band);
+/* Asynchronous hand-off of one complete band of a resident layer, like
+ * aqz_stage_copy_layer_async for its chunk range: dst receives
+ * chunks_per_band * bytes_per_chunk bytes, has_data (NULL to skip)
+ * chunks_per_band flags.  The band must be complete: all its frames
+ * written (frames_written(level) >= layer * frames_per_layer +
+ * (band + 1) * frames_per_band), or the layer finalized. */
+aqz_status aqz_stage_copy_band_async(aqz_stage* st, uint32_t level,
+                                     uint64_t layer, uint32_t band, void* dst,
+                                     size_t cap, uint8_t* has_data,
+                                     size_t has_data_cap);
+
+/* ---- memory accounting ------------------------------------------------------
+ * What the stage holds, for ZarrStream_get_current_memory_usage
+ * (zarr.stream.cpp:1057-1068) and ZarrStreamSettings_estimate_max_memory_usage
+ * (acquire.zarr.cpp:216-314) to include. */
+typedef struct
+{
+    uint64_t device_bytes; /* HBM: chunk-layer rings, has_data words, frame
+                              tables, scratch, H2D staging, compressed frames */
+    uint64_t pinned_bytes; /* page-locked host memory: host-source staging,
+                              compressed-offset read-back */
+} aqz_memory_usage;
+/* Bytes currently allocated by the stage. */
+aqz_status aqz_stage_memory_usage(const aqz_stage* st, aqz_memory_usage* out);
+/* Upper bound of what a stage created with (desc, opt) allocates, compressed
+ * hand-off excluded (add aqz_compressor_max_bytes per compressed slot).  No
+ * GPU needed. */
+aqz_status aqz_stage_estimate_memory(const aqz_array_desc* desc,
+                                     const aqz_stage_options* opt,
+                                     aqz_memory_usage* out);
 /* Page-locked host memory for frames and hand-off buffers. */
 aqz_status aqz_host_alloc(size_t bytes, void** out);
 void aqz_host_free(void* p);
@@ -378,23 +427,6 @@ uint32_t aqz_compressor_blocksize(const aqz_compressor* c);
  * it can be flushed (the reference's lazily zeroed chunks, chunk.cpp:8-15).
  * The unpaired trailing z plane is dropped, as in the reference. */
 aqz_status aqz_stage_finalize(aqz_stage* st);
-
-/* ---- instrumentation (bench) ---------------------------------------- */
-/* Time every launch of the dominant (fused pyramid) kernel with HIP events
- * recorded on the stream it is launched on. */
-aqz_status aqz_stage_enable_kernel_timing(aqz_stage* st, int32_t enable);
-/* Sum of those kernels' durations (ms) and their count since enabling;
- * synchronizes. */
-aqz_status aqz_stage_kernel_timing(aqz_stage* st, double* total_ms,
-                                   uint64_t* launches);
-/* One timing event pair on the stage's stream (the stream its kernels run
- * on): which = 0 records the begin mark, 1 the end mark, after all work
- * enqueued so far.  aqz_stage_timing_elapsed waits for the end mark and
- * returns the milliseconds between the two. */
-aqz_status aqz_stage_timing_mark(aqz_stage* st, int32_t which);
-aqz_status aqz_stage_timing_elapsed(aqz_stage* st, double* ms);
-/* Name of the dominant kernel symbol (for matching rocprof output). */
-const char* aqz_stage_dominant_kernel(const aqz_stage* st);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,59 @@
+/*
+ * aqz_gpu_bench.h -- measurement and tuning entry points of libaqz_gpu.so.
+ *
+ * NOT part of the drop-in ABI (include/aqz_gpu.h): nothing the reference's
+ * streaming layer calls.  bench.py, the tuning tools under tools/ and the
+ * tests use these to reproduce the BASELINE configurations and to time the
+ * dominant kernel on the stream it runs on.
+ */
+#ifndef AQZ_GPU_BENCH_H
+#define AQZ_GPU_BENCH_H
+
+#include "aqz_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct
+{
+    uint32_t force_levels;     /* 0 = the reference level rule
+                                  (downsampler.cpp:512-541).  >0: keep halving
+                                  XY until this many levels exist -- BASELINE
+                                  configs[1] asks for 5 levels at 256-px
+                                  chunks, where the rule stops at 4; pixels
+                                  are unchanged (each level is the 2x2 of the
+                                  one above). */
+    int32_t skip_level0_split; /* 1 = do not tile-split level 0 (the
+                                  pyramid-only side measurement) */
+} aqz_stage_bench_options;
+
+/* aqz_stage_create with the bench extensions (bench may be NULL). */
+aqz_status aqz_stage_create_bench(const aqz_array_desc* desc,
+                                  const aqz_stage_options* opt,
+                                  const aqz_stage_bench_options* bench,
+                                  aqz_stage** out);
+
+/* Kernel A/B switches for tuning runs (0, 0 = the shipped kernels). */
+aqz_status aqz_stage_set_tuning(aqz_stage* st, uint32_t knobs, uint32_t nt);
+
+/* Time every launch of the dominant (fused pyramid) kernel with HIP events
+ * recorded on the stream it is launched on. */
+aqz_status aqz_stage_enable_kernel_timing(aqz_stage* st, int32_t enable);
+/* Sum of those kernels' durations (ms) and their count since enabling;
+ * synchronizes. */
+aqz_status aqz_stage_kernel_timing(aqz_stage* st, double* total_ms,
+                                   uint64_t* launches);
+/* One timing event pair on the stage's stream (the stream its kernels run
+ * on): which = 0 records the begin mark, 1 the end mark, after all work
+ * enqueued so far.  aqz_stage_timing_elapsed waits for the end mark and
+ * returns the milliseconds between the two. */
+aqz_status aqz_stage_timing_mark(aqz_stage* st, int32_t which);
+aqz_status aqz_stage_timing_elapsed(aqz_stage* st, double* ms);
+/* Name of the dominant kernel symbol (for matching rocprof output). */
+const char* aqz_stage_dominant_kernel(const aqz_stage* st);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AQZ_GPU_BENCH_H */

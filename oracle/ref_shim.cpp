@@ -128,6 +128,34 @@ ref_ds_take_frame(void* h, int level, void* dst, size_t cap, size_t* nbytes)
     return 1;
 }
 
+// Downsampler::get_metadata().dump() (downsampler.cpp:440-485) and
+// downsampling_method() (:422-438): the OME "metadata" block and "type"
+// MultiscaleArray writes into zarr.json (multiscale.array.cpp:271).
+// Returns the length; writes at most cap bytes (NUL-terminated if room).
+size_t
+ref_ds_metadata(void* h, char* buf, size_t cap)
+{
+    const std::string s = static_cast<RefDs*>(h)->ds->get_metadata().dump();
+    if (buf && cap) {
+        const size_t n = s.size() < cap - 1 ? s.size() : cap - 1;
+        std::memcpy(buf, s.data(), n);
+        buf[n] = 0;
+    }
+    return s.size();
+}
+
+size_t
+ref_ds_method_name(void* h, char* buf, size_t cap)
+{
+    const std::string s = static_cast<RefDs*>(h)->ds->downsampling_method();
+    if (buf && cap) {
+        const size_t n = s.size() < cap - 1 ? s.size() : cap - 1;
+        std::memcpy(buf, s.data(), n);
+        buf[n] = 0;
+    }
+    return s.size();
+}
+
 // ---- ArrayDimensions ----------------------------------------------------
 void*
 ref_dims_create(const or_dim* dims, int ndims, int dtype)
@@ -211,6 +239,18 @@ uint32_t
 ref_dims_shard_internal_index(void* h, uint32_t c)
 {
     return static_cast<ArrayDimensions*>(h)->shard_internal_index(c);
+}
+
+// dim-1 banding geometry (array.dimensions.cpp:344-373)
+void
+ref_dims_dim1_banding(void* h, int* supported, uint32_t* n_bands,
+                      uint64_t* frames_per_band, uint32_t* chunks_per_band)
+{
+    auto* d = static_cast<ArrayDimensions*>(h);
+    *supported = d->supports_dim1_banding() ? 1 : 0;
+    *n_bands = d->dim1_band_count();
+    *frames_per_band = d->frames_per_dim1_band();
+    *chunks_per_band = d->chunks_per_dim1_band();
 }
 
 // Tile split of one frame into a chunk layer using the reference's own

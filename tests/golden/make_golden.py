@@ -10,6 +10,10 @@ Outputs (data only -- inputs and expected outputs):
   tile_split.npz      ragged tile-split layers + has_data flags
   digests.json        sha256 of every level frame for BASELINE-sized configs
                       (inputs regenerated from splitmix64 seeds)
+  metadata.json       Downsampler::downsampling_method() and
+                      get_metadata().dump() per method (downsampler.cpp:
+                      422-485): the OME block MultiscaleArray embeds in
+                      zarr.json (`make_golden.py metadata` writes only this)
 """
 import hashlib
 import json
@@ -79,9 +83,33 @@ def digest_seed(key):
     return int(hashlib.sha256(key.encode()).hexdigest()[:12], 16)
 
 
+def write_metadata():
+    import ctypes as C
+    R = ob.ref()
+    R.ref_ds_metadata.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+    R.ref_ds_metadata.restype = C.c_size_t
+    R.ref_ds_method_name.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+    R.ref_ds_method_name.restype = C.c_size_t
+    out = {}
+    dims = [(ob.TIME, 0, 5, 1), (ob.SPACE, 10, 5, 1), (ob.SPACE, 10, 5, 1)]
+    for m in range(4):
+        ds = ob.OracleDownsampler(dims, ob.U16, m, 0, use_ref=True)
+        buf = C.create_string_buffer(4096)
+        n = R.ref_ds_metadata(ds.h, buf, 4096)
+        assert n < 4096
+        name = C.create_string_buffer(64)
+        R.ref_ds_method_name(ds.h, name, 64)
+        out[str(m)] = {"method_name": name.value.decode(), "metadata": buf.value.decode()}
+    with open(os.path.join(HERE, "metadata.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def main():
     if not ob.ref_available():
         sys.exit("oracle/_ref/libaqzref.so missing: run `make -C oracle ref` first")
+    write_metadata()
+    if sys.argv[1:] == ["metadata"]:
+        return
     arrays = {}
     for key, dims, dt, m, frames in cascade_cases():
         ds = ob.OracleDownsampler(dims, dt, m, 0, use_ref=True)

@@ -1,0 +1,184 @@
+"""GPU parity of exactly what bench.py times.
+
+* C2 as benched: u16 2048x2048, 256-px chunks, t-chunk 64, force_levels=5
+  (the BASELINE "5-level @ 256-px chunks" geometry; the reference rule
+  stops at 4 levels, downsampler.cpp:512-541), 128-frame launches from a
+  device-resident ring, the bench's layer_slots=2 ring.  Pixels of every
+  level come from the oracle run at 128-px chunks (5 levels by the
+  reference rule, the same pixels -- level values do not depend on the
+  chunk size) tiled at the forced 256-px level dims.
+* c2-ref4: the same frames under the reference level rule (4 levels).
+* C4 as stated in BASELINE configs[3]: u16 2048x2048x256 planes, z-chunk 64,
+  128-plane launches (fused 2x2x2 kernel); then the same volume split into
+  4 z slabs (what --gpus 4 runs: aqz.dist.z_slab(256, 4, r, 4)), one stage
+  per slab with first_frame = the slab's first plane; the slabs' chunk
+  layers assemble, with no exchange, into the single-volume result.
+
+Reference: downsampler.cpp:306-414, 494-597; array.cpp:507-622.
+"""
+import numpy as np
+import pytest
+
+import bench
+from helpers import assert_same_pixels, expected_stage_layers
+from oracle_bindings import MEAN, SPACE, U16, synthetic_frames
+
+pytestmark = pytest.mark.gpu
+
+
+def distinct_frames(n, h, w, seed, base=8):
+    """n distinct u16 frames: `base` splitmix frames, frame i XOR-ed with a
+    per-frame constant (cheap at GiB scale, and no two frames equal)."""
+    b = synthetic_frames(U16, min(n, base), h, w, seed)
+    out = np.empty((n, h, w), np.uint16)
+    for i in range(n):
+        np.bitwise_xor(b[i % len(b)], np.uint16((i * 40503 + 1) & 0xFFFF), out=out[i])
+    return out
+
+
+def _device_ring(frames):
+    import torch
+    t = torch.from_numpy(frames.view(np.int16)).cuda()
+    torch.cuda.synchronize()
+    return t
+
+
+def _check_layer(st, l, layer, exp):
+    buf, flags = exp.pop((l, layer))
+    got, gflags = st.copy_layer(l, layer)
+    assert_same_pixels(got, buf, U16, f"L{l} layer{layer}")
+    assert np.array_equal(gflags, flags), f"has_data L{l} layer{layer}"
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c2-ref4"])
+def test_bench_c2_configuration_exact(gpu, cfg):
+    c = bench.CONFIGS[cfg]
+    dims, B = c["dims"], c["batch"]
+    h, w = dims[-2][1], dims[-1][1]
+    st = gpu.Stage(dims, U16, MEAN, force_levels=c["force_levels"],
+                   max_batch_frames=B, layer_slots=2)
+    L = st.n_levels()
+    assert L == (5 if cfg == "c2" else 4)
+    ldims = [st.level_dims(l) for l in range(L)]
+    assert [d[-1][1] for d in ldims] == [2048, 1024, 512, 256, 128][:L]
+    assert all(d[-1][2] == 256 and d[-2][2] == 256 for d in ldims)
+    if cfg == "c2":
+        assert st.dominant_kernel() == "fused_pyramid_strip"
+    # oracle pixels: the reference rule at 128-px chunks gives the same
+    # 5 levels (c2); c2-ref4 is the reference configuration itself
+    odims = list(dims)
+    if c["force_levels"]:
+        odims[-1] = (SPACE, w, 128, 1)
+        odims[-2] = (SPACE, h, 128, 1)
+    n = 2 * max(B, 128)
+    frames = distinct_frames(n, h, w, 7 + L)
+    exp, fw, _ = expected_stage_layers(odims, U16, MEAN, frames, level_dims=ldims)
+    assert len(fw) == L
+    ring = _device_ring(frames)
+    F = [st.layout(l)["frames_per_layer"] for l in range(L)]
+    done = [0] * L
+    for s in range(n // B):
+        st.append_ptr(ring.data_ptr() + s * B * h * w * 2, B)
+        st.synchronize()
+        # check every layer completed by this launch before the 3-slot
+        # ring reuses its slot
+        for l in range(L):
+            while (done[l] + 1) * F[l] <= st.frames_written(l):
+                _check_layer(st, l, done[l], exp)
+                done[l] += 1
+    for l in range(L):
+        assert st.frames_written(l) == fw[l]
+    assert not exp, f"unchecked layers: {sorted(exp)}"
+    st.close()
+
+
+@pytest.fixture(scope="module")
+def c4_volume():
+    c = bench.CONFIGS["c4"]
+    dims = c["dims"]
+    Z, h, w = dims[1][1], dims[-2][1], dims[-1][1]
+    assert (Z, h, w) == (256, 2048, 2048) and dims[1][2] == 64
+    frames = distinct_frames(Z, h, w, 404)
+    exp, fw, ldims = expected_stage_layers(dims, U16, MEAN, frames)
+    return c, frames, exp, fw, ldims
+
+
+def test_c4_volume_exact(gpu, c4_volume):
+    c, frames, exp, fw, ldims = c4_volume
+    dims, B = c["dims"], c["batch"]
+    st = gpu.Stage(dims, U16, MEAN, max_batch_frames=B, layer_slots=2)
+    assert st.dominant_kernel() == "fused_pyramid_3d"
+    assert st.n_levels() == 4 == len(ldims)
+    assert [st.level_dims(l)[1][1] for l in range(4)] == [256, 128, 64, 64]
+    ring = _device_ring(frames)
+    fbytes = frames[0].nbytes
+    for s in range(len(frames) // B):
+        st.append_ptr(ring.data_ptr() + s * B * fbytes, B)
+    st.finalize()
+    for l in range(4):
+        assert st.frames_written(l) == fw[l], (l, st.frames_written(l), fw[l])
+    for (l, layer), (buf, flags) in sorted(exp.items()):
+        got, gflags = st.copy_layer(l, layer)
+        assert_same_pixels(got, buf, U16, f"L{l} layer{layer}")
+        assert np.array_equal(gflags, flags), (l, layer)
+    st.close()
+
+
+def test_c4_z_slabs_over_4_stages(gpu, c4_volume):
+    """The --gpus 4 decomposition on one device: 4 stages own the z slabs
+    [64r, 64r+64); OR-ing their chunk layers gives exactly the single-stage
+    layers (each slab writes only its own chunk regions; the rest stays 0)."""
+    import aqz
+    from aqz.dist import z_levels, z_slab
+    c, frames, exp, fw, ldims = c4_volume
+    dims = c["dims"]
+    planes = [lv[1][1] for lv in aqz.pyramid_levels(dims)]
+    align = 1 << z_levels(planes)
+    assert align == 4
+    ring = _device_ring(frames)
+    fbytes = frames[0].nbytes
+    stages = []
+    for r in range(4):
+        lo, hi = z_slab(planes[0], 4, r, align)
+        assert (lo, hi) == (64 * r, 64 * r + 64)
+        st = gpu.Stage(dims, U16, MEAN, max_batch_frames=c["batch"], layer_slots=2,
+                       first_frame=lo)
+        st.append_ptr(ring.data_ptr() + lo * fbytes, hi - lo)
+        stages.append(st)
+    for st in stages:
+        st.finalize()
+    for l in range(4):
+        assert stages[-1].frames_written(l) == fw[l]
+    for (l, layer), (buf, flags) in sorted(exp.items()):
+        acc, facc = None, None
+        for st in stages:
+            got, gflags = st.copy_layer(l, layer)
+            acc = got if acc is None else np.bitwise_or(acc, got, out=acc)
+            facc = gflags if facc is None else np.maximum(facc, gflags)
+        assert_same_pixels(acc, buf, U16, f"slabs L{l} layer{layer}")
+        assert np.array_equal(facc, flags), (l, layer)
+    for st in stages:
+        st.close()
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_self_launched(gpu):
+    """`bench.py --gpus 2` with no launcher starts 2 ranks itself (both on
+    this box's one GPU, gloo for the barrier / max) and reports n_gpus 2."""
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, AQZ_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2",
+                        "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+                        "--no-pyramid-only-line"],
+                       capture_output=True, text=True, timeout=110, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["value"] > 0

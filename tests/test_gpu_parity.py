@@ -136,13 +136,18 @@ def test_downsampler_reference_known_answers(gpu):
 
 
 def test_downsampler_metadata_and_errors(gpu):
+    """method name and get_metadata().dump() byte-identical to the
+    reference's (tests/golden/metadata.json, from the compiled reference)."""
+    import json
+    import os
     import aqz
+    golden = json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                         "metadata.json")))
     dims = [(TIME, 0, 5, 1), (SPACE, 10, 5, 1), (SPACE, 10, 5, 1)]
-    names = {DECIMATE: "decimate", MEAN: "local_mean", MIN: "local_min", MAX: "local_max"}
-    for m, n in names.items():
+    for m in ALL_METHODS:
         ds = gpu.Downsampler(dims, U16, m)
-        assert ds.method_name() == n
-        assert "skimage" in ds.metadata_json() or "np.ndarray" in ds.metadata_json()
+        assert ds.method_name() == golden[str(m)]["method_name"]
+        assert ds.metadata_json() == golden[str(m)]["metadata"]
     with pytest.raises(aqz.AqzError) as e:
         gpu.Downsampler(dims, U16, 4)
     assert e.value.status == 1

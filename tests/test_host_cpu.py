@@ -12,13 +12,15 @@ import aqz
 import oracle_bindings as ob
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(REPO, "include", "aqz_gpu.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in ("aqz_gpu.h", "aqz_gpu_bench.h")]
 
 
 def declared_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(aqz_[a-z0-9_]+)\s*\(", text)))
+    names = set()
+    for h in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(aqz_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():
@@ -132,3 +134,48 @@ def test_host_transposition_matches_reference():
             assert a.transpose_frame_id(fid) == r.transpose_frame_id(fid)
             assert a.tile_group_offset(a.transpose_frame_id(fid)) == \
                 r.tile_group_offset(r.transpose_frame_id(fid))
+
+
+@pytest.mark.skipif(not ob.ref_available(), reason="oracle/_ref not built")
+def test_dim1_banding_geometry_matches_reference():
+    """supports_dim1_banding / dim1_band_count / frames_per_dim1_band /
+    chunks_per_dim1_band (array.dimensions.cpp:344-373)."""
+    import ctypes as C
+    R = ob.ref()
+    R.ref_dims_dim1_banding.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_uint32),
+                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+    rng = np.random.default_rng(14)
+    seen = set()
+    for _ in range(150):
+        dims = _random_dims(rng)
+        if rng.integers(0, 2):
+            dims[0] = (dims[0][0], dims[0][1], 1, dims[0][3])  # append chunk 1
+        a = aqz.Dims(dims, ob.U16)
+        r = ob.OracleDims(dims, ob.U16, use_ref=True)
+        s, n, f, c = C.c_int(), C.c_uint32(), C.c_uint64(), C.c_uint32()
+        R.ref_dims_dim1_banding(r.h, C.byref(s), C.byref(n), C.byref(f), C.byref(c))
+        got = a.dim1_banding()
+        assert got == (bool(s.value), n.value, f.value, c.value), dims
+        seen.add(got[0])
+    assert seen == {True, False}
+    # C4 (BASELINE configs[3]): 4 z bands of 64 planes, 64 chunks each
+    c4 = [(ob.TIME, 0, 1, 1), (ob.SPACE, 256, 64, 1), (ob.SPACE, 2048, 256, 1),
+          (ob.SPACE, 2048, 256, 1)]
+    assert aqz.Dims(c4, ob.U16).dim1_banding() == (True, 4, 64, 64)
+
+
+def test_memory_estimate_counts_the_rings():
+    """aqz_stage_estimate_memory (no GPU): the chunk-layer rings dominate;
+    for C2 as benched's level-0 geometry, 3 slots x 64 chunks x 8 MiB."""
+    c2 = [(ob.TIME, 0, 64, 1), (ob.SPACE, 2048, 256, 1), (ob.SPACE, 2048, 256, 1)]
+    m = aqz.estimate_memory(c2, ob.U16, ob.MEAN, max_batch_frames=128, layer_slots=2)
+    ring0 = 3 * 64 * 256 * 256 * 64 * 2
+    lv = aqz.pyramid_levels(c2)
+    rings = sum(3 * (-(-d[-1][1] // 256)) * (-(-d[-2][1] // 256)) * 256 * 256 * 64 * 2
+                for d in lv)
+    assert rings >= ring0
+    staging = 2 * 128 * 2048 * 2048 * 2
+    assert rings + staging <= m["device_bytes"] <= rings + staging + (1 << 30)
+    assert m["pinned_bytes"] >= staging
+    big = aqz.estimate_memory(c2, ob.U16, ob.MEAN, max_batch_frames=128, layer_slots=4)
+    assert big["device_bytes"] > m["device_bytes"]

@@ -57,7 +57,6 @@ def main():
     bytes_moved_extra = {}
 
     def mk(name, **kw):
-        kw.setdefault("blocks_per_cu", args.bpc)
         print(f"stage {name}", file=sys.stderr)
         st = aqz.Stage(dims, 1, 1, max_batch_frames=B, layer_slots=2, **kw)
         st.set_stream(stream.cuda_stream)
@@ -87,10 +86,6 @@ def main():
             mk(f"full5_pad{pad}_{j}", force_levels=5)
             bytes_moved_extra[f"full5_pad{pad}_{j}"] = B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64 + 1 / 256))
             os.environ.pop("AQZ_CHUNK_PAD")
-    for b in args.bpcs.split(","):
-        if b:
-            mk(f"full5_bpc{b}", force_levels=5, blocks_per_cu=int(b))
-            bytes_moved_extra[f"full5_bpc{b}"] = B * fbytes * (2 + (1 / 4 + 1 / 16 + 1 / 64 + 1 / 256))
     mk("split_only", multiscale=False)
     for nl in ((2, 3, 4) if args.depth else ()):
         mk(f"pyr{nl}_only", force_levels=nl, skip_level0_split=True)
