@@ -197,6 +197,8 @@ def lib():
         "aqz_stage_timing_mark": ([vp, i32], i32),
         "aqz_stage_timing_elapsed": ([vp, C.POINTER(C.c_double)], i32),
         "aqz_stage_dominant_kernel": ([vp], C.c_char_p),
+        "aqz_stage_placement": ([vp, C.POINTER(C.c_double), sz, C.POINTER(sz),
+                                 C.POINTER(u32)], i32),
         "aqz_stage_compress_layer": ([vp, u32, u64, C.POINTER(CompressionC)], i32),
         "aqz_stage_compressed_offsets": ([vp, u32, u64, C.POINTER(u64), sz], i32),
         "aqz_stage_copy_compressed_async": ([vp, u32, u64, vp, sz], i32),
@@ -620,6 +622,16 @@ class Stage:
 
     def dominant_kernel(self):
         return lib().aqz_stage_dominant_kernel(self.h).decode()
+
+    def placement(self):
+        """Creation-time placement calibration: {"candidates_ms": [...],
+        "kept": i} (empty list when none ran)."""
+        arr = (C.c_double * 16)()
+        n, kept = C.c_size_t(0), C.c_uint32(0)
+        _check(lib().aqz_stage_placement(self.h, arr, 16, C.byref(n), C.byref(kept)),
+               "placement")
+        return {"candidates_ms": [round(arr[i], 5) for i in range(min(16, n.value))],
+                "kept": kept.value}
 
     # ---- device compression of resident layers ----------------------------
     def compress_layer(self, level, layer, codec=CODEC_BLOSC_LZ4, clevel=5, shuffle=1):

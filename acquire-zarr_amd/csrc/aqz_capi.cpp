@@ -707,6 +707,21 @@ aqz_stage_dominant_kernel(const aqz_stage* st)
     return st ? st->st->dominant_kernel() : "";
 }
 
+aqz_status
+aqz_stage_placement(const aqz_stage* st, double* ms, size_t cap, size_t* n, uint32_t* kept)
+{
+    if (!st)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    const auto& v = st->st->placement_ms();
+    if (n)
+        *n = v.size();
+    if (kept)
+        *kept = uint32_t(st->st->placement_best());
+    for (size_t i = 0; ms && i < v.size() && i < cap; ++i)
+        ms[i] = v[i];
+    return AQZ_STATUS_SUCCESS;
+}
+
 } // extern "C"
 
 // ---- chunk compression ----------------------------------------------------

@@ -262,6 +262,9 @@ class Stage
     void mark(int which);
     double marked_ms();
     const char* dominant_kernel() const;
+    // placement calibration: ms per candidate launch and the one kept
+    const std::vector<double>& placement_ms() const { return placement_ms_; }
+    size_t placement_best() const { return placement_best_; }
 
   private:
     struct Pending
@@ -273,6 +276,8 @@ class Stage
     };
 
     void run_batch(const uint8_t* dsrc, uint32_t n);
+    void place_level(StageLevel& L);
+    void calibrate_placement();
     void build_shard_order(StageLevel& L);
     FusedParams fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
                              uint32_t rh_log2, bool tail);
@@ -337,6 +342,8 @@ class Stage
     uint64_t timed_launches_ = 0;
     hipEvent_t mark_ev_[2] = { nullptr, nullptr };
     hipEvent_t ext_ev_ = nullptr;  // wait_stream
+    std::vector<double> placement_ms_;  // calibration: ms per candidate
+    size_t placement_best_ = 0;
     bool finalized_ = false;
 };
 

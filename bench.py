@@ -523,6 +523,7 @@ def main():
         if args.no_kernel_events:
             kms = elapsed * 1e3
         kernel = st.dominant_kernel()
+        placement = st.placement()
         # algorithmic bytes per launch: every input frame read once, plus
         # every frame each level emitted in the timed region written once
         # (a z-halving level emits half as many frames as its parent)
@@ -533,7 +534,7 @@ def main():
         alg = (emitted[0] * fbytes * (1 if pyramid_only else 2) + out_bytes) // max(1, steps)
         avg_ms = kms / max(1, launches)
         return dict(elapsed=elapsed, sizes=sizes, fbytes=fbytes, kernel=kernel,
-                    avg_ms=avg_ms, alg=alg,
+                    avg_ms=avg_ms, alg=alg, placement=placement,
                     achieved=alg / (avg_ms * 1e-3) / 1e9 if launches else 0.0,
                     value=world * steps * B * fbytes / elapsed / 1e9)
 
@@ -584,7 +585,10 @@ def main():
                      "traffic_source": traffic_src,
                      "kernel": kernel,
                      "kernel_avg_ms": round(avg_ms, 5),
-                     "alg_bytes_per_launch": alg_per_launch},
+                     "alg_bytes_per_launch": alg_per_launch,
+                     # creation-time placement calibration of the chunk-layer
+                     # rings (ms per calibration launch of each candidate)
+                     "placement": main_run["placement"]},
         "input_rate_frac_of_peak": round(value / world / HBM_PEAK_GBS, 4),
     }
     if side:

@@ -53,6 +53,13 @@ aqz_status aqz_stage_timing_elapsed(aqz_stage* st, double* ms);
 /* Name of the dominant kernel symbol (for matching rocprof output). */
 const char* aqz_stage_dominant_kernel(const aqz_stage* st);
 
+/* Placement calibration done at creation (the chunk-layer rings were
+ * allocated up to n times and the fastest placement kept): the ms per
+ * calibration launch of every candidate (up to cap of them, *n = count,
+ * 0 = no calibration ran) and the index of the one kept. */
+aqz_status aqz_stage_placement(const aqz_stage* st, double* ms, size_t cap,
+                               size_t* n, uint32_t* kept);
+
 #ifdef __cplusplus
 }
 #endif
