@@ -331,7 +331,7 @@ class Stage
     uint64_t appended_ = 0, consumed_ = 0;
     void note_consumed(hipStream_t s, uint64_t frames);
     void retire_consumed(bool wait);
-    uint32_t nt_mode_ = 0;           // non-temporal load/store bits
+    uint32_t nt_mode_ = 7;           // nontemporal policy: input loads (1), level-0 (2) and level-1/2 (4) stores
     uint32_t knobs_ = 0;             // tuning A/B switches
     std::vector<Pending> pend_;
     // kernel timing

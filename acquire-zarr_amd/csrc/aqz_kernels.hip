@@ -84,28 +84,64 @@ struct VecT<1>
     using type = uint8_t;
 };
 
-template<typename T, int N>
+// Stores / loads through global (address space 1) pointers: the tile
+// pointers come out of the FrameRef tables, so without the cast the
+// compiler can only prove a generic pointer and emits flat_* instructions.
+// NT selects the nontemporal form at compile time (a runtime branch between
+// a plain and a nontemporal access of the same address folds into one plain
+// access and loses the hint).
+template<typename V>
+using gptr = __attribute__((address_space(1))) V*;
+
+template<bool NT, typename V>
 __device__ __forceinline__ void
-store_vec(uint8_t* p, const T* v, bool nt = false)
+gstore(uint8_t* p, V v)
 {
-    using V = typename VecT<N * sizeof(T)>::type;
-    V raw;
-    __builtin_memcpy(&raw, v, N * sizeof(T));
-    if constexpr (N * sizeof(T) == 8) {
-        if (nt) {
-            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-            u32x2 w;
-            __builtin_memcpy(&w, &raw, 8);
-            __builtin_nontemporal_store(w, reinterpret_cast<u32x2*>(p));
-            return;
-        }
-    } else if constexpr (N * sizeof(T) <= 4) {
-        if (nt) {
-            __builtin_nontemporal_store(raw, reinterpret_cast<V*>(p));
-            return;
-        }
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, (gptr<V>)(p));
+    else
+        *(gptr<V>)(p) = v;
+}
+
+template<bool NT, typename V>
+__device__ __forceinline__ V
+gload(const uint8_t* p)
+{
+    if constexpr (NT)
+        return __builtin_nontemporal_load((const gptr<V>)(p));
+    else
+        return *(const gptr<V>)(p);
+}
+
+// N pixels as one store of N * sizeof(T) bytes
+template<typename T, int N, bool NT>
+__device__ __forceinline__ void
+gstore_px(uint8_t* p, const T* v)
+{
+    typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+    constexpr int B = N * int(sizeof(T));
+    if constexpr (B == 16) {
+        u32x4v w;
+        __builtin_memcpy(&w, v, 16);
+        gstore<NT>(p, w);
+    } else if constexpr (B == 8) {
+        u32x2v w;
+        __builtin_memcpy(&w, v, 8);
+        gstore<NT>(p, w);
+    } else {
+        using V = typename VecT<B>::type;
+        V w;
+        __builtin_memcpy(&w, v, B);
+        gstore<NT>(p, w);
     }
-    *reinterpret_cast<V*>(p) = raw;
+}
+
+template<typename T, int N, bool NT = false>
+__device__ __forceinline__ void
+store_vec(uint8_t* p, const T* v)
+{
+    gstore_px<T, N, NT>(p, v);
 }
 
 template<typename T, int N>
@@ -682,28 +718,23 @@ shfl_down_t(T v, int d)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+template<bool NT>
 __device__ __forceinline__ uint4
-ld16(const uint8_t* s, bool nt)
+ld16(const uint8_t* s)
 {
-    u32x4 v;
-    if (nt)
-        v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s));
-    else
-        v = *reinterpret_cast<const u32x4*>(s);
+    const u32x4 v = gload<NT, u32x4>(s);
     return uint4{ v.x, v.y, v.z, v.w };
 }
 
+template<bool NT>
 __device__ __forceinline__ void
-st16(uint8_t* d, const uint4& a, bool nt)
+st16(uint8_t* d, const uint4& a)
 {
-    const u32x4 v = { a.x, a.y, a.z, a.w };
-    if (nt)
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(d));
-    else
-        *reinterpret_cast<u32x4*>(d) = v;
+    gstore<NT>(d, u32x4{ a.x, a.y, a.z, a.w });
 }
 
 // The two 16-B row vectors of this thread for one pass of an interior region.
+template<int NTM>
 __device__ __forceinline__ void
 load_pass(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
           uint32_t pass, uint32_t bpp, uint4& a, uint4& b)
@@ -712,13 +743,13 @@ load_pass(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
     const uint64_t row = uint64_t(p.W[0]) * bpp;
     const uint8_t* s = p.src + uint64_t(f) * p.src_stride + uint64_t(y) * row +
                        uint64_t(x0 + (threadIdx.x & 31) * (16 / bpp)) * bpp;
-    a = ld16(s, p.nt & 1);
-    b = ld16(s + row, p.nt & 1);
+    a = ld16<(NTM & 1) != 0>(s);
+    b = ld16<(NTM & 1) != 0>(s + row);
 }
 
 // One 16-row pass of an interior region: level-0 tile rows, level 1 (2x2 in
 // registers), level 2 (rows of lanes l and l^32 meet by a cross-lane swap).
-template<typename T, int M, uint32_t RW>
+template<typename T, int M, uint32_t RW, int NTM>
 __device__ __forceinline__ void
 fast_pass(const FusedParams& p, uint32_t pass, const uint4& ra, const uint4& rb,
           FastTile& t0, FastTile& t1, FastTile& t2, T* lds_l2)
@@ -731,8 +762,8 @@ fast_pass(const FusedParams& p, uint32_t pass, const uint4& ra, const uint4& rb,
     const uint32_t trow = p.tw * uint32_t(sizeof(T)); // bytes per tile row
     if (t0.p) {
         const uint32_t dy = pass * 16 + 2 * rp;
-        st16(t0.p + uint64_t(dy) * trow, ra, p.nt & 2);
-        st16(t0.p + uint64_t(dy + 1) * trow, rb, p.nt & 2);
+        st16<(NTM & 2) != 0>(t0.p + uint64_t(dy) * trow, ra);
+        st16<(NTM & 2) != 0>(t0.p + uint64_t(dy + 1) * trow, rb);
         t0.nz |= ((ra.x | ra.y | ra.z | ra.w) | (rb.x | rb.y | rb.z | rb.w)) != 0u;
     }
     if (p.n_fused < 1)
@@ -745,7 +776,7 @@ fast_pass(const FusedParams& p, uint32_t pass, const uint4& ra, const uint4& rb,
     for (int i = 0; i < HV; ++i)
         o[i] = reduce4<M, T>(r0[2 * i], r0[2 * i + 1], r1[2 * i], r1[2 * i + 1]);
     if (t1.p && !(p.knobs & 4u)) {
-        store_vec<T, HV>(t1.p + uint64_t(pass * 8 + rp) * trow, o, p.nt & 4);
+        store_vec<T, HV, (NTM & 4) != 0>(t1.p + uint64_t(pass * 8 + rp) * trow, o);
         t1.nz |= any_nonzero<T, HV>(o);
     }
     if (p.n_fused < 2)
@@ -766,7 +797,7 @@ fast_pass(const FusedParams& p, uint32_t pass, const uint4& ra, const uint4& rb,
             for (int j = 0; j < QV; ++j)
                 q[j] = reduce4<M, T>(o[2 * j], o[2 * j + 1], b[2 * j], b[2 * j + 1]);
             if (t2.p && !(p.knobs & 8u)) {
-                store_vec<T, QV>(t2.p + uint64_t(row2) * trow, q, p.nt & 4);
+                store_vec<T, QV, (NTM & 4) != 0>(t2.p + uint64_t(row2) * trow, q);
                 t2.nz |= any_nonzero<T, QV>(q);
             }
             if (lds_l2) {
@@ -815,7 +846,7 @@ region_of_block(const FusedParams& p)
 // cascade invariant live across the row passes, which costs occupancy.
 constexpr uint32_t kPassBatch = 4;
 
-template<typename T, int M>
+template<typename T, int M, int NTM>
 __global__ __launch_bounds__(256) void
 fused_pyramid(const FusedParams p)
 {
@@ -846,11 +877,11 @@ fused_pyramid(const FusedParams p)
         uint4 ra[kPassBatch], rb[kPassBatch];
 #pragma unroll
         for (uint32_t i = 0; i < kPassBatch; ++i) // passes past npass re-read the last
-            load_pass(p, f, y0, x0, min(p0 + i, npass - 1), sizeof(T), ra[i], rb[i]);
+            load_pass<NTM>(p, f, y0, x0, min(p0 + i, npass - 1), sizeof(T), ra[i], rb[i]);
 #pragma unroll
         for (uint32_t i = 0; i < kPassBatch; ++i)
             if (p0 + i < npass)
-                fast_pass<T, M, RW>(p, p0 + i, ra[i], rb[i], t0, t1, t2, lds_l2);
+                fast_pass<T, M, RW, NTM>(p, p0 + i, ra[i], rb[i], t0, t1, t2, lds_l2);
     }
     if (!(p.knobs & 32u)) {
         flush_tile_flag(t0);
@@ -870,10 +901,14 @@ fused_pyramid(const FusedParams p)
 // cascade down to level 4 needs no LDS and no barrier.  Only pyramids deeper
 // than 4 levels hand their one level-4 row per wave to LDS for levels 5-6.
 // ---------------------------------------------------------------------------
-template<typename T, int M>
+// NTM: compile-time nontemporal policy -- bit 1 input loads, bit 2 level-0
+// tile stores, bit 4 level-1/2 stores (the launcher maps p.nt onto one of the
+// instantiated policies).
+template<typename T, int M, int NTM>
 __global__ __launch_bounds__(256) void
 fused_pyramid_strip(const FusedParams p)
 {
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
     constexpr int VEC = 16 / sizeof(T); // pixels per 16-B row vector
     constexpr int HV = VEC / 2;         // level-1 pixels per lane
     constexpr int QV = VEC / 4;         // level-2 pixels per lane
@@ -909,8 +944,10 @@ fused_pyramid_strip(const FusedParams p)
                            uint64_t(x0 + cv * VEC) * sizeof(T);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            ra[i] = ld16(s + uint64_t(4 * i) * row, p.nt & 1);
-            rb[i] = ld16(s + uint64_t(4 * i + 1) * row, p.nt & 1);
+            const u32x4v a = gload<(NTM & 1) != 0, u32x4v>(s + uint64_t(4 * i) * row);
+            const u32x4v b = gload<(NTM & 1) != 0, u32x4v>(s + uint64_t(4 * i + 1) * row);
+            ra[i] = uint4{ a.x, a.y, a.z, a.w };
+            rb[i] = uint4{ b.x, b.y, b.z, b.w };
         }
     }
     FastTile t0 = fast_tile<T>(p, 0, f, y0 + ry, x0 + cv * VEC);
@@ -923,8 +960,10 @@ fused_pyramid_strip(const FusedParams p)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         if (t0.p) {
-            st16(t0.p + uint64_t(4 * i) * trow, ra[i], p.nt & 2);
-            st16(t0.p + uint64_t(4 * i + 1) * trow, rb[i], p.nt & 2);
+            gstore<(NTM & 2) != 0>(t0.p + uint64_t(4 * i) * trow,
+                                   u32x4v{ ra[i].x, ra[i].y, ra[i].z, ra[i].w });
+            gstore<(NTM & 2) != 0>(t0.p + uint64_t(4 * i + 1) * trow,
+                                   u32x4v{ rb[i].x, rb[i].y, rb[i].z, rb[i].w });
             t0.nz |= ((ra[i].x | ra[i].y | ra[i].z | ra[i].w) |
                       (rb[i].x | rb[i].y | rb[i].z | rb[i].w)) != 0u;
         }
@@ -937,7 +976,7 @@ fused_pyramid_strip(const FusedParams p)
         for (int j = 0; j < HV; ++j)
             o[j] = reduce4<M, T>(r0[2 * j], r0[2 * j + 1], r1[2 * j], r1[2 * j + 1]);
         if (t1.p) {
-            store_vec<T, HV>(t1.p + uint64_t(2 * i) * trow, o, p.nt & 4);
+            gstore_px<T, HV, (NTM & 4) != 0>(t1.p + uint64_t(2 * i) * trow, o);
             t1.nz |= any_nonzero<T, HV>(o);
         }
         if (nf < 2)
@@ -953,7 +992,7 @@ fused_pyramid_strip(const FusedParams p)
         for (int j = 0; j < QV; ++j)
             q2[i][j] = reduce4<M, T>(o[2 * j], o[2 * j + 1], b[2 * j], b[2 * j + 1]);
         if (lane < 32 && t2.p) {
-            store_vec<T, QV>(t2.p + uint64_t(i) * trow, q2[i], p.nt & 4);
+            gstore_px<T, QV, (NTM & 4) != 0>(t2.p + uint64_t(i) * trow, q2[i]);
             t2.nz |= any_nonzero<T, QV>(q2[i]);
         }
     }
@@ -986,7 +1025,7 @@ fused_pyramid_strip(const FusedParams p)
         if (t3.p) {
 #pragma unroll
             for (int rr = 0; rr < 2; ++rr) {
-                store_vec<T, N3>(t3.p + uint64_t(rr) * trow, v3[rr]);
+                gstore_px<T, N3, false>(t3.p + uint64_t(rr) * trow, v3[rr]);
                 t3.nz |= any_nonzero<T, N3>(v3[rr]);
             }
         }
@@ -1012,7 +1051,7 @@ fused_pyramid_strip(const FusedParams p)
         if (valid4)
             t4 = fast_tile<T>(p, 4, f, (y0 >> 4) + w, (x0 >> 4) + (cv / S4) * N4);
         if (t4.p) {
-            store_vec<T, N4>(t4.p, v4);
+            gstore_px<T, N4, false>(t4.p, v4);
             t4.nz |= any_nonzero<T, N4>(v4);
         }
         flush_tile_flag(t4);
@@ -1137,10 +1176,11 @@ flush_planes(const FusedParams& p, int k, uint32_t first, uint32_t g,
     }
 }
 
-template<typename T, int M>
+template<typename T, int M, int NTM>
 __global__ __launch_bounds__(256) void
 fused_pyramid_3d(const FusedParams p)
 {
+    // NTM: compile-time nontemporal policy, as fused_pyramid_strip
     constexpr int VEC = 16 / sizeof(T);
     constexpr int HV = VEC / 2;
     constexpr int QV = HV / 2;
@@ -1178,20 +1218,20 @@ fused_pyramid_3d(const FusedParams p)
     T h1[HV], h2[QV]; // earlier planes of the current z pairs
     const uint32_t units = npass * G;
     uint4 ca, cb;
-    load_pass(p, grp * G, y0, x0, 0, sizeof(T), ca, cb);
+    load_pass<NTM>(p, grp * G, y0, x0, 0, sizeof(T), ca, cb);
     for (uint32_t u = 0; u < units; ++u) {
         const uint32_t pass = u / G, pl = u - pass * G;
         uint4 na{}, nb{};
         if (u + 1 < units) {
             const uint32_t pn = (u + 1) / G;
-            load_pass(p, grp * G + (u + 1 - pn * G), y0, x0, pn, sizeof(T), na, nb);
+            load_pass<NTM>(p, grp * G + (u + 1 - pn * G), y0, x0, pn, sizeof(T), na, nb);
         }
         // level 0: this plane's tile rows
         const Ref f0 = frame_ref(p, 0, grp * G + pl);
         if (f0.tiles) {
             const uint32_t dy = pass * 16 + 2 * rp;
-            st16(f0.tiles + c0.off + uint64_t(dy) * trow, ca, false);
-            st16(f0.tiles + c0.off + uint64_t(dy + 1) * trow, cb, false);
+            st16<(NTM & 2) != 0>(f0.tiles + c0.off + uint64_t(dy) * trow, ca);
+            st16<(NTM & 2) != 0>(f0.tiles + c0.off + uint64_t(dy + 1) * trow, cb);
             if (((ca.x | ca.y | ca.z | ca.w) | (cb.x | cb.y | cb.z | cb.w)) != 0u)
                 nz0 |= 1u << pl;
         }
@@ -1220,7 +1260,8 @@ fused_pyramid_3d(const FusedParams p)
             if (emit1) {
                 const Ref f1 = frame_ref(p, 1, grp * g1 + q1);
                 if (f1.tiles) {
-                    store_vec<T, HV>(f1.tiles + c1.off + uint64_t(pass * 8 + rp) * trow, o);
+                    store_vec<T, HV, (NTM & 4) != 0>(
+                      f1.tiles + c1.off + uint64_t(pass * 8 + rp) * trow, o);
                     if (any_nonzero<T, HV>(o))
                         nz1 |= 1u << q1;
                 }
@@ -1253,7 +1294,8 @@ fused_pyramid_3d(const FusedParams p)
                         const uint32_t row2 = pass * 4 + (rp >> 1);
                         const Ref f2 = frame_ref(p, 2, grp * g2 + q2);
                         if (f2.tiles) {
-                            store_vec<T, QV>(f2.tiles + c2.off + uint64_t(row2) * trow, q);
+                            store_vec<T, QV, (NTM & 4) != 0>(
+                              f2.tiles + c2.off + uint64_t(row2) * trow, q);
                             if (any_nonzero<T, QV>(q))
                                 nz2 |= 1u << q2;
                         }
@@ -1398,12 +1440,30 @@ launch_interior(uint32_t blocks, const FusedParams& p, hipStream_t stream)
     if constexpr (sizeof(T) <= 4) {
         if (p.rh_log2 == 6 && p.n_fused >= 3 && !(p.knobs & 128u) &&
             (p.scratch_level == 0 || p.scratch_level >= 5)) {
-            hipLaunchKernelGGL((fused_pyramid_strip<T, M>), dim3(blocks), dim3(256), 0,
-                               stream, p);
+            switch (p.nt) {
+                case 1:
+                    hipLaunchKernelGGL((fused_pyramid_strip<T, M, 1>), dim3(blocks),
+                                       dim3(256), 0, stream, p);
+                    break;
+                case 3:
+                    hipLaunchKernelGGL((fused_pyramid_strip<T, M, 3>), dim3(blocks),
+                                       dim3(256), 0, stream, p);
+                    break;
+                case 7:
+                    hipLaunchKernelGGL((fused_pyramid_strip<T, M, 7>), dim3(blocks),
+                                       dim3(256), 0, stream, p);
+                    break;
+                default:
+                    hipLaunchKernelGGL((fused_pyramid_strip<T, M, 0>), dim3(blocks),
+                                       dim3(256), 0, stream, p);
+            }
             return;
         }
     }
-    hipLaunchKernelGGL((fused_pyramid<T, M>), dim3(blocks), dim3(256), 0, stream, p);
+    if (p.nt)
+        hipLaunchKernelGGL((fused_pyramid<T, M, 7>), dim3(blocks), dim3(256), 0, stream, p);
+    else
+        hipLaunchKernelGGL((fused_pyramid<T, M, 0>), dim3(blocks), dim3(256), 0, stream, p);
 }
 
 hipError_t
@@ -1444,8 +1504,14 @@ launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
     if (blocks == 0)
         return hipSuccess;
 #define CALL(T, MM)                                                            \
-    hipLaunchKernelGGL((fused_pyramid_3d<T, MM>), dim3(uint32_t(blocks)),     \
-                       dim3(256), 0, stream, p)
+    do {                                                                       \
+        if (p.nt)                                                              \
+            hipLaunchKernelGGL((fused_pyramid_3d<T, MM, 7>), dim3(uint32_t(blocks)), \
+                               dim3(256), 0, stream, p);                      \
+        else                                                                   \
+            hipLaunchKernelGGL((fused_pyramid_3d<T, MM, 0>), dim3(uint32_t(blocks)), \
+                               dim3(256), 0, stream, p);                      \
+    } while (0)
     switch (dtype) {
         case 0: AQZ_DISPATCH_M(uint8_t, method, CALL); break;
         case 1: AQZ_DISPATCH_M(uint16_t, method, CALL); break;

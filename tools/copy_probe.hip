@@ -51,7 +51,12 @@ k_stream(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
 #pragma unroll
     for (int i = 0; i < U; ++i)
         v[i] = ld<NTL>(src + base + i * 256);
-    if constexpr (MODE == 0) { // read only
+    if constexpr (MODE == 3) { // read 1 : write 1/3 (the pyramid-only shape)
+        const size_t b2 = size_t(blockIdx.x) * (U * 256 / 3) + threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < U / 3; ++i)
+            st<NTS>(dst2 + b2 + i * 256, v[3 * i] ^ v[3 * i + 1] ^ v[3 * i + 2]);
+    } else if constexpr (MODE == 0) { // read only
         uint32_t acc = 0;
 #pragma unroll
         for (int i = 0; i < U; ++i)
@@ -98,7 +103,7 @@ run(const char* name, const u32x4* src, u32x4* dst, u32x4* dst2, size_t bytes,
     CK(hipEventElapsedTime(&ms, a, b));
     ms /= reps;
     const double rd = double(per) * 16;
-    const double wr = MODE == 0 ? 0 : rd * (MODE == 2 ? 4.0 / 3.0 : 1.0);
+    const double wr = MODE == 0 ? 0 : rd * (MODE == 2 ? 4.0 / 3.0 : MODE == 3 ? 1.0 / 3.0 : 1.0);
     printf("%-28s U=%d grid=%7u  %.4f ms  read %.0f GB/s  bus %.0f GB/s\n", name, U,
            grid, ms, rd / ms / 1e6, (rd + wr) / ms / 1e6);
 }
@@ -157,6 +162,11 @@ main()
         run<6, false, true, 2>("copy+1/3 nts", s, d, d2, bytes, sink, ring);
         run<6, true, true, 2>("copy+1/3 ntl nts", s, d, d2, bytes, sink, ring);
         run<12, false, false, 2>("copy+1/3", s, d, d2, bytes, sink, ring);
+        run<6, false, false, 3>("read+1/3w", s, d, d2, bytes, sink, ring);
+        run<6, true, false, 3>("read+1/3w ntl", s, d, d2, bytes, sink, ring);
+        run<6, false, true, 3>("read+1/3w nts", s, d, d2, bytes, sink, ring);
+        run<6, true, true, 3>("read+1/3w ntl nts", s, d, d2, bytes, sink, ring);
+        run<12, true, true, 3>("read+1/3w ntl nts", s, d, d2, bytes, sink, ring);
         printf("\n");
     }
     return 0;
