@@ -1216,15 +1216,20 @@ fused_pyramid_3d(const FusedParams p)
     uint32_t nz0 = 0, nz1 = 0, nz2 = 0;
 
     T h1[HV], h2[QV]; // earlier planes of the current z pairs
+    // units = (pass, plane) pairs in pass-major order, processed in order
+    // (z pairs); the rows of the next two units are in flight while one is
+    // reduced
     const uint32_t units = npass * G;
-    uint4 ca, cb;
+    uint4 ca, cb, na{}, nb{};
     load_pass<NTM>(p, grp * G, y0, x0, 0, sizeof(T), ca, cb);
+    if (units > 1)
+        load_pass<NTM>(p, grp * G + (1 % G), y0, x0, 1 / G, sizeof(T), na, nb);
     for (uint32_t u = 0; u < units; ++u) {
         const uint32_t pass = u / G, pl = u - pass * G;
-        uint4 na{}, nb{};
-        if (u + 1 < units) {
-            const uint32_t pn = (u + 1) / G;
-            load_pass<NTM>(p, grp * G + (u + 1 - pn * G), y0, x0, pn, sizeof(T), na, nb);
+        uint4 fa{}, fb{};
+        if (u + 2 < units) {
+            const uint32_t pn = (u + 2) / G;
+            load_pass<NTM>(p, grp * G + (u + 2 - pn * G), y0, x0, pn, sizeof(T), fa, fb);
         }
         // level 0: this plane's tile rows
         const Ref f0 = frame_ref(p, 0, grp * G + pl);
@@ -1310,6 +1315,8 @@ fused_pyramid_3d(const FusedParams p)
         }
         ca = na;
         cb = nb;
+        na = fa;
+        nb = fb;
     }
     flush_planes(p, 0, grp * G, G, c0.chunk, nz0);
     if (p.n_fused >= 1)
