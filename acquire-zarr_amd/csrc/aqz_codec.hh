@@ -72,3 +72,24 @@ struct BloscParams
 hipError_t launch_blosc_lz4(const BloscParams& p, hipStream_t stream);
 
 } // namespace aqz
+
+namespace aqz {
+
+// Block shuffle of a resident chunk layer for the host-side zstd codecs
+// (aqz_hostzstd.hh): block j of chunk c (blocks of `blocksize` bytes) goes,
+// byte- or bit-shuffled as c-blosc 1.x does it, to
+// out + c * nbytes + j * blocksize.  Chunks whose flag is not `tag` are
+// skipped (flags may be null).
+struct ShuffleParams
+{
+    const uint8_t* chunks;
+    uint64_t pitch;
+    uint32_t n_chunks;
+    const uint32_t* flags;
+    uint32_t tag;
+    uint32_t nbytes, typesize, shuffle, blocksize, nblocks;
+    uint8_t* out;
+};
+hipError_t launch_shuffle_blocks(const ShuffleParams& p, hipStream_t stream);
+
+} // namespace aqz

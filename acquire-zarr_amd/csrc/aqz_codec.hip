@@ -601,7 +601,95 @@ write_frames(const BloscParams p)
     copy_bytes(rec + 4, p.scratch + uint64_t(gid) * p.g.slot, n);
 }
 
+// One workgroup per (block, chunk): the c-blosc 1.x byte shuffle (byte jj
+// of element i -> jj * ne + i) or bitshuffle (bit b of byte jj of element
+// 8m + k -> bit k of byte m of plane 8 jj + b) of one block.
+__global__ __launch_bounds__(256) void
+shuffle_blocks(const ShuffleParams p)
+{
+    const uint32_t j = blockIdx.x, c = blockIdx.y;
+    if (p.flags && p.flags[c] != p.tag)
+        return;
+    const uint32_t t = threadIdx.x;
+    const uint32_t b0 = j * p.blocksize;
+    const uint32_t bsize = min(p.blocksize, p.nbytes - b0);
+    const uint32_t ts = p.typesize;
+    const uint32_t ne = bsize / ts;
+    const uint8_t* src = p.chunks + c * p.pitch + b0;
+    uint8_t* dst = p.out + uint64_t(c) * p.nbytes + b0;
+    const bool src16 = (reinterpret_cast<uintptr_t>(src) & 15u) == 0;
+    if (p.shuffle == 1 && ts > 1) {
+        uint32_t done = 0; // elements handled by the vector path
+        if ((ts == 2 || ts == 4 || ts == 8) && src16) {
+            const uint32_t vec = 16 / ts; // elements per 16-B load
+            const bool dst_ok = (reinterpret_cast<uintptr_t>(dst) % vec) == 0 && ne % vec == 0;
+            if (dst_ok) {
+                for (uint32_t w = t; w < ne / vec; w += 256) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(src + 16ull * w);
+                    uint8_t e[16];
+                    __builtin_memcpy(e, &v, 16);
+                    for (uint32_t jj = 0; jj < ts; ++jj) {
+                        uint8_t o[8];
+                        for (uint32_t k = 0; k < vec; ++k)
+                            o[k] = e[k * ts + jj];
+                        uint8_t* d = dst + uint64_t(jj) * ne + uint64_t(w) * vec;
+                        if (vec == 8) {
+                            uint2 x;
+                            __builtin_memcpy(&x, o, 8);
+                            *reinterpret_cast<uint2*>(d) = x;
+                        } else if (vec == 4) {
+                            uint32_t x;
+                            __builtin_memcpy(&x, o, 4);
+                            *reinterpret_cast<uint32_t*>(d) = x;
+                        } else {
+                            uint16_t x;
+                            __builtin_memcpy(&x, o, 2);
+                            *reinterpret_cast<uint16_t*>(d) = x;
+                        }
+                    }
+                }
+                done = ne;
+            }
+        }
+        for (uint32_t x = t; x < (ne - done) * ts; x += 256) {
+            const uint32_t i = done + x / ts, jj = x % ts;
+            dst[uint64_t(jj) * ne + i] = src[uint64_t(i) * ts + jj];
+        }
+        for (uint32_t x = ne * ts + t; x < bsize; x += 256)
+            dst[x] = src[x];
+        return;
+    }
+    if (p.shuffle == 2 && ne % 8 == 0 && ne * ts == bsize) {
+        const uint32_t row = ne / 8;
+        for (uint32_t m = t; m < row; m += 256) {
+            const uint8_t* g = src + uint64_t(8) * m * ts; // 8 elements
+            for (uint32_t jj = 0; jj < ts; ++jj) {
+                uint64_t x = 0;
+                for (uint32_t k = 0; k < 8; ++k)
+                    x |= uint64_t(g[k * ts + jj]) << (8 * k);
+                x = transpose8(x);
+                for (uint32_t b = 0; b < 8; ++b)
+                    dst[uint64_t(jj * 8 + b) * row + m] = uint8_t(x >> (8 * b));
+            }
+        }
+        return;
+    }
+    for (uint32_t x = t; x < bsize; x += 256)
+        dst[x] = src[x];
+}
+
 } // namespace
+
+hipError_t
+launch_shuffle_blocks(const ShuffleParams& p, hipStream_t stream)
+{
+    if (p.n_chunks == 0 || p.nblocks == 0)
+        return hipSuccess;
+    if (p.nblocks > 0x7fffffffu || p.n_chunks > 65535u)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(shuffle_blocks, dim3(p.nblocks, p.n_chunks), dim3(256), 0, stream, p);
+    return hipGetLastError();
+}
 
 hipError_t
 launch_blosc_lz4(const BloscParams& p, hipStream_t stream)

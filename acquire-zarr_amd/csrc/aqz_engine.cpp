@@ -535,6 +535,9 @@ Stage::calibrate_placement()
 
 Stage::~Stage()
 {
+    // host compression jobs read pinned inputs and wait on events: finish
+    // them before anything is freed (the pool drains its queue)
+    zpool_.reset();
     if (stream_)
         (void)hipStreamSynchronize(stream_);
     for (hipStream_t s : { h2d_, comp_, d2h_ })
@@ -564,6 +567,9 @@ Stage::~Stage()
             if (e)
                 (void)hipEventDestroy(e);
         for (hipEvent_t e : L.cdone_ev)
+            if (e)
+                (void)hipEventDestroy(e);
+        for (hipEvent_t e : L.zin_ev)
             if (e)
                 (void)hipEventDestroy(e);
     }
@@ -1320,6 +1326,11 @@ Stage::memory_usage() const
             f.device += b.n;
         for (const PinnedBuf& b : L.h_coffsets)
             f.pinned += b.n;
+        for (const PinnedBuf& b : L.h_zin)
+            f.pinned += b.n;
+        for (const PinnedBuf& b : L.h_zhas)
+            f.pinned += b.n;
+        f.device += L.d_zshuf.n;
         if (L.comp)
             f.device += L.comp->device_bytes();
     }
@@ -1485,8 +1496,17 @@ Stage::compressed_entries(uint32_t level, uint64_t layer, ChunkEntry* out, size_
         throw Error(3, "layer was not compressed (or its slot was reused)");
     if (n < L.n_chunks)
         throw Error(2, "entries too small");
-    hip_check(hipEventSynchronize(L.comp_ev[slot]), "hipEventSynchronize");
-    const uint64_t* off = reinterpret_cast<const uint64_t*>(L.h_coffsets[slot].p);
+    const uint64_t* off;
+    if (L.comp_host[slot]) {
+        HostLayerJob& j = *L.zjob[slot];
+        j.wait();
+        if (j.status)
+            throw Error(j.status, "zstd compression failed");
+        off = j.offsets.data();
+    } else {
+        hip_check(hipEventSynchronize(L.comp_ev[slot]), "hipEventSynchronize");
+        off = reinterpret_cast<const uint64_t*>(L.h_coffsets[slot].p);
+    }
     const uint32_t cl = uint32_t(layer % L.layers_per_shard);
     for (uint32_t i = 0; i < L.n_chunks; ++i) {
         const uint32_t c = L.h_order[i];
@@ -1557,6 +1577,123 @@ Compressor::run(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
 }
 
 void
+Stage::ensure_comp_slots(StageLevel& L)
+{
+    if (!L.cframes.empty())
+        return;
+    L.cframes.resize(L.n_slots);
+    L.coffsets.resize(L.n_slots);
+    L.h_coffsets.resize(L.n_slots);
+    L.comp_ev.assign(L.n_slots, nullptr);
+    L.cdone_ev.assign(L.n_slots, nullptr);
+    L.cdone_pending.assign(L.n_slots, 0);
+    L.comp_layer.assign(L.n_slots, -1);
+    L.h_zin.resize(L.n_slots);
+    L.h_zhas.resize(L.n_slots);
+    L.zin_ev.assign(L.n_slots, nullptr);
+    L.zjob.resize(L.n_slots);
+    L.comp_host.assign(L.n_slots, 0);
+    for (uint32_t s = 0; s < L.n_slots; ++s) {
+        hip_check(hipEventCreateWithFlags(&L.comp_ev[s], hipEventDisableTiming),
+                  "hipEventCreate");
+        hip_check(hipEventCreateWithFlags(&L.cdone_ev[s], hipEventDisableTiming),
+                  "hipEventCreate");
+        hip_check(hipEventCreateWithFlags(&L.zin_ev[s], hipEventDisableTiming),
+                  "hipEventCreate");
+    }
+}
+
+// host threads for the zstd codecs (AQZ_ZSTD_THREADS)
+static unsigned
+zstd_workers()
+{
+    if (const char* s = std::getenv("AQZ_ZSTD_THREADS"))
+        return unsigned(std::max(1, std::atoi(s)));
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    return std::min(16u, std::max(1u, hw - 1));
+}
+
+// blosc-zstd and plain zstd (aqz_hostzstd.hh): on the compression stream,
+// after the kernels that wrote the layer, the layer's blocks are shuffled
+// on the device (blosc-zstd with a shuffle) and the chunks go D2H with their
+// has_data bytes; the host pool compresses as soon as they have landed.
+void
+Stage::compress_layer_host(StageLevel& L, uint32_t slot, uint64_t layer,
+                           const Compression& c)
+{
+    const ZstdLib& z = ZstdLib::get();
+    if (!z.ok)
+        throw Error(4, "libzstd.so.1 is not available: no zstd codecs");
+    if (c.codec == 2 && (c.shuffle < 0 || c.shuffle > 2 || c.clevel < 0 || c.clevel > 9))
+        throw Error(1, "invalid blosc compression settings");
+    if (c.codec == 3 && (c.clevel < -131072 || c.clevel > z.max_clevel()))
+        throw Error(1, "invalid zstd level");
+    if (L.bpc > 0x7fffffefull)
+        throw Error(1, "chunk size outside the blosc1 limits");
+    ensure_comp_slots(L);
+    if (!zpool_)
+        zpool_ = std::make_unique<TaskPool>(zstd_workers());
+    if (L.zjob[slot])
+        L.zjob[slot]->wait(); // its inputs and frames are about to be reused
+    else
+        L.zjob[slot] = std::make_shared<HostLayerJob>();
+    // device frames of an earlier blosc-lz4 use of the slot may still be
+    // on their way out
+    if (L.cdone_pending[slot]) {
+        hip_check(hipStreamWaitEvent(comp_, L.cdone_ev[slot], 0), "hipStreamWaitEvent");
+        L.cdone_pending[slot] = 0;
+    }
+    L.h_zin[slot].alloc(L.layer_bytes);
+    L.h_zhas[slot].alloc(L.n_chunks);
+    hip_check(hipEventRecord(L.ready_ev[slot], stream_), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(comp_, L.ready_ev[slot], 0), "hipStreamWaitEvent");
+    const uint8_t* chunks = L.ring.p + slot * L.slot_bytes;
+    const auto* flags = reinterpret_cast<const uint32_t*>(L.flags.p) + size_t(slot) * L.n_chunks;
+    const uint32_t tag = uint32_t(layer / L.n_slots + 1);
+    const bool shuffle = c.codec == 2 && (c.shuffle == 2 || (c.shuffle == 1 && bpp_ > 1));
+    if (shuffle) {
+        const ZstdBloscGeom g = make_zstd_blosc_geom(uint32_t(L.bpc), uint32_t(bpp_));
+        L.d_zshuf.alloc(L.layer_bytes);
+        ShuffleParams sp{ chunks, L.pitch, L.n_chunks, flags, tag, uint32_t(L.bpc),
+                          uint32_t(bpp_), uint32_t(c.shuffle), g.blocksize, g.nblocks,
+                          L.d_zshuf.p };
+        hip_check(launch_shuffle_blocks(sp, comp_), "shuffle launch");
+        memcpy_pieces(L.h_zin[slot].p, L.d_zshuf.p, L.layer_bytes, hipMemcpyDeviceToHost,
+                      comp_);
+    } else {
+        copy_chunks(L.h_zin[slot].p, chunks, L.bpc, L.pitch, L.n_chunks,
+                    hipMemcpyDeviceToHost, comp_);
+    }
+    uint8_t* fb = L.flag_bytes.p + size_t(slot) * L.n_chunks;
+    hip_check(launch_flags_to_bytes(flags, fb, L.n_chunks, tag, comp_), "flags launch");
+    hip_check(hipMemcpyAsync(L.h_zhas[slot].p, fb, L.n_chunks, hipMemcpyDeviceToHost, comp_),
+              "hipMemcpyAsync");
+    hip_check(hipEventRecord(L.zin_ev[slot], comp_), "hipEventRecord");
+    // the ring slot is rewritten only after this D2H
+    hip_check(hipEventRecord(L.copy_ev[slot], comp_), "hipEventRecord");
+    L.copy_pending[slot] = 1;
+
+    HostLayerJob& j = *L.zjob[slot];
+    j.codec = c.codec;
+    j.clevel = c.clevel;
+    j.shuffle = c.codec == 2 ? c.shuffle : 0;
+    j.typesize = uint32_t(bpp_);
+    j.bpc = L.bpc;
+    j.n_chunks = L.n_chunks;
+    j.chunks = L.h_zin[slot].p;
+    j.has_data = L.h_zhas[slot].p;
+    j.order = L.h_order;
+    const ZstdBloscGeom g = make_zstd_blosc_geom(uint32_t(L.bpc), uint32_t(bpp_));
+    j.frame_cap = std::max<uint64_t>(z.compress_bound(L.bpc),
+                                     L.bpc + 16 + 8ull * g.nblocks + 64);
+    j.tmp.resize(size_t(j.frame_cap) * L.n_chunks);
+    host_zstd_compress(*zpool_, L.zjob[slot],
+                       [ev = L.zin_ev[slot]] { (void)hipEventSynchronize(ev); });
+    L.comp_layer[slot] = int64_t(layer);
+    L.comp_host[slot] = 1;
+}
+
+void
 Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
 {
     if (level >= lv_.size())
@@ -1567,6 +1704,10 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
     const uint32_t slot = uint32_t(layer % L.n_slots);
     if (L.slot_layer[slot] != int64_t(layer))
         throw Error(3, "chunk layer not resident");
+    if (c.codec == 2 || c.codec == 3) {
+        compress_layer_host(L, slot, layer, c);
+        return;
+    }
     if (!L.comp || L.comp_cfg.codec != c.codec || L.comp_cfg.clevel != c.clevel ||
         L.comp_cfg.shuffle != c.shuffle) {
         hip_check(hipStreamSynchronize(comp_), "hipStreamSynchronize");
@@ -1574,21 +1715,10 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
         L.comp = std::make_unique<Compressor>(L.bpc, uint32_t(bpp_), c);
         L.comp_cfg = c;
     }
-    if (L.cframes.empty()) {
-        L.cframes.resize(L.n_slots);
-        L.coffsets.resize(L.n_slots);
-        L.h_coffsets.resize(L.n_slots);
-        L.comp_ev.assign(L.n_slots, nullptr);
-        L.cdone_ev.assign(L.n_slots, nullptr);
-        L.cdone_pending.assign(L.n_slots, 0);
-        L.comp_layer.assign(L.n_slots, -1);
-        for (uint32_t s = 0; s < L.n_slots; ++s) {
-            hip_check(hipEventCreateWithFlags(&L.comp_ev[s], hipEventDisableTiming),
-                      "hipEventCreate");
-            hip_check(hipEventCreateWithFlags(&L.cdone_ev[s], hipEventDisableTiming),
-                      "hipEventCreate");
-        }
-    }
+    ensure_comp_slots(L);
+    if (L.zjob[slot]) // the slot last ran on the host: its inputs are in use
+        L.zjob[slot]->wait();
+    L.comp_host[slot] = 0;
     // the slot's previous frames may still be on their way to the host
     if (L.cdone_pending[slot]) {
         hip_check(hipStreamWaitEvent(comp_, L.cdone_ev[slot], 0), "hipStreamWaitEvent");
@@ -1630,6 +1760,14 @@ Stage::compressed_offsets(uint32_t level, uint64_t layer, uint64_t* offsets, siz
         throw Error(3, "layer was not compressed (or its slot was reused)");
     if (n < size_t(L.n_chunks) + 1)
         throw Error(2, "offsets too small");
+    if (L.comp_host[slot]) {
+        HostLayerJob& j = *L.zjob[slot];
+        j.wait();
+        if (j.status)
+            throw Error(j.status, "zstd compression failed");
+        std::memcpy(offsets, j.offsets.data(), (size_t(L.n_chunks) + 1) * 8);
+        return;
+    }
     hip_check(hipEventSynchronize(L.comp_ev[slot]), "hipEventSynchronize");
     std::memcpy(offsets, L.h_coffsets[slot].p, (size_t(L.n_chunks) + 1) * 8);
 }
@@ -1643,6 +1781,17 @@ Stage::copy_compressed_async(uint32_t level, uint64_t layer, void* dst, size_t c
     const uint32_t slot = L.n_slots ? uint32_t(layer % L.n_slots) : 0;
     if (L.comp_layer.empty() || L.comp_layer[slot] != int64_t(layer))
         throw Error(3, "layer was not compressed (or its slot was reused)");
+    if (L.comp_host[slot]) {
+        // host frames: gathered into dst (host memory) right away
+        HostLayerJob& j = *L.zjob[slot];
+        j.wait();
+        if (j.status)
+            throw Error(j.status, "zstd compression failed");
+        if (cap < j.offsets[L.n_chunks])
+            throw Error(2, "destination too small for the compressed layer");
+        j.gather(static_cast<uint8_t*>(dst));
+        return;
+    }
     hip_check(hipEventSynchronize(L.comp_ev[slot]), "hipEventSynchronize");
     const uint64_t total =
       reinterpret_cast<const uint64_t*>(L.h_coffsets[slot].p)[L.n_chunks];

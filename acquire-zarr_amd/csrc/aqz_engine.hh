@@ -11,6 +11,7 @@
 #include "aqz_codec.hh"
 #include "aqz_copy.hh"
 #include "aqz_geometry.hh"
+#include "aqz_hostzstd.hh"
 #include "aqz_params.hh"
 
 #include <hip/hip_runtime.h>
@@ -183,6 +184,14 @@ struct StageLevel
     std::vector<hipEvent_t> cdone_ev;      // the slot's frames were copied out
     std::vector<uint8_t> cdone_pending;
     std::vector<int64_t> comp_layer;       // layer compressed in each slot
+    // host-side zstd codecs (aqz_hostzstd.hh): per slot the pinned inputs
+    // (shuffled or raw chunks, has_data bytes), their D2H event and the
+    // host job; comp_host[slot] = the slot's compression ran on the host
+    std::vector<PinnedBuf> h_zin, h_zhas;
+    std::vector<hipEvent_t> zin_ev;
+    std::vector<std::shared_ptr<HostLayerJob>> zjob;
+    std::vector<uint8_t> comp_host;
+    DevBuf d_zshuf;                        // device shuffle target
     // shard packing: compressed frames leave in shard-major order
     // (shard_index_for_chunk, then shard_internal_index); internal indices
     // of a layer = h_internal0 + (layer mod layers_per_shard) * stride
@@ -279,6 +288,9 @@ class Stage
     void place_level(StageLevel& L);
     void calibrate_placement();
     void build_shard_order(StageLevel& L);
+    void ensure_comp_slots(StageLevel& L);
+    void compress_layer_host(StageLevel& L, uint32_t slot, uint64_t layer,
+                             const Compression& c);
     FusedParams fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
                              uint32_t rh_log2, bool tail);
     void run_fused(const uint8_t* dsrc, uint32_t n);
@@ -319,6 +331,7 @@ class Stage
     // compresses while layer i's frames go D2H on d2h_
     hipStream_t comp_ = nullptr;
     std::unique_ptr<CopyPool> pool_;
+    std::unique_ptr<TaskPool> zpool_; // host zstd workers
     // XY-transposed storage order: level-0 frames are transposed into xbuf_
     // (acquisition rows x cols -> storage rows x cols) before the pipeline
     bool xy_ = false;

@@ -202,7 +202,8 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
         src_arr = np.empty(src_frames * fbytes, dtype=np.uint8)
         src_ptr, mem = src_arr.ctypes.data, aqz.MEM_HOST
     rng = np.random.default_rng(7 + rank)
-    if args.compress:
+    codec = {"none": 0, "lz4": 1, "blosc-zstd": 2, "zstd": 3}[args.codec]
+    if codec:
         # compressible camera-like frames (smooth background + noise)
         n_px = src_arr.size // bpp
         v = 1000.0 + 200.0 * np.sin(np.arange(n_px) / 977.0) + rng.normal(0, 30.0, n_px)
@@ -217,6 +218,7 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
     hd = [[aqz.HostBuffer(lay[l]["chunks_per_layer"]) for _ in range(4)] for l in range(L)]
     handed = [0] * L
     d2h = [0]
+    out_bytes = [0]  # bytes handed to the sink (frames or raw chunks)
     pending = []  # compressed layers whose frames are not copied yet
 
     def drain_compressed():
@@ -225,22 +227,26 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
             i = layer % 4
             off = st.compressed_offsets(l, layer)
             st.copy_compressed_async(l, layer, dst[l][i].ptr, cap[l])
-            d2h[0] += int(off[-1])
+            # PCIe bytes: the frames (device lz4) or the shuffled layer (host zstd)
+            d2h[0] += int(off[-1]) if codec == 1 else lbytes[l]
+            out_bytes[0] += int(off[-1])
 
     def hand_off():
-        if args.compress:
+        if codec:
             drain_compressed()  # last step's layers: their kernels are done by now
         for l in range(L):
             done = st.frames_written(l) // lay[l]["frames_per_layer"]
             while handed[l] < done:
                 i = handed[l] % 4
-                if args.compress:
-                    st.compress_layer(l, handed[l], clevel=5, shuffle=args.compress)
+                if codec:
+                    st.compress_layer(l, handed[l], codec=codec,
+                                      clevel=3 if codec == 3 else 5, shuffle=args.compress)
                     pending.append((l, handed[l]))
                 else:
                     st.copy_layer_async(l, handed[l], dst[l][i].ptr, lbytes[l],
                                         hd[l][i].ptr, hd[l][i].nbytes)
                     d2h[0] += lbytes[l]
+                    out_bytes[0] += lbytes[l]
                 handed[l] += 1
 
     def step(s):
@@ -255,6 +261,7 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
     if dist:
         dist.barrier()
     d2h[0] = 0
+    out_bytes[0] = 0
     t0 = time.perf_counter()
     for s in range(args.steps):
         step(args.warmup + s)
@@ -271,15 +278,18 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
     in_bytes = args.steps * B * fbytes
     return {
         "metric": "end-to-end input GB/s, host frames -> H2D -> multiscale stage -> "
-                  + ("device blosc-lz4 compression (shuffle %d) -> D2H of every "
-                     "compressed chunk layer" % args.compress if args.compress
-                     else "D2H of every chunk layer"),
+                  + ({1: "device blosc-lz4 compression (shuffle %d) -> D2H of every "
+                         "compressed chunk layer" % args.compress,
+                      2: "device shuffle (%d) -> D2H -> host blosc-zstd of every chunk "
+                         "layer" % args.compress,
+                      3: "D2H -> host zstd (level 3) of every chunk layer"}[codec]
+                     if codec else "D2H of every chunk layer"),
         "value": round(world * in_bytes / el / 1e9, 3), "unit": "GB/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el * 1e3 / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
         "dtype": {U8: "u8", U16: "u16", F32: "f32"}[dt],
-        "data": f"synthetic{' camera-like' if args.compress else ' random'}, host {args.e2e} source ring of {src_frames} frames",
+        "data": f"synthetic{' camera-like' if codec else ' random'}, host {args.e2e} source ring of {src_frames} frames",
         "config": {"workload": cfg["workload"].replace("device-resident", "host-resident") +
                    f" [e2e, {args.e2e} source]", "frames_per_step_per_gpu": B,
                    "levels": L},
@@ -287,6 +297,7 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
         "d2h_gbs_per_gpu": round(d2h[0] / el / 1e9, 3),
         "frames_per_s_per_gpu": round(args.steps * B / el, 1),
         "d2h_bytes_per_input_byte": round(d2h[0] / in_bytes, 4),
+        "sink_bytes_per_input_byte": round(out_bytes[0] / in_bytes, 4),
     }
 
 
@@ -418,14 +429,21 @@ def main():
     ap.add_argument("--batch", type=int, default=0,
                     help="frames per append (default: the config's batch)")
     ap.add_argument("--compress", type=int, default=0, choices=[0, 1, 2],
-                    help="e2e: compress every chunk layer on the device (blosc-lz4, "
-                         "1 = byte shuffle, 2 = bitshuffle) and hand off the frames")
+                    help="e2e: compress every chunk layer (blosc shuffle: 1 = byte, "
+                         "2 = bit) and hand off the frames; implies --codec lz4 "
+                         "unless --codec says otherwise")
+    ap.add_argument("--codec", default="none",
+                    choices=["none", "lz4", "blosc-zstd", "zstd"],
+                    help="e2e: chunk codec (lz4: blosc1-lz4 on the device; blosc-zstd "
+                         "and zstd: device shuffle + host zstd pool)")
     ap.add_argument("--e2e", choices=["pinned", "pageable"], default=None,
                     help="end-to-end mode: frames start in host memory (pinned or "
                          "pageable), every completed chunk layer is handed back to "
                          "pinned host buffers (DESIGN.md 'End to end')")
     ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.codec == "none" and args.compress:
+        args.codec = "lz4"
 
     if args.gpus < 1:
         sys.exit("--gpus must be >= 1")

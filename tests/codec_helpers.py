@@ -135,3 +135,88 @@ def chunk_payloads(rng, dtype, n_px: int, kinds=("camera", "zeros", "random",
             a = (np.arange(n_px) % 251).astype(dtype)
         out[k] = a
     return out
+
+
+# ---- zstd (blosc-zstd and plain zstd frames) ------------------------------
+_LIBZSTD_PATHS = (os.path.join(ORACLE_DIR, "_ref", "lib", "libzstd.so.1"),
+                  "/opt/conda/lib/libzstd.so.1", "libzstd.so.1")
+_zstd = None
+
+
+def libzstd():
+    """libzstd (test-only decoder): conda's copy, else the system's."""
+    global _zstd
+    if _zstd is None:
+        for p in _LIBZSTD_PATHS:
+            try:
+                L = C.CDLL(p)
+            except OSError:
+                continue
+            L.ZSTD_decompress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
+            L.ZSTD_decompress.restype = C.c_size_t
+            L.ZSTD_isError.argtypes = [C.c_size_t]
+            L.ZSTD_isError.restype = C.c_uint
+            L.ZSTD_getFrameContentSize.argtypes = [C.c_void_p, C.c_size_t]
+            L.ZSTD_getFrameContentSize.restype = C.c_ulonglong
+            L.ZSTD_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                        C.c_int]
+            L.ZSTD_compress.restype = C.c_size_t
+            L.ZSTD_compressBound.argtypes = [C.c_size_t]
+            L.ZSTD_compressBound.restype = C.c_size_t
+            _zstd = L
+            break
+        else:
+            _zstd = False
+    return _zstd or None
+
+
+def zstd_decode(frame, nbytes: int) -> bytes:
+    L = libzstd()
+    frame = bytes(frame)
+    out = C.create_string_buffer(max(1, nbytes))
+    n = L.ZSTD_decompress(out, nbytes, frame, len(frame))
+    assert not L.ZSTD_isError(n) and n == nbytes, f"zstd decode failed ({n})"
+    return out.raw[:nbytes]
+
+
+def zstd_compress(data: bytes, level: int) -> bytes:
+    L = libzstd()
+    cap = L.ZSTD_compressBound(len(data))
+    out = C.create_string_buffer(cap)
+    n = L.ZSTD_compress(out, cap, data, len(data), level)
+    assert not L.ZSTD_isError(n)
+    return out.raw[:n]
+
+
+def blosc_zstd_decode(frame) -> bytes:
+    """A blosc1 frame decoded by this restatement of the published format
+    (header, block starts, per block per stream (csize, bytes); csize ==
+    stream bytes = stored raw) with libzstd for the streams and the oracle's
+    unshuffles -- independent of c-blosc."""
+    frame = bytes(frame)
+    h = header(frame)
+    nbytes, bs, ts, fl = h["nbytes"], h["blocksize"], h["typesize"], h["flags"]
+    assert (fl >> 5) == 4, "not a zstd blosc frame"
+    if fl & 0x2:
+        return frame[16:16 + nbytes]
+    nblocks = -(-nbytes // bs)
+    starts = struct.unpack("<%dI" % nblocks, frame[16:16 + 4 * nblocks])
+    out = bytearray()
+    for j in range(nblocks):
+        blen = min(bs, nbytes - j * bs)
+        split = not (fl & 0x10) and ts <= 16 and blen // ts >= 128 and blen == bs
+        ns = ts if split else 1
+        pos = starts[j]
+        blk = bytearray()
+        for _ in range(ns):
+            cs = struct.unpack("<I", frame[pos:pos + 4])[0]
+            slen = blen // ns
+            data = frame[pos + 4:pos + 4 + cs]
+            blk += data if cs == slen else zstd_decode(data, slen)
+            pos += 4 + cs
+        if fl & 0x1 and ts > 1:
+            blk = shuffle("unshuffle", ts, bytes(blk))
+        elif fl & 0x4:
+            blk = shuffle("bitunshuffle", ts, bytes(blk))
+        out += blk
+    return bytes(out)

@@ -100,3 +100,21 @@ def test_shard_table_layout_and_crc():
     for n in (0, 1, 31, 1000):
         d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
         assert aqz.crc32c(d) == crc32c(d)
+
+
+@pytest.mark.skipif(libblosc() is None, reason="c-blosc not in this image")
+def test_blosc_zstd_decoder_restatement_pinned_to_cblosc():
+    """codec_helpers.blosc_zstd_decode (the GPU zstd tests' independent
+    decoder) reads c-blosc 1.21.0's own zstd frames -- split and unsplit
+    blocks, byte/bit shuffle, raw (incompressible) streams, memcpyed frames."""
+    from codec_helpers import blosc_zstd_decode, camera_like, libblosc_compress, libzstd
+    if libzstd() is None:
+        pytest.skip("no libzstd")
+    rng = np.random.default_rng(1)
+    for ts, dt in ((1, np.uint8), (2, np.uint16), (4, np.uint32), (8, np.uint64)):
+        for sh in (0, 1, 2):
+            for clevel in (0, 1, 5, 9):
+                a = camera_like(rng, 300_000 // ts, dt).tobytes()
+                assert blosc_zstd_decode(libblosc_compress(a, ts, clevel, sh, b"zstd")) == a
+                r = rng.integers(0, 256, len(a), dtype=np.uint8).tobytes()
+                assert blosc_zstd_decode(libblosc_compress(r, ts, clevel, sh, b"zstd")) == r

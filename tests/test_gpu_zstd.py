@@ -1,0 +1,131 @@
+"""GPU stage with the zstd codecs (SURVEY §8f rank 2 remainder): blosc1
+frames with codec zstd (zarr.common.cpp:106-140 with "zstd") and plain zstd
+frames (zarr.common.cpp:142-166), as Chunk::compress_and_take_buffer
+dispatches them (chunk.cpp:78-106).  The device shuffles every block of the
+resident layer and the host zstd pool compresses (aqz_hostzstd.hh).
+
+Bar: every frame decodes to the oracle's chunk exactly -- blosc-zstd with a
+restated blosc1 decoder over libzstd (codec_helpers.blosc_zstd_decode) and
+with c-blosc 1.21.0 itself, plain zstd with libzstd -- chunks without data
+are skipped, incompressible chunks become memcpyed frames (blosc's rule),
+and the ratio on camera-like data stays close to c-blosc's zstd."""
+import numpy as np
+import pytest
+
+from codec_helpers import (blosc_zstd_decode, camera_like, header, libblosc,
+                           libblosc_compress, libblosc_decode, libzstd, zstd_compress,
+                           zstd_decode)
+from helpers import expected_stage_layers
+from oracle_bindings import MEAN, SPACE, TIME, U8, U16, F32, synthetic_frames
+
+pytestmark = pytest.mark.gpu
+
+needs_zstd = pytest.mark.skipif(libzstd() is None, reason="no libzstd to decode with")
+
+
+def _frames(dtype, n, h, w, seed):
+    """Half incompressible (random) rows, half camera-like, and one band of
+    all-zero chunks."""
+    fr = synthetic_frames(dtype, n, h, w, seed)
+    rng = np.random.default_rng(seed)
+    npdt = fr.dtype
+    cam = camera_like(rng, n * (h // 2) * w, np.uint16).astype(np.float64)
+    if dtype == U8:
+        cam = cam / 8
+    fr[:, h // 2:, :] = cam.astype(npdt).reshape(n, h // 2, w)
+    fr[:, : h // 8, :] = 0
+    return fr
+
+
+def _run(gpu, dtype, codec, clevel, shuffle):
+    dims = [(TIME, 0, 2, 1), (SPACE, 512, 128, 1), (SPACE, 384, 128, 1)]
+    n = 6
+    frames = _frames(dtype, n, 512, 384, 40 + codec * 3 + shuffle)
+    exp, fw, _ = expected_stage_layers(dims, dtype, MEAN, frames)
+    st = gpu.Stage(dims, dtype, MEAN, layer_slots=2, max_batch_frames=2)
+    L = st.n_levels()
+    lay = [st.layout(l) for l in range(L)]
+    got = {}
+    for b in range(0, n, 2):
+        st.append(np.ascontiguousarray(frames[b:b + 2]))
+        for l in range(L):
+            layer = st.frames_written(l) // lay[l]["frames_per_layer"] - 1
+            if layer >= 0 and (l, layer) not in got:
+                st.compress_layer(l, layer, codec=codec, clevel=clevel, shuffle=shuffle)
+                got[(l, layer)] = (st.copy_compressed(l, layer)[0],
+                                   st.compressed_entries(l, layer))
+    st.close()
+    assert sorted(got) == sorted(exp)
+    n_memcpy = n_frames = 0
+    for (l, layer), (buf, flags) in exp.items():
+        data, ent = got[(l, layer)]
+        bpc = lay[l]["bytes_per_chunk"]
+        assert sorted(e[0] for e in ent) == list(range(lay[l]["chunks_per_layer"]))
+        for c, _, _, o, nb in ent:
+            fr = data[o:o + nb].tobytes()
+            if not flags[c]:
+                assert len(fr) == 0, (l, layer, c)
+                continue
+            chunk = buf[c * bpc:(c + 1) * bpc].tobytes()
+            n_frames += 1
+            if codec == 3:
+                assert zstd_decode(fr, bpc) == chunk, (l, layer, c)
+                continue
+            h = header(fr)
+            assert h["version"] == 2 and (h["flags"] >> 5) == 4 and h["nbytes"] == bpc
+            assert h["typesize"] == {U8: 1, U16: 2, F32: 4}[dtype]
+            assert h["cbytes"] == len(fr) and len(fr) <= bpc + 16
+            if h["flags"] & 0x2:
+                n_memcpy += 1
+            else:
+                assert bool(h["flags"] & 0x1) == (shuffle == 1)
+                assert bool(h["flags"] & 0x4) == (shuffle == 2)
+            assert blosc_zstd_decode(fr) == chunk, (l, layer, c, h)
+            if libblosc() is not None:
+                assert libblosc_decode(fr) == chunk, (l, layer, c, h)
+    assert n_frames > 0
+    return n_memcpy
+
+
+@needs_zstd
+@pytest.mark.parametrize("dtype", [U8, U16, F32], ids=["u8", "u16", "f32"])
+@pytest.mark.parametrize("shuffle", [0, 1, 2])
+def test_stage_blosc_zstd_layers(gpu, dtype, shuffle):
+    _run(gpu, dtype, 2, 5, shuffle)
+
+
+@needs_zstd
+def test_stage_blosc_zstd_clevel0_memcpyed(gpu):
+    assert _run(gpu, U16, 2, 0, 1) > 0
+
+
+@needs_zstd
+@pytest.mark.parametrize("level", [1, 3, 9])
+def test_stage_plain_zstd_layers(gpu, level):
+    _run(gpu, U16, 3, level, 0)
+
+
+@needs_zstd
+@pytest.mark.skipif(libblosc() is None, reason="c-blosc not in this image")
+def test_blosc_zstd_ratio_close_to_cblosc(gpu):
+    """One C2-shaped chunk layer level (256x256 chunks, 8 frames) of
+    camera-like u16 data: the device+host frames are at most 10% larger than
+    c-blosc zstd clevel 5 on the same chunks; plain zstd at level 3 within 5%
+    of ZSTD_compress (the same library, bigger single frames here)."""
+    dims = [(TIME, 0, 8, 1), (SPACE, 512, 256, 1), (SPACE, 512, 256, 1)]
+    rng = np.random.default_rng(8)
+    frames = camera_like(rng, 8 * 512 * 512, np.uint16).reshape(8, 512, 512)
+    st = gpu.Stage(dims, U16, MEAN, multiscale=False, layer_slots=2, max_batch_frames=8)
+    st.append(frames)
+    layer, _ = st.copy_layer(0, 0)
+    bpc = st.layout(0)["bytes_per_chunk"]
+    chunks = [layer[c * bpc:(c + 1) * bpc].tobytes() for c in range(4)]
+    for codec, shuffle, ref in ((2, 1, lambda ch: libblosc_compress(ch, 2, 5, 1, b"zstd")),
+                                (2, 2, lambda ch: libblosc_compress(ch, 2, 5, 2, b"zstd")),
+                                (3, 0, lambda ch: zstd_compress(ch, 5))):
+        st.compress_layer(0, 0, codec=codec, clevel=5, shuffle=shuffle)
+        data, off = st.copy_compressed(0, 0)
+        ours = int(off[-1])
+        theirs = sum(len(ref(ch)) for ch in chunks)
+        assert ours <= 1.10 * theirs, (codec, shuffle, ours, theirs)
+    st.close()
