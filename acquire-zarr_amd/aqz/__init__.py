@@ -199,6 +199,7 @@ def lib():
         "aqz_stage_dominant_kernel": ([vp], C.c_char_p),
         "aqz_stage_placement": ([vp, C.POINTER(C.c_double), sz, C.POINTER(sz),
                                  C.POINTER(u32)], i32),
+        "aqz_stage_host_affinity": ([vp, C.POINTER(i32), C.POINTER(u32)], i32),
         "aqz_stage_compress_layer": ([vp, u32, u64, C.POINTER(CompressionC)], i32),
         "aqz_stage_compressed_offsets": ([vp, u32, u64, C.POINTER(u64), sz], i32),
         "aqz_stage_copy_compressed_async": ([vp, u32, u64, vp, sz], i32),
@@ -622,6 +623,13 @@ class Stage:
 
     def dominant_kernel(self):
         return lib().aqz_stage_dominant_kernel(self.h).decode()
+
+    def host_affinity(self):
+        """(NUMA node of the device, CPUs the host pools are pinned to)."""
+        node, n = C.c_int32(-1), C.c_uint32(0)
+        _check(lib().aqz_stage_host_affinity(self.h, C.byref(node), C.byref(n)),
+               "host_affinity")
+        return node.value, n.value
 
     def placement(self):
         """Creation-time placement calibration: {"candidates_ms": [...],

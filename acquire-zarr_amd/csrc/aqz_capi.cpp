@@ -708,6 +708,18 @@ aqz_stage_dominant_kernel(const aqz_stage* st)
 }
 
 aqz_status
+aqz_stage_host_affinity(const aqz_stage* st, int32_t* numa_node, uint32_t* n_cpus)
+{
+    if (!st)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    if (numa_node)
+        *numa_node = st->st->numa_node();
+    if (n_cpus)
+        *n_cpus = uint32_t(st->st->numa_cpus());
+    return AQZ_STATUS_SUCCESS;
+}
+
+aqz_status
 aqz_stage_placement(const aqz_stage* st, double* ms, size_t cap, size_t* n, uint32_t* kept)
 {
     if (!st)

@@ -1,13 +1,79 @@
 #include "aqz_copy.hh"
 
+#include <pthread.h>
+#include <sched.h>
+
+#include <cctype>
 #include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
 
 namespace aqz {
 
-CopyPool::CopyPool(unsigned workers)
+std::vector<int>
+numa_cpus_for_pci(const char* bus_id, int* node_out)
+{
+    std::vector<int> cpus;
+    if (node_out)
+        *node_out = -1;
+    if (!bus_id || !*bus_id)
+        return cpus;
+    std::string id(bus_id);
+    for (auto& ch : id)
+        ch = char(std::tolower(static_cast<unsigned char>(ch)));
+    int node = -1;
+    {
+        std::ifstream f("/sys/bus/pci/devices/" + id + "/numa_node");
+        if (!(f >> node) || node < 0)
+            return cpus;
+    }
+    if (node_out)
+        *node_out = node;
+    std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+    std::string list;
+    if (!std::getline(f, list))
+        return cpus;
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0)
+        return cpus;
+    std::stringstream ss(list);
+    std::string part;
+    while (std::getline(ss, part, ',')) {
+        int a = -1, b = -1;
+        if (std::sscanf(part.c_str(), "%d-%d", &a, &b) == 2) {
+        } else if (std::sscanf(part.c_str(), "%d", &a) == 1) {
+            b = a;
+        } else {
+            continue;
+        }
+        for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+            if (c >= 0 && CPU_ISSET(c, &allowed))
+                cpus.push_back(c);
+    }
+    return cpus;
+}
+
+void
+pin_current_thread(const std::vector<int>& cpus)
+{
+    if (cpus.empty())
+        return;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    for (int c : cpus)
+        CPU_SET(c, &set);
+    (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
+
+CopyPool::CopyPool(unsigned workers, std::vector<int> cpus)
 {
     for (unsigned i = 0; i < workers; ++i)
-        threads_.emplace_back([this, i] { run(i); });
+        threads_.emplace_back([this, i, cpus] {
+            pin_current_thread(cpus);
+            run(i);
+        });
 }
 
 CopyPool::~CopyPool()

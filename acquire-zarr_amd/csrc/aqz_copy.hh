@@ -16,10 +16,18 @@
 
 namespace aqz {
 
+// NUMA placement of the host threads that feed one GPU (one
+// host thread group per GPU, pinned to the GPU's NUMA node).  The CPUs of
+// the NUMA node of PCI device `bus_id` ("dddd:bb:dd.f"), intersected with
+// this process's affinity; empty when unknown (no sysfs entry, node -1).
+std::vector<int> numa_cpus_for_pci(const char* bus_id, int* node = nullptr);
+// Pins the calling thread to `cpus` (no-op when empty).
+void pin_current_thread(const std::vector<int>& cpus);
+
 class CopyPool
 {
   public:
-    explicit CopyPool(unsigned workers);
+    explicit CopyPool(unsigned workers, std::vector<int> cpus = {});
     ~CopyPool();
     CopyPool(const CopyPool&) = delete;
     CopyPool& operator=(const CopyPool&) = delete;

@@ -223,6 +223,14 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
     hip_check(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking),
               "hipStreamCreate");
     stream_ = own_stream_;
+    {
+        const char* e = std::getenv("AQZ_NUMA");
+        char bus[64] = { 0 };
+        if (!(e && std::atoi(e) == 0) &&
+            hipDeviceGetPCIBusId(bus, int(sizeof(bus)), desc.device) == hipSuccess)
+            numa_cpus_ = numa_cpus_for_pci(bus, &numa_node_);
+        (void)hipGetLastError();
+    }
 
     const size_t n = base->ndims();
     const uint32_t B = opt_.max_batch_frames;
@@ -732,7 +740,7 @@ Stage::append(const void* frames, uint64_t n_frames, int mem)
                 h_stage_[j].alloc(size_t(B) * fbytes);
                 hip_check(hipEventSynchronize(h2d_ev_[j]), "hipEventSynchronize");
                 if (!pool_)
-                    pool_ = std::make_unique<CopyPool>(copy_workers());
+                    pool_ = std::make_unique<CopyPool>(copy_workers(), numa_cpus_);
                 pool_->copy(h_stage_[j].p, p, nbytes);
                 hsrc = h_stage_[j].p;
             }
@@ -1632,7 +1640,7 @@ Stage::compress_layer_host(StageLevel& L, uint32_t slot, uint64_t layer,
         throw Error(1, "chunk size outside the blosc1 limits");
     ensure_comp_slots(L);
     if (!zpool_)
-        zpool_ = std::make_unique<TaskPool>(zstd_workers());
+        zpool_ = std::make_unique<TaskPool>(zstd_workers(), numa_cpus_);
     if (L.zjob[slot])
         L.zjob[slot]->wait(); // its inputs and frames are about to be reused
     else

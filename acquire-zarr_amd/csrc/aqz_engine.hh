@@ -271,6 +271,8 @@ class Stage
     void mark(int which);
     double marked_ms();
     const char* dominant_kernel() const;
+    int numa_node() const { return numa_node_; }
+    size_t numa_cpus() const { return numa_cpus_.size(); }
     // placement calibration: ms per candidate launch and the one kept
     const std::vector<double>& placement_ms() const { return placement_ms_; }
     size_t placement_best() const { return placement_best_; }
@@ -332,6 +334,10 @@ class Stage
     hipStream_t comp_ = nullptr;
     std::unique_ptr<CopyPool> pool_;
     std::unique_ptr<TaskPool> zpool_; // host zstd workers
+    // CPUs of the device's NUMA node: the host pools run there (AQZ_NUMA=0
+    // turns it off)
+    std::vector<int> numa_cpus_;
+    int numa_node_ = -1;
     // XY-transposed storage order: level-0 frames are transposed into xbuf_
     // (acquisition rows x cols -> storage rows x cols) before the pipeline
     bool xy_ = false;

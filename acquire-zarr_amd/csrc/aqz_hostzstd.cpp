@@ -1,6 +1,8 @@
 // aqz_hostzstd.cpp -- see aqz_hostzstd.hh.
 #include "aqz_hostzstd.hh"
 
+#include "aqz_copy.hh"
+
 #include <dlfcn.h>
 
 #include <algorithm>
@@ -32,10 +34,13 @@ ZstdLib::get()
 }
 
 // ---- task pool ---------------------------------------------------------------
-TaskPool::TaskPool(unsigned workers)
+TaskPool::TaskPool(unsigned workers, std::vector<int> cpus)
 {
     for (unsigned i = 0; i < std::max(1u, workers); ++i)
-        threads_.emplace_back([this] { run(); });
+        threads_.emplace_back([this, cpus] {
+            pin_current_thread(cpus);
+            run();
+        });
 }
 
 TaskPool::~TaskPool()

@@ -52,7 +52,8 @@ struct ZstdLib
 class TaskPool
 {
   public:
-    explicit TaskPool(unsigned workers);
+    // cpus: pin every worker there (empty = no pinning)
+    explicit TaskPool(unsigned workers, std::vector<int> cpus = {});
     ~TaskPool();
     TaskPool(const TaskPool&) = delete;
     TaskPool& operator=(const TaskPool&) = delete;

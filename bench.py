@@ -274,6 +274,7 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
         t = torch.tensor([el], dtype=torch.float64, device=reduce_dev(dist, dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    affinity = st.host_affinity()
     st.close()
     in_bytes = args.steps * B * fbytes
     return {
@@ -296,6 +297,7 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
         "h2d_gbs_per_gpu": round(in_bytes / el / 1e9, 3),
         "d2h_gbs_per_gpu": round(d2h[0] / el / 1e9, 3),
         "frames_per_s_per_gpu": round(args.steps * B / el, 1),
+        "host_threads": {"numa_node": affinity[0], "pinned_cpus": affinity[1]},
         "d2h_bytes_per_input_byte": round(d2h[0] / in_bytes, 4),
         "sink_bytes_per_input_byte": round(out_bytes[0] / in_bytes, 4),
     }

@@ -60,6 +60,12 @@ const char* aqz_stage_dominant_kernel(const aqz_stage* st);
 aqz_status aqz_stage_placement(const aqz_stage* st, double* ms, size_t cap,
                                size_t* n, uint32_t* kept);
 
+/* NUMA placement of the stage's host threads (staging copy pool, host zstd
+ * pool): the NUMA node of the stage's device (-1 = unknown) and how many of
+ * this process's CPUs lie on it (0 = the threads are not pinned). */
+aqz_status aqz_stage_host_affinity(const aqz_stage* st, int32_t* numa_node,
+                                   uint32_t* n_cpus);
+
 #ifdef __cplusplus
 }
 #endif
