@@ -339,11 +339,19 @@ aqz_status aqz_stage_device_layer(aqz_stage* st, uint32_t level,
  * ZarrCompressionSettings (zarr.types.h:112-122) as applied by
  * Chunk::compress_and_take_buffer (chunk.cpp:78-106) ->
  * zarr::compress_in_place (zarr.common.cpp:106-140) -> blosc_compress_ctx.
- * codec: ZarrCompressionCodec values; only AQZ_CODEC_BLOSC_LZ4 runs on the
- * device (others -> AQZ_STATUS_NOT_YET_IMPLEMENTED).  clevel 0 stores every
- * chunk as a memcpyed frame; levels 1-9 run the same GPU match finder.
- * Frames decode (any blosc1 decoder) to the chunk bytes exactly; their
- * compressed bytes differ from c-blosc's (block size, match finder). */
+ * codec: ZarrCompressionCodec values.
+ *  - AQZ_CODEC_BLOSC_LZ4: blosc1 frames made on the device (shuffle +
+ *    LZ4); clevel 0 stores every chunk as a memcpyed frame, levels 1-9 run
+ *    the same GPU match finder.
+ *  - AQZ_CODEC_BLOSC_ZSTD: the device shuffles every block, the layer goes
+ *    D2H and a host pool runs zstd per block (blosc clevel -> zstd level as
+ *    c-blosc maps it) into blosc1 frames.
+ *  - AQZ_CODEC_ZSTD: plain zstd frames of the chunk bytes at level clevel
+ *    (ZSTD_compress, zarr.common.cpp:142-166), on the host pool.
+ *  The zstd codecs need the system's libzstd.so.1 (loaded on first use;
+ *  absent -> AQZ_STATUS_NOT_YET_IMPLEMENTED).  Frames decode (any blosc1 /
+ *  zstd decoder) to the chunk bytes exactly; their compressed bytes differ
+ *  from c-blosc's (block size, match finder, no stream split for zstd). */
 #define AQZ_CODEC_NONE 0
 #define AQZ_CODEC_BLOSC_LZ4 1
 #define AQZ_CODEC_BLOSC_ZSTD 2
@@ -370,8 +378,10 @@ aqz_status aqz_stage_compress_layer(aqz_stage* st, uint32_t level, uint64_t laye
  * offsets[chunks_per_layer] = total bytes.  n >= chunks_per_layer + 1. */
 aqz_status aqz_stage_compressed_offsets(aqz_stage* st, uint32_t level,
                                         uint64_t layer, uint64_t* offsets, size_t n);
-/* Asynchronous copy of the layer's frames (total bytes) to dst (host or
- * device); complete after aqz_stage_wait_copies. */
+/* Copy of the layer's frames (total bytes) to dst.  blosc-lz4: dst host or
+ * device, asynchronous, complete after aqz_stage_wait_copies.  blosc-zstd /
+ * zstd (frames made on the host): dst is host memory, filled before the
+ * call returns. */
 aqz_status aqz_stage_copy_compressed_async(aqz_stage* st, uint32_t level,
                                            uint64_t layer, void* dst, size_t cap);
 
@@ -408,7 +418,7 @@ aqz_status aqz_shard_table(const uint64_t* offsets, const uint64_t* extents,
                            uint32_t chunks_per_shard, void* out, size_t cap);
 uint32_t aqz_crc32c(const void* data, size_t n);
 
-/* Stand-alone compressor for device-resident chunk arrays: chunk i of
+/* Stand-alone compressor (blosc-lz4 only) for device-resident chunk arrays: chunk i of
  * n_chunks at chunks + i * pitch, chunk_bytes each; frames back to back at
  * dst (device, >= aqz_compressor_max_bytes), offsets (device, n_chunks + 1
  * uint64) as above.  Enqueued on `stream` (hipStream_t; NULL = default). */
