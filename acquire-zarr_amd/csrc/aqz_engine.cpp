@@ -373,8 +373,31 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         hip_check(hipEventCreateWithFlags(&consume_ev_[j], hipEventDisableTiming),
                   "hipEventCreate");
     }
-    hip_check(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking), "hipStreamCreate");
-    hip_check(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking), "hipStreamCreate");
+    // HIP runs its streams on at most GPU_MAX_HW_QUEUES hardware queues (4 by
+    // default) per priority level; streams beyond that share a queue and then
+    // run in submission order.  With the default stream, the compute and the
+    // compression stream, the two PCIe streams made a fifth normal-priority
+    // stream: compression waited for every queued D2H piece (e2e trace: 41 ->
+    // 51 GB/s with 8 queues).  The PCIe streams take high priority, a queue
+    // pool of their own; their work is DMA and small blits, so priority costs
+    // the kernels nothing.  AQZ_COPY_PRIORITY=0 keeps them at normal priority (2: lowest).
+    {
+        const char* e = std::getenv("AQZ_COPY_PRIORITY");
+        int least = 0, greatest = 0;
+        hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest),
+                  "hipDeviceGetStreamPriorityRange");
+        const int mode = e ? std::atoi(e) : 1;
+        if (mode == 0) {
+            hip_check(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking), "hipStreamCreate");
+            hip_check(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking), "hipStreamCreate");
+        } else {
+            const int prio = mode == 2 ? least : greatest;
+            hip_check(hipStreamCreateWithPriority(&h2d_, hipStreamNonBlocking, prio),
+                      "hipStreamCreate");
+            hip_check(hipStreamCreateWithPriority(&d2h_, hipStreamNonBlocking, prio),
+                      "hipStreamCreate");
+        }
+    }
     hip_check(hipStreamCreateWithFlags(&comp_, hipStreamNonBlocking), "hipStreamCreate");
     for (auto& L : lv_) {
         hip_check(hipEventCreateWithFlags(&L.ops_ev, hipEventDisableTiming),
