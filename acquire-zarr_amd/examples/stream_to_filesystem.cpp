@@ -15,7 +15,8 @@
 // sink.cpp:47-100).  zarr.json metadata is not written (out of scope).
 //
 //   stream_to_filesystem OUT_DIR [--config c1|c2|c3] [--frames N]
-//       [--ring R] [--codec raw|lz4] [--shuffle 0|1|2] [--source pinned|pageable]
+//       [--ring R] [--codec raw|lz4|blosc-zstd|zstd] [--shuffle 0|1|2]
+//       [--source pinned|pageable]
 //       [--seed S] [--writers K] [--pattern random|camera] [--no-write]
 //
 // Frames are a splitmix64 byte stream (seed S; the same stream as the test
@@ -231,7 +232,7 @@ main(int argc, char** argv)
 {
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s OUT_DIR [--config c1|c2|c3] [--frames N] [--ring R] "
-                             "[--codec raw|lz4] [--shuffle 0|1|2] "
+                             "[--codec raw|lz4|blosc-zstd|zstd] [--shuffle 0|1|2] "
                              "[--source pinned|pageable] [--seed S] [--writers K] "
                              "[--no-write]\n",
                      argv[0]);
@@ -292,7 +293,16 @@ main(int argc, char** argv)
     } else {
         die("unknown config");
     }
-    const bool compress = codec == "lz4";
+    int32_t codec_id = AQZ_CODEC_NONE;
+    if (codec == "lz4")
+        codec_id = AQZ_CODEC_BLOSC_LZ4;
+    else if (codec == "blosc-zstd")
+        codec_id = AQZ_CODEC_BLOSC_ZSTD;
+    else if (codec == "zstd")
+        codec_id = AQZ_CODEC_ZSTD;
+    else if (codec != "raw")
+        die("unknown codec");
+    const bool compress = codec_id != AQZ_CODEC_NONE;
     aqz_array_desc desc{ dims.data(), dims.size(), dtype, 1, AQZ_METHOD_MEAN, 0, nullptr, 0 };
     // this writer emits sharded Zarr v3 arrays only (every dimension has a
     // shard size); an unsharded array stores each chunk as its own file with
@@ -360,7 +370,10 @@ main(int argc, char** argv)
         bufs[l] = std::vector<Buffer>(kBufs);
         const size_t layer_bytes = lv[l].lay.bytes_per_chunk * lv[l].lay.chunks_per_layer;
         for (Buffer& b : bufs[l]) {
-            b.cap = layer_bytes + 64 * size_t(lv[l].lay.chunks_per_layer) + 4096;
+            // + per-chunk frame overhead (blosc header + block table, or a
+            // zstd frame's block headers: < 0.5% of the chunk)
+            b.cap = layer_bytes + layer_bytes / 128 +
+                    (64 + 1024) * size_t(lv[l].lay.chunks_per_layer) + 4096;
             check(aqz_host_alloc(b.cap, reinterpret_cast<void**>(&b.p)), "aqz_host_alloc");
             check(aqz_host_alloc(lv[l].lay.chunks_per_layer, reinterpret_cast<void**>(&b.has)),
                   "aqz_host_alloc");
@@ -461,7 +474,9 @@ main(int argc, char** argv)
             std::this_thread::sleep_for(std::chrono::microseconds(50));
         return b;
     };
-    const aqz_compression comp{ AQZ_CODEC_BLOSC_LZ4, 5, shuffle };
+    // blosc codecs at clevel 5, plain zstd at level 3 (the settings' levels)
+    const aqz_compression comp{ codec_id, codec_id == AQZ_CODEC_ZSTD ? 3 : 5,
+                                codec_id == AQZ_CODEC_ZSTD ? 0 : shuffle };
 
     // completed layers of every level -> compression or raw D2H
     auto hand_off = [&](bool final) {
@@ -575,7 +590,11 @@ main(int argc, char** argv)
                 "\"source\": \"%s\", \"codec\": \"%s\", \"shuffle\": %d, "
                 "\"bytes_to_sink\": %llu, \"sink_bytes_per_input_byte\": %.4f, "
                 "\"writers\": %d, \"write\": %s, \"pattern\": \"%s\"}\n",
-                compress ? "device blosc-lz4" : "raw chunks", in_bytes / el / 1e9,
+                codec_id == AQZ_CODEC_BLOSC_LZ4    ? "device blosc-lz4"
+                : codec_id == AQZ_CODEC_BLOSC_ZSTD ? "blosc-zstd"
+                : codec_id == AQZ_CODEC_ZSTD       ? "zstd"
+                                                   : "raw chunks",
+                in_bytes / el / 1e9,
                 static_cast<unsigned long long>(n_frames), el, nl, config.c_str(),
                 source.c_str(), codec.c_str(), shuffle,
                 static_cast<unsigned long long>(bytes_written.load()),

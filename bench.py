@@ -24,6 +24,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "acquire-zarr_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# probed ceiling of the pyramid-only access shape (each input byte read once
+# with nt loads, 1/3 of it written): tools/copy_probe.hip MODE 3,
+# profiles/r02_copy_probe.txt "read+1/3w ntl" -- 5105 GB/s read, 6807 GB/s bus
+PYR_PROBE_READ_GBS = 5105.0
 
 SPACE, CHANNEL, TIME = 0, 1, 2
 U8, U16, F32 = 0, 1, 8
@@ -619,7 +623,12 @@ def main():
             "value": round(side["value"], 2), "unit": "GB/s",
             "kernel_avg_ms": round(side["avg_ms"], 5),
             "achieved": round(side["achieved"], 1),
-            "input_rate_frac_of_peak": round(side["value"] / world / HBM_PEAK_GBS, 4)}
+            "input_rate_frac_of_peak": round(side["value"] / world / HBM_PEAK_GBS, 4),
+            # the same shape's probed ceiling on a plain streaming kernel
+            "probed_ceiling_input_gbs": PYR_PROBE_READ_GBS,
+            "input_rate_frac_of_probed_ceiling": round(
+                side["value"] / world / PYR_PROBE_READ_GBS, 4),
+            "probed_ceiling_source": "profiles/r02_copy_probe.txt read+1/3w ntl"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:

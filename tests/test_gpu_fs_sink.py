@@ -14,7 +14,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from codec_helpers import crc32c, oracle_decode
+from codec_helpers import blosc_zstd_decode, crc32c, libzstd, oracle_decode, zstd_decode
 from helpers import expected_stage_layers
 from oracle_bindings import MEAN, SPACE, TIME, U16, OracleDims, OracleDownsampler, \
     synthetic_frames
@@ -46,9 +46,13 @@ def shards_along(level_dims):
 
 
 @pytest.mark.parametrize("codec,shuffle,source", [("lz4", 2, "pinned"), ("lz4", 1, "pageable"),
-                                                  ("raw", 0, "pinned")])
+                                                  ("raw", 0, "pinned"),
+                                                  ("blosc-zstd", 1, "pinned"),
+                                                  ("zstd", 0, "pinned")])
 def test_stream_to_filesystem_shards(gpu, tmp_path, codec, shuffle, source):
     assert os.path.exists(EXE), "build acquire-zarr_amd (make) first"
+    if "zstd" in codec and libzstd() is None:
+        pytest.skip("libzstd.so.1 absent")
     n, seed = 100, 31  # one full t-chunk layer + a partial one
     out = tmp_path / "store"
     r = subprocess.run([EXE, str(out), "--config", "c1", "--frames", str(n), "--ring", str(n),
@@ -94,7 +98,12 @@ def test_stream_to_filesystem_shards(gpu, tmp_path, codec, shuffle, source):
                         assert off == UNWRITTEN and ext == UNWRITTEN, (level, row, s, i)
                         continue
                     got = blob[off:off + ext]
-                    got = oracle_decode(got) if codec == "lz4" else got
+                    if codec == "lz4":
+                        got = oracle_decode(got)
+                    elif codec == "blosc-zstd":
+                        got = blosc_zstd_decode(got)
+                    elif codec == "zstd":
+                        got = zstd_decode(got, bpc)
                     assert got == w, (level, row, s, i)
                     checked += 1
     assert checked > 0
