@@ -13,6 +13,8 @@
 // compressed bytes differ while every decoded byte is identical.
 #pragma once
 
+#include "aqz_zstd.hh"
+
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -91,5 +93,76 @@ struct ShuffleParams
     uint8_t* out;
 };
 hipError_t launch_shuffle_blocks(const ShuffleParams& p, hipStream_t stream);
+
+} // namespace aqz
+
+namespace aqz {
+
+// Device zstd (aqz_zstd.hh for the format pieces): blosc1 frames with the
+// zstd codec (one zstd frame per blosc block, "don't split") or plain zstd
+// frames (one per chunk), for a whole resident chunk layer.  A segment is
+// what one zstd frame holds (a blosc block, or a chunk); it is cut into
+// zstd blocks of zstd::kBlock bytes, the parallel unit.
+struct ZstdSegTable
+{
+    uint32_t mode;   // 0 raw literals, 1 one symbol, 2 Huffman
+    uint32_t tree_n; // bytes of the tree description
+    uint32_t pad[2];
+    uint16_t code[256];
+    uint8_t len[256];
+    uint8_t tree[160];
+};
+
+struct ZstdParams
+{
+    const uint8_t* src;     // segment data: chunk c at src + c * src_pitch
+    uint64_t src_pitch;
+    const uint8_t* chunks;  // the unshuffled chunks (memcpyed blosc frames)
+    uint64_t pitch;
+    uint32_t n_chunks, nbytes, typesize, shuffle;
+    uint32_t blosc;         // 1 blosc-zstd frames, 0 plain zstd frames
+    uint32_t seg_bytes;     // bytes per segment (blosc block size or nbytes)
+    uint32_t nseg;          // segments per chunk
+    uint32_t bps;           // zstd block slots per segment
+    uint32_t store_only;    // blosc clevel 0: every frame memcpyed
+    uint32_t match;         // 1: LZ sequences (zstd_parse); 0: literals only
+    const uint32_t* flags;  // has_data words (nullptr: every chunk has data)
+    uint32_t tag;
+    const zstd::SeqTables* seqt; // predefined sequence tables (device)
+    // per parse unit (kZSubBlocks per zstd block, kZSub bytes each)
+    uint8_t* lits;          // literal bytes, kZSub per unit
+    uint64_t* seqs;         // kZSubSeq packed sequences per unit
+    uint32_t* snseq, *snlit, *stail;
+    // per zstd block ([n_chunks * nseg * bps])
+    uint32_t* hist;         // [.. * 256] literal histogram
+    uint8_t* bkind;         // 0 raw, 1 RLE, 2 compressed, 3 none
+    uint8_t* bltype;        // compressed: literals 0 raw, 2 Huffman
+    uint32_t* bpay;         // compressed: literal payload bytes; RLE: the byte
+    uint32_t* bseqb;        // compressed: sequences section bytes
+    uint32_t* bnlit;        // literals of the block
+    uint32_t* bpos;         // block offset after the frame header
+    uint8_t* scratch;       // [literal payload][sequences section], zstd::kBlock each
+    // per segment ([n_chunks * nseg])
+    ZstdSegTable* tab;
+    uint32_t* carrier;      // block carrying the tree (~0: none)
+    uint32_t* ssize;        // record bytes (zstd frame, or the raw block)
+    uint8_t* sraw;          // 1: record stored raw (blosc)
+    uint32_t* spos;         // record offset inside the chunk frame (blosc)
+    // per chunk
+    uint32_t* fsize;
+    uint8_t* mode;          // 1: memcpyed blosc frame
+    const uint32_t* order;
+    uint64_t* offsets;
+    uint64_t* cstart;
+    uint8_t* out;
+};
+
+// parse units of a zstd block: 4 KiB, one wave each (LDS-resident, as the
+// LZ4 encoder's streams), at most kZSubSeq sequences each
+constexpr uint32_t kZSub = 4096;
+constexpr uint32_t kZSubBlocks = zstd::kBlock / kZSub;
+constexpr uint32_t kZSubSeq = 256;
+
+hipError_t launch_zstd(const ZstdParams& p, hipStream_t stream);
 
 } // namespace aqz

@@ -16,6 +16,7 @@
 //   write_frames        header, block starts and stream records, back to
 //                       back in chunk order
 #include "aqz_codec.hh"
+#include "aqz_zstd.hh"
 
 namespace aqz {
 
@@ -678,6 +679,686 @@ shuffle_blocks(const ShuffleParams p)
         dst[x] = src[x];
 }
 
+
+// ---- device zstd (aqz_codec.hh ZstdParams; format pieces in aqz_zstd.hh) ----
+//   zstd_parse   per 4 KiB unit, one wave (match mode): greedy LZ parse with
+//                the LZ4 encoder's window probing (4 x 64 positions hashed
+//                per batch against an LDS table, ballot, scalar walk), a
+//                minimum match length from the unit's byte entropy; packed
+//                sequences and the literal bytes go to the unit's slots, the
+//                literal histogram to its block
+//   zstd_hist    per zstd block (literals-only mode): byte histogram
+//   zstd_table   per segment (one zstd frame): Huffman code of the frame's
+//                literals and its tree description
+//   zstd_encode  per zstd block: RLE when one byte value; the 4 Huffman
+//                streams, one wave each (lane-parallel bit packing: each lane
+//                owns a run of literals, a suffix scan of their bit counts
+//                places it -- a stream is written last literal first); the
+//                sequences bitstream (one lane, backwards); compressed iff
+//                smaller than the block counted with the tree
+//   zstd_segment per segment: which block carries the tree, block offsets,
+//                frame bytes; a blosc record larger than its block is raw
+//   zstd_chunk   per chunk: blosc record offsets / memcpyed rule, frame bytes
+//   zstd_write   per zstd block: headers, tree, payload or raw bytes
+constexpr uint32_t kZMinHuf = 64; // fewer literals: raw (as the host model)
+constexpr uint32_t kZStreamWords = (zstd::kBlock / 4 * zstd::kHufMaxBits) / 32 + 2;
+
+struct ZBlock
+{
+    uint32_t c, j, b, seg, len, seglen, nb;
+};
+
+__device__ __forceinline__ ZBlock
+zblock(const ZstdParams& p, uint32_t g)
+{
+    ZBlock z;
+    z.b = g % p.bps;
+    z.seg = g / p.bps;
+    z.c = z.seg / p.nseg;
+    z.j = z.seg - z.c * p.nseg;
+    const uint64_t s0 = uint64_t(z.j) * p.seg_bytes;
+    z.seglen = uint32_t(min(uint64_t(p.seg_bytes), uint64_t(p.nbytes) - s0));
+    z.nb = (z.seglen + zstd::kBlock - 1) / zstd::kBlock;
+    const uint32_t o = z.b * zstd::kBlock;
+    z.len = o < z.seglen ? min(zstd::kBlock, z.seglen - o) : 0;
+    return z;
+}
+
+__device__ __forceinline__ const uint8_t*
+zblock_src(const ZstdParams& p, const ZBlock& z)
+{
+    return p.src + z.c * p.src_pitch + uint64_t(z.j) * p.seg_bytes + uint64_t(z.b) * zstd::kBlock;
+}
+
+__device__ __forceinline__ bool
+zchunk_skip(const ZstdParams& p, uint32_t c)
+{
+    return p.flags && p.flags[c] != p.tag;
+}
+
+__global__ __launch_bounds__(64) void
+zstd_parse(const ZstdParams p)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t sw[kZSub / 4 + 4];
+    __shared__ uint16_t table[kHashSize];
+    __shared__ uint32_t lh[256];
+    __shared__ uint64_t sseq[kZSubSeq];
+    const uint32_t q = blockIdx.x, g = q / kZSubBlocks, k = q - g * kZSubBlocks;
+    const uint32_t lane = threadIdx.x;
+    const ZBlock z = zblock(p, g);
+    const uint32_t so = k * kZSub;
+    const uint32_t L = so < z.len ? min(kZSub, z.len - so) : 0;
+    if (L == 0 || zchunk_skip(p, z.c)) {
+        if (lane == 0) {
+            p.snseq[q] = 0;
+            p.snlit[q] = 0;
+            p.stail[q] = 0;
+        }
+        return;
+    }
+    const uint8_t* src = zblock_src(p, z) + so;
+    uint8_t* sb = reinterpret_cast<uint8_t*>(sw);
+    if ((reinterpret_cast<uintptr_t>(src) & 3u) == 0) {
+        const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
+        for (uint32_t w = lane; w < L / 4; w += 64)
+            sw[w] = s4[w];
+        for (uint32_t i = (L & ~3u) + lane; i < L; i += 64)
+            sb[i] = src[i];
+    } else {
+        for (uint32_t i = lane; i < L; i += 64)
+            sb[i] = src[i];
+    }
+    for (uint32_t i = L + lane; i < L + 8; i += 64)
+        sb[i] = 0;
+    for (uint32_t b = lane; b < 256; b += 64)
+        lh[b] = 0;
+    for (uint32_t i = lane; i < kHashSize / 2; i += 64)
+        reinterpret_cast<uint32_t*>(table)[i] = 0;
+    __syncthreads();
+    for (uint32_t i = lane; i < L; i += 64)
+        atomicAdd(&lh[sb[i]], 1u);
+    __syncthreads();
+    float e = 0.f;
+    for (uint32_t b = lane; b < 256; b += 64)
+        if (lh[b]) {
+            const float pr = float(lh[b]) / float(L);
+            e -= pr * __log2f(pr);
+        }
+    for (int d = 32; d > 0; d >>= 1)
+        e += __shfl_xor(e, d);
+    const uint32_t minlen = zstd::min_match(e, kLenCap);
+    __syncthreads();
+    for (uint32_t b = lane; b < 256; b += 64)
+        lh[b] = 0;
+    __syncthreads();
+
+    // greedy parse: probe four 64-position windows, walk the matches
+    uint32_t nseq = 0, anchor = 0, p0 = 0, misses = 0;
+    bool full = false;
+    if (L >= 8) {
+        const uint32_t mflimit = L - 4; // last position a match may start
+        const uint32_t matchlimit = L;  // a match ends at or before here
+        for (uint32_t base = 0; base <= mflimit && !full;) {
+            uint32_t cand[kWin], mlen[kWin];
+            uint64_t M[kWin];
+#pragma unroll
+            for (uint32_t w = 0; w < kWin; ++w) {
+                const uint32_t qq = base + 64 * w + lane;
+                cand[w] = 0;
+                mlen[w] = 0;
+                if (qq <= mflimit) {
+                    const uint32_t v = lds_rd32(sw, qq);
+                    const uint32_t h = (v * 2654435761u) >> (32 - kLz4HashLog);
+                    const uint32_t en = table[h];
+                    table[h] = uint16_t(qq + 1);
+                    uint32_t c = ~0u;
+                    if (en != 0 && lds_rd32(sw, en - 1) == v)
+                        c = en - 1;
+                    else if (qq > 0 && lds_rd32(sw, qq - 1) == v)
+                        c = qq - 1;
+                    if (c != ~0u) {
+                        const uint32_t lim = min(matchlimit - qq, kLenCap);
+                        uint32_t len = 4;
+                        bool done = false;
+                        while (len + 4 <= lim) {
+                            const uint32_t x = lds_rd32(sw, qq + len) ^ lds_rd32(sw, c + len);
+                            if (x) {
+                                len += uint32_t(__builtin_ctz(x)) >> 3;
+                                done = true;
+                                break;
+                            }
+                            len += 4;
+                        }
+                        if (!done)
+                            while (len < lim && sb[qq + len] == sb[c + len])
+                                ++len;
+                        if (len >= minlen) {
+                            cand[w] = c;
+                            mlen[w] = len;
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (uint32_t w = 0; w < kWin; ++w)
+                M[w] = __ballot(mlen[w] != 0);
+            bool any = false;
+#pragma unroll
+            for (uint32_t w = 0; w < kWin; ++w) {
+                const uint32_t wb = base + 64 * w;
+                while (p0 < wb + 64 && !full) {
+                    const uint32_t sh = p0 > wb ? p0 - wb : 0;
+                    const uint64_t mm = M[w] & (~0ull << sh);
+                    if (mm == 0)
+                        break;
+                    const uint32_t i = uint32_t(__ffsll(static_cast<long long>(mm))) - 1;
+                    const uint32_t qq = wb + i;
+                    const uint32_t cc = rdlane(cand[w], i);
+                    uint32_t len = rdlane(mlen[w], i);
+                    if (len == kLenCap) {
+                        for (;;) {
+                            const uint32_t a = qq + len + lane;
+                            const bool eq = a < matchlimit && sb[a] == sb[cc + len + lane];
+                            const uint64_t miss = __ballot(!eq);
+                            if (miss == 0) {
+                                len += 64;
+                                continue;
+                            }
+                            len += uint32_t(__ffsll(static_cast<long long>(miss))) - 1;
+                            break;
+                        }
+                    }
+                    if (lane == 0)
+                        sseq[nseq] = zstd::pack_seq(qq - anchor, len, qq - cc);
+                    ++nseq;
+                    full = nseq == kZSubSeq;
+                    p0 = qq + len;
+                    anchor = p0;
+                    any = true;
+                }
+            }
+            misses = any ? 0 : misses + 1;
+            const uint32_t skip = misses > 1 ? (misses - 1) * 64 * kWin : 0;
+            base = max(base + 64 * kWin + skip, p0 & ~63u);
+        }
+    }
+    __syncthreads();
+    // literal runs -> the unit's literal slot, and their histogram
+    uint8_t* lo = p.lits + uint64_t(q) * kZSub;
+    uint32_t at = 0, pos = 0;
+    for (uint32_t s = 0; s < nseq; ++s) {
+        const zstd::Seq v = zstd::unpack_seq(sseq[s]);
+        for (uint32_t i = lane; i < v.lit; i += 64) {
+            const uint8_t x = sb[pos + i];
+            lo[at + i] = x;
+            atomicAdd(&lh[x], 1u);
+        }
+        at += v.lit;
+        pos += v.lit + v.len;
+    }
+    const uint32_t tail = L - pos;
+    for (uint32_t i = lane; i < tail; i += 64) {
+        const uint8_t x = sb[pos + i];
+        lo[at + i] = x;
+        atomicAdd(&lh[x], 1u);
+    }
+    at += tail;
+    uint64_t* so_ = p.seqs + uint64_t(q) * kZSubSeq;
+    for (uint32_t s = lane; s < nseq; s += 64)
+        so_[s] = sseq[s];
+    __syncthreads();
+    for (uint32_t b = lane; b < 256; b += 64)
+        if (lh[b])
+            atomicAdd(&p.hist[uint64_t(g) * 256 + b], lh[b]);
+    if (lane == 0) {
+        p.snseq[q] = nseq;
+        p.snlit[q] = at;
+        p.stail[q] = tail;
+    }
+}
+
+__global__ __launch_bounds__(256) void
+zstd_hist(const ZstdParams p)
+{
+    __shared__ uint32_t h[4][256];
+    const uint32_t g = blockIdx.x, t = threadIdx.x, w = t >> 6;
+    const ZBlock z = zblock(p, g);
+    const bool skip = z.len == 0 || zchunk_skip(p, z.c);
+    for (uint32_t k = 0; k < 4; ++k)
+        h[k][t] = 0;
+    __syncthreads();
+    if (!skip) {
+        const uint8_t* s = zblock_src(p, z);
+        uint32_t done = 0;
+        if ((reinterpret_cast<uintptr_t>(s) & 3u) == 0) {
+            const uint32_t* sw = reinterpret_cast<const uint32_t*>(s);
+            for (uint32_t i = t; i < z.len / 4; i += 256) {
+                const uint32_t v = sw[i];
+                atomicAdd(&h[w][v & 255u], 1u);
+                atomicAdd(&h[w][(v >> 8) & 255u], 1u);
+                atomicAdd(&h[w][(v >> 16) & 255u], 1u);
+                atomicAdd(&h[w][v >> 24], 1u);
+            }
+            done = z.len & ~3u;
+        }
+        for (uint32_t i = done + t; i < z.len; i += 256)
+            atomicAdd(&h[w][s[i]], 1u);
+    }
+    __syncthreads();
+    p.hist[uint64_t(g) * 256 + t] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
+}
+
+__global__ __launch_bounds__(64) void
+zstd_table(const ZstdParams p)
+{
+    __shared__ zstd::HufWork w;
+    __shared__ uint64_t key[256];
+    __shared__ uint8_t len[256];
+    __shared__ uint32_t npresent;
+    const uint32_t s = blockIdx.x, t = threadIdx.x;
+    if (zchunk_skip(p, s / p.nseg))
+        return;
+    if (t == 0)
+        npresent = 0;
+    __syncthreads();
+    for (uint32_t k = t; k < 256; k += 64) {
+        uint32_t a = 0;
+        for (uint32_t b = 0; b < p.bps; ++b)
+            a += p.hist[(uint64_t(s) * p.bps + b) * 256 + k];
+        w.cnt[k] = a;
+        key[k] = uint64_t(a) << 8 | k;
+        len[k] = 0;
+        if (a)
+            atomicAdd(&npresent, 1u);
+    }
+    __syncthreads();
+    // bitonic sort of (count, symbol), 64 lanes x 2 pairs
+    for (uint32_t size = 2; size <= 256; size <<= 1)
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            for (uint32_t q = t; q < 128; q += 64) {
+                const uint32_t i = 2 * q - (q & (stride - 1));
+                const uint32_t j = i + stride;
+                const bool up = (i & size) == 0;
+                const uint64_t a = key[i], b = key[j];
+                if ((a > b) == up) {
+                    key[i] = b;
+                    key[j] = a;
+                }
+            }
+            __syncthreads();
+        }
+    const uint32_t n = npresent;
+    for (uint32_t k = t; k < n; k += 64)
+        w.sorted[k] = uint16_t(key[256 - n + k] & 255u);
+    __syncthreads();
+    if (t != 0)
+        return;
+    ZstdSegTable& T = p.tab[s];
+    T.mode = n == 1 ? 1 : 0;
+    T.tree_n = 0;
+    if (n >= 2) {
+        zstd::huf_lengths_sorted(w, n, len, zstd::kHufMaxBits);
+        uint16_t code[256];
+        const uint32_t mb = zstd::huf_codes(len, code);
+        uint8_t tree[160];
+        T.tree_n = zstd::huf_write_tree(len, mb, tree);
+        T.mode = T.tree_n ? 2 : 0;
+        for (uint32_t k = 0; k < 256; ++k) {
+            T.code[k] = code[k];
+            T.len[k] = len[k];
+        }
+        for (uint32_t k = 0; k < T.tree_n; ++k)
+            T.tree[k] = tree[k];
+    }
+}
+
+// literal i of block g: the block's bytes (literals only) or the parse
+// units' literal slots (pre = literal prefix of the units)
+struct ZLits
+{
+    const uint8_t* base; // block bytes, or the block's first unit slot
+    const uint32_t* pre; // [kZSubBlocks + 1] or nullptr
+    __device__ __forceinline__ uint8_t operator()(uint32_t i) const
+    {
+        if (!pre)
+            return base[i];
+        uint32_t k = 0;
+        while (k + 1 < kZSubBlocks && pre[k + 1] <= i)
+            ++k;
+        return base[uint64_t(k) * kZSub + (i - pre[k])];
+    }
+};
+
+__global__ __launch_bounds__(256) void
+zstd_encode(const ZstdParams p)
+{
+    __shared__ uint32_t buf[4][kZStreamWords];
+    __shared__ uint16_t code[256];
+    __shared__ uint8_t clen[256];
+    __shared__ int32_t rle;
+    __shared__ uint32_t ssz[4];
+    __shared__ uint32_t pre[kZSubBlocks + 1], spre[kZSubBlocks + 1], carry[kZSubBlocks];
+    __shared__ uint32_t dec[4]; // kind, literal type, literal payload, sequence bytes
+    const uint32_t g = blockIdx.x, t = threadIdx.x;
+    const ZBlock z = zblock(p, g);
+    if (z.len == 0 || zchunk_skip(p, z.c)) {
+        if (t == 0)
+            p.bkind[g] = 3;
+        return;
+    }
+    if (t == 0) {
+        rle = -1;
+        pre[0] = 0;
+        spre[0] = 0;
+        if (p.match) {
+            const uint64_t u0 = uint64_t(g) * kZSubBlocks;
+            uint32_t cr = 0;
+            for (uint32_t k = 0; k < kZSubBlocks; ++k) {
+                pre[k + 1] = pre[k] + p.snlit[u0 + k];
+                spre[k + 1] = spre[k] + p.snseq[u0 + k];
+                carry[k] = cr;
+                cr = p.snseq[u0 + k] ? p.stail[u0 + k] : cr + p.snlit[u0 + k];
+            }
+        } else {
+            for (uint32_t k = 0; k < kZSubBlocks; ++k) {
+                pre[k + 1] = z.len;
+                spre[k + 1] = 0;
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t nl = pre[kZSubBlocks], nseq = spre[kZSubBlocks];
+    if (nl > 0 && p.hist[uint64_t(g) * 256 + t] == nl)
+        rle = int32_t(t); // one literal value: every byte of the block is it
+    __syncthreads();
+    if (rle >= 0) {
+        if (t == 0) {
+            p.bkind[g] = 1;
+            p.bpay[g] = uint32_t(rle);
+        }
+        return;
+    }
+    const ZstdSegTable& T = p.tab[z.seg];
+    const ZLits lit{ p.match ? p.lits + uint64_t(g) * kZSubBlocks * kZSub : zblock_src(p, z),
+                     p.match ? pre : nullptr };
+    const bool try_huf = T.mode == 2 && nl >= kZMinHuf;
+    if (try_huf) {
+        code[t] = T.code[t];
+        clen[t] = T.len[t];
+        for (uint32_t i = t; i < 4 * kZStreamWords; i += 256)
+            (&buf[0][0])[i] = 0;
+    }
+    __syncthreads();
+    if (try_huf) {
+        const uint32_t w = t >> 6, lane = t & 63u;
+        const uint32_t seg4 = zstd::lit_segment(nl);
+        const uint32_t a = min(nl, w * seg4), e = min(nl, (w + 1) * seg4);
+        const uint32_t slen = e - a, per = (slen + 63) / 64;
+        const uint32_t la = a + min(slen, lane * per), le = a + min(slen, (lane + 1) * per);
+        uint32_t bits = 0;
+        for (uint32_t i = la; i < le; ++i)
+            bits += clen[lit(i)];
+        // bits of the lanes above: the stream is written last literal first
+        uint32_t x = bits;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_down(x, d);
+            if (lane + uint32_t(d) < 64)
+                x += y;
+        }
+        const uint32_t total = __shfl(x, 0);
+        uint32_t pos = x - bits;
+        uint32_t* sb = buf[w];
+        for (uint32_t i = le; i-- > la;) {
+            const uint8_t sym = lit(i);
+            const uint32_t v = code[sym], n = clen[sym];
+            const uint32_t o = pos & 31u;
+            atomicOr(&sb[pos >> 5], v << o);
+            if (o + n > 32)
+                atomicOr(&sb[(pos >> 5) + 1], v >> (32 - o));
+            pos += n;
+        }
+        if (lane == 0) {
+            atomicOr(&sb[total >> 5], 1u << (total & 31u)); // end mark
+            ssz[w] = total / 8 + 1;
+        }
+    }
+    __syncthreads();
+    uint8_t* d = p.scratch + uint64_t(g) * zstd::kBlock;
+    if (t == 0) {
+        // literals: Huffman when it beats raw counted with the tree
+        uint32_t ltype = 0, lpay = nl, lsec = zstd::lit_header_raw_bytes(nl) + nl;
+        if (try_huf) {
+            const uint32_t pay = 6 + ssz[0] + ssz[1] + ssz[2] + ssz[3];
+            const uint32_t wt = T.tree_n + pay;
+            const uint32_t hs = zstd::lit_header_huf_bytes(nl, wt) + wt;
+            if (hs < lsec) {
+                ltype = 2;
+                lpay = pay;
+                lsec = hs;
+            }
+        }
+        // sequences section after the literal payload
+        uint32_t sq = 0;
+        if (lpay < zstd::kBlock) {
+            uint8_t* o = d + lpay;
+            const uint32_t cap = zstd::kBlock - lpay;
+            if (cap >= 4) {
+                sq = zstd::write_seq_header(o, nseq);
+                if (nseq) {
+                    const uint64_t* sv = p.seqs + uint64_t(g) * kZSubBlocks * kZSubSeq;
+                    const uint32_t bits = zstd::encode_sequences(
+                      *p.seqt,
+                      [&](uint32_t i) {
+                          uint32_t k = 0;
+                          while (k + 1 < kZSubBlocks && spre[k + 1] <= i)
+                              ++k;
+                          zstd::Seq v =
+                            zstd::unpack_seq(sv[uint64_t(k) * kZSubSeq + (i - spre[k])]);
+                          if (i == spre[k])
+                              v.lit += carry[k];
+                          return v;
+                      },
+                      nseq, o + sq, cap - sq);
+                    sq = bits ? sq + bits : 0;
+                }
+            }
+        }
+        const bool ok = sq != 0 && lsec + sq < z.len;
+        dec[0] = ok ? 2 : 0;
+        dec[1] = ltype;
+        dec[2] = lpay;
+        dec[3] = sq;
+    }
+    __syncthreads();
+    if (dec[0] != 2) {
+        if (t == 0)
+            p.bkind[g] = 0;
+        return;
+    }
+    const uint32_t lpay = dec[2];
+    if (dec[1] == 2) {
+        if (t == 0) {
+            zstd::put_le(d, ssz[0], 2);
+            zstd::put_le(d + 2, ssz[1], 2);
+            zstd::put_le(d + 4, ssz[2], 2);
+        }
+        uint32_t at = 6;
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint8_t* sbk = reinterpret_cast<const uint8_t*>(buf[k]);
+            for (uint32_t i = t; i < ssz[k]; i += 256)
+                d[at + i] = sbk[i];
+            at += ssz[k];
+        }
+    } else {
+        for (uint32_t i = t; i < nl; i += 256)
+            d[i] = lit(i);
+    }
+    if (t == 0) {
+        p.bkind[g] = 2;
+        p.bltype[g] = uint8_t(dec[1]);
+        p.bpay[g] = lpay;
+        p.bseqb[g] = dec[3];
+        p.bnlit[g] = nl;
+    }
+}
+
+__global__ __launch_bounds__(64) void
+zstd_segment(const ZstdParams p)
+{
+    const uint32_t s = blockIdx.x;
+    if (threadIdx.x != 0)
+        return;
+    if (zchunk_skip(p, s / p.nseg)) {
+        p.ssize[s] = 0;
+        return;
+    }
+    const ZBlock z0 = zblock(p, s * p.bps);
+    const uint32_t tree_n = p.tab[s].tree_n;
+    uint32_t carrier = ~0u, pos = 0;
+    for (uint32_t b = 0; b < z0.nb; ++b) {
+        const uint32_t g = s * p.bps + b;
+        const uint32_t blen = min(zstd::kBlock, z0.seglen - b * zstd::kBlock);
+        const uint32_t k = p.bkind[g];
+        uint32_t sz = 0;
+        if (k == 0) {
+            sz = 3 + blen;
+        } else if (k == 1) {
+            sz = 4;
+        } else if (k == 2) {
+            const uint32_t nl = p.bnlit[g];
+            if (p.bltype[g] == 2) {
+                if (carrier == ~0u)
+                    carrier = b;
+                const uint32_t cs = p.bpay[g] + (carrier == b ? tree_n : 0);
+                sz = 3 + zstd::lit_header_huf_bytes(nl, cs) + cs + p.bseqb[g];
+            } else {
+                sz = 3 + zstd::lit_header_raw_bytes(nl) + nl + p.bseqb[g];
+            }
+        }
+        p.bpos[g] = pos;
+        pos += sz;
+    }
+    p.carrier[s] = carrier;
+    const uint32_t frame = zstd::frame_header_bytes(z0.seglen) + pos;
+    const bool raw = p.blosc && frame >= z0.seglen;
+    p.sraw[s] = raw ? 1 : 0;
+    p.ssize[s] = raw ? z0.seglen : frame;
+}
+
+__global__ __launch_bounds__(256) void
+zstd_chunk(const ZstdParams p)
+{
+    const uint32_t c = blockIdx.x;
+    const bool skip = zchunk_skip(p, c);
+    if (!p.blosc) {
+        if (threadIdx.x == 0) {
+            p.fsize[c] = skip ? 0 : p.ssize[c];
+            p.mode[c] = 0;
+        }
+        return;
+    }
+    const uint32_t hdr = 16 + 4 * p.nseg;
+    uint32_t carry = hdr;
+    if (!p.store_only)
+        for (uint32_t j0 = 0; j0 < p.nseg; j0 += 256) {
+            const uint32_t j = j0 + threadIdx.x;
+            const uint32_t rec = j < p.nseg ? 4 + p.ssize[uint64_t(c) * p.nseg + j] : 0;
+            uint32_t tot;
+            const uint32_t pre = block_scan256(rec, &tot);
+            if (j < p.nseg)
+                p.spos[uint64_t(c) * p.nseg + j] = carry + pre;
+            carry += tot;
+        }
+    if (threadIdx.x == 0) {
+        const bool memcpyed = p.store_only || uint64_t(carry) > uint64_t(p.nbytes) + 16;
+        p.fsize[c] = skip ? 0 : (memcpyed ? p.nbytes + 16 : carry);
+        p.mode[c] = memcpyed ? 1 : 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void
+zstd_write(const ZstdParams p)
+{
+    const uint32_t g = blockIdx.x, t = threadIdx.x;
+    const ZBlock z = zblock(p, g);
+    const uint32_t fs = p.fsize[z.c];
+    if (fs == 0 || z.len == 0)
+        return;
+    uint8_t* o = p.out + p.cstart[z.c];
+    uint8_t* fr = o;
+    if (p.blosc) {
+        const bool memcpyed = p.mode[z.c] != 0;
+        if (z.j == 0 && z.b == 0 && t == 0) {
+            o[0] = 2; // BLOSC_VERSION_FORMAT
+            o[1] = 1; // BLOSC_ZSTD_VERSION_FORMAT
+            o[2] = uint8_t(4u << 5 | 0x10u | (p.shuffle == 1 ? 0x1u : 0u) |
+                           (p.shuffle == 2 ? 0x4u : 0u) | (memcpyed ? 0x2u : 0u));
+            o[3] = uint8_t(p.typesize);
+            put32(o + 4, p.nbytes);
+            put32(o + 8, p.seg_bytes);
+            put32(o + 12, fs);
+        }
+        const uint64_t off = uint64_t(z.j) * p.seg_bytes + uint64_t(z.b) * zstd::kBlock;
+        if (memcpyed) {
+            copy_bytes(o + 16 + off, p.chunks + z.c * p.pitch + off, z.len);
+            return;
+        }
+        const uint32_t sp = p.spos[z.seg];
+        if (z.b == 0 && t == 0) {
+            put32(o + 16 + 4 * z.j, sp);
+            put32(o + sp, p.ssize[z.seg]);
+        }
+        fr = o + sp + 4;
+        if (p.sraw[z.seg]) {
+            copy_bytes(fr + uint64_t(z.b) * zstd::kBlock, zblock_src(p, z), z.len);
+            return;
+        }
+    }
+    const uint32_t fh = zstd::frame_header_bytes(z.seglen);
+    if (z.b == 0 && t == 0)
+        zstd::write_frame_header(fr, z.seglen);
+    uint8_t* d = fr + fh + p.bpos[g];
+    const bool last = z.b + 1 == z.nb;
+    const uint32_t k = p.bkind[g];
+    if (k == 0) {
+        if (t == 0)
+            zstd::write_block_header(d, last, 0, z.len);
+        copy_bytes(d + 3, zblock_src(p, z), z.len);
+    } else if (k == 1) {
+        if (t == 0) {
+            zstd::write_block_header(d, last, 1, z.len);
+            d[3] = uint8_t(p.bpay[g]);
+        }
+    } else if (k == 2) {
+        const uint32_t nl = p.bnlit[g], pay = p.bpay[g], sq = p.bseqb[g];
+        const uint8_t* scr = p.scratch + uint64_t(g) * zstd::kBlock;
+        if (p.bltype[g] == 2) {
+            const ZstdSegTable& T = p.tab[z.seg];
+            const bool carry = p.carrier[z.seg] == z.b;
+            const uint32_t cs = pay + (carry ? T.tree_n : 0);
+            const uint32_t lh = zstd::lit_header_huf_bytes(nl, cs);
+            if (t == 0) {
+                zstd::write_block_header(d, last, 2, lh + cs + sq);
+                zstd::write_lit_header_huf(d + 3, carry ? 2 : 3, nl, cs);
+            }
+            uint8_t* q = d + 3 + lh;
+            if (carry) {
+                for (uint32_t i = t; i < T.tree_n; i += 256)
+                    q[i] = T.tree[i];
+                q += T.tree_n;
+            }
+            copy_bytes(q, scr, pay + sq);
+        } else {
+            const uint32_t lh = zstd::lit_header_raw_bytes(nl);
+            if (t == 0) {
+                zstd::write_block_header(d, last, 2, lh + nl + sq);
+                zstd::write_lit_header_raw(d + 3, 0, nl);
+            }
+            copy_bytes(d + 3 + lh, scr, nl + sq);
+        }
+    }
+}
+
 } // namespace
 
 hipError_t
@@ -704,6 +1385,37 @@ launch_blosc_lz4(const BloscParams& p, hipStream_t stream)
     hipLaunchKernelGGL(scan_offsets, dim3(1), dim3(256), 0, stream, p.fsize, p.order,
                        p.offsets, p.cstart, p.n_chunks);
     hipLaunchKernelGGL(write_frames, dim3(uint32_t(ns)), dim3(256), 0, stream, p);
+    return hipGetLastError();
+}
+
+hipError_t
+launch_zstd(const ZstdParams& p, hipStream_t stream)
+{
+    if (p.n_chunks == 0)
+        return hipSuccess;
+    const uint64_t nseg = uint64_t(p.n_chunks) * p.nseg;
+    const uint64_t nblk = nseg * p.bps;
+    if (nblk * kZSubBlocks > 0x7fffffffull || p.nseg == 0 || p.bps == 0 ||
+        uint64_t(p.bps) * zstd::kBlock < p.seg_bytes)
+        return hipErrorInvalidValue;
+    if (!p.store_only) {
+        if (p.match) {
+            hipError_t e = hipMemsetAsync(p.hist, 0, nblk * 256 * 4, stream);
+            if (e != hipSuccess)
+                return e;
+            hipLaunchKernelGGL(zstd_parse, dim3(uint32_t(nblk * kZSubBlocks)), dim3(64), 0,
+                               stream, p);
+        } else {
+            hipLaunchKernelGGL(zstd_hist, dim3(uint32_t(nblk)), dim3(256), 0, stream, p);
+        }
+        hipLaunchKernelGGL(zstd_table, dim3(uint32_t(nseg)), dim3(64), 0, stream, p);
+        hipLaunchKernelGGL(zstd_encode, dim3(uint32_t(nblk)), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL(zstd_segment, dim3(uint32_t(nseg)), dim3(64), 0, stream, p);
+    }
+    hipLaunchKernelGGL(zstd_chunk, dim3(p.n_chunks), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL(scan_offsets, dim3(1), dim3(256), 0, stream, p.fsize, p.order,
+                       p.offsets, p.cstart, p.n_chunks);
+    hipLaunchKernelGGL(zstd_write, dim3(uint32_t(nblk)), dim3(256), 0, stream, p);
     return hipGetLastError();
 }
 

@@ -2,6 +2,7 @@
 // aqz_engine.cpp -- see aqz_engine.hh.  Citations are to
 // /root/reference/src/streaming/.
 #include "aqz_engine.hh"
+#include "aqz_zstd.hh"
 
 #include <algorithm>
 #include <cstdlib>
@@ -1563,16 +1564,20 @@ Stage::shard_geometry(uint32_t level, uint32_t* chunks_per_shard, uint32_t* n_sh
 
 // ---- device compression of resident layers ----------
 Compressor::Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compression& c)
+  : c_(c)
+  , nbytes_(chunk_bytes)
+  , typesize_(typesize)
 {
-    if (c.codec != 1)
-        throw Error(4, "only blosc-lz4 compresses on the device");
-    if (c.shuffle < 0 || c.shuffle > 2 || c.clevel < 0 || c.clevel > 9)
+    if (c.codec < 1 || c.codec > 3)
+        throw Error(4, "unknown codec");
+    if (c.codec != 3 && (c.shuffle < 0 || c.shuffle > 2 || c.clevel < 0 || c.clevel > 9))
         throw Error(1, "invalid compression settings");
     if (chunk_bytes == 0 || chunk_bytes > 0x7fffffefull || typesize == 0 ||
         typesize > 255)
         throw Error(1, "chunk size outside the blosc1 limits");
-    g_ = make_blosc_geom(uint32_t(chunk_bytes), typesize, uint32_t(c.shuffle));
-    store_only_ = c.clevel == 0;
+    if (c.codec == 1)
+        g_ = make_blosc_geom(uint32_t(chunk_bytes), typesize, uint32_t(c.shuffle));
+    store_only_ = c.codec != 3 && c.clevel == 0;
 }
 
 void
@@ -1580,6 +1585,10 @@ Compressor::run(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
                 const uint32_t* flags, uint32_t tag, uint8_t* out, uint64_t* offsets,
                 hipStream_t stream, const uint32_t* order)
 {
+    if (c_.codec != 1) {
+        run_zstd(chunks, pitch, n_chunks, flags, tag, out, offsets, stream, order);
+        return;
+    }
     const uint64_t ns = uint64_t(n_chunks) * g_.spc;
     scratch_.alloc(store_only_ ? 1 : ns * g_.slot);
     ssize_.alloc(ns * 4);
@@ -1607,6 +1616,112 @@ Compressor::run(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
     hip_check(launch_blosc_lz4(p, stream), "blosc-lz4 launch");
 }
 
+// blosc-zstd: one zstd frame per blosc block of the (device-shuffled)
+// chunk; zstd: one frame per chunk (aqz_codec.hh ZstdParams).
+void
+Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
+                     const uint32_t* flags, uint32_t tag, uint8_t* out, uint64_t* offsets,
+                     hipStream_t stream, const uint32_t* order)
+{
+    const bool blosc = c_.codec == 2;
+    ZstdParams p{};
+    p.chunks = chunks;
+    p.pitch = pitch;
+    p.n_chunks = n_chunks;
+    p.nbytes = uint32_t(nbytes_);
+    p.typesize = typesize_;
+    p.shuffle = blosc ? uint32_t(c_.shuffle) : 0;
+    p.blosc = blosc ? 1 : 0;
+    p.store_only = store_only_ ? 1 : 0;
+    p.flags = flags;
+    p.tag = tag;
+    if (blosc) {
+        const ZstdBloscGeom g = make_zstd_blosc_geom(uint32_t(nbytes_), typesize_);
+        p.seg_bytes = g.blocksize;
+        p.nseg = g.nblocks;
+    } else {
+        p.seg_bytes = uint32_t(nbytes_);
+        p.nseg = 1;
+    }
+    p.bps = (p.seg_bytes + zstd::kBlock - 1) / zstd::kBlock;
+    p.src = chunks;
+    p.src_pitch = pitch;
+    const bool shuffle = blosc && !store_only_ &&
+                         (c_.shuffle == 2 || (c_.shuffle == 1 && typesize_ > 1));
+    if (shuffle) {
+        zin_.alloc(size_t(n_chunks) * nbytes_);
+        ShuffleParams sp{ chunks, pitch, n_chunks, flags, tag, p.nbytes, typesize_,
+                          uint32_t(c_.shuffle), p.seg_bytes, p.nseg, zin_.p };
+        hip_check(launch_shuffle_blocks(sp, stream), "shuffle launch");
+        p.src = zin_.p;
+        p.src_pitch = nbytes_;
+    }
+    const uint64_t nseg = uint64_t(n_chunks) * p.nseg, nblk = nseg * p.bps;
+    // LZ matches unless AQZ_ZSTD_MATCH=0 (literals only: the serial model's
+    // byte-exact mode, tests/test_gpu_zstd.py)
+    const char* me = std::getenv("AQZ_ZSTD_MATCH");
+    p.match = (me && std::atoi(me) == 0) ? 0 : 1;
+    if (!store_only_) {
+        if (!seqt_.p) {
+            zstd::SeqTables t;
+            if (!zstd::build_seq_tables(t))
+                throw Error(10, "zstd sequence tables");
+            seqt_.alloc(sizeof(t));
+            hip_check(hipMemcpy(seqt_.p, &t, sizeof(t), hipMemcpyHostToDevice), "hipMemcpy");
+        }
+        if (p.match) {
+            const uint64_t nu = nblk * kZSubBlocks;
+            lits_.alloc(nu * kZSub);
+            seqs_.alloc(nu * kZSubSeq * 8);
+            snseq_.alloc(nu * 4);
+            snlit_.alloc(nu * 4);
+            stail_.alloc(nu * 4);
+        }
+        bltype_.alloc(nblk);
+        bseqb_.alloc(nblk * 4);
+        bnlit_.alloc(nblk * 4);
+        hist_.alloc(nblk * 256 * 4);
+        bkind_.alloc(nblk);
+        bpay_.alloc(nblk * 4);
+        bpos_.alloc(nblk * 4);
+        scratch_.alloc(nblk * zstd::kBlock);
+        tab_.alloc(nseg * sizeof(ZstdSegTable));
+        carrier_.alloc(nseg * 4);
+        sraw_.alloc(nseg);
+        ssize_.alloc(nseg * 4);
+    }
+    spos_.alloc(nseg * 4);
+    fsize_.alloc(size_t(n_chunks) * 4);
+    mode_.alloc(n_chunks);
+    cstart_.alloc(size_t(n_chunks) * 8);
+    p.seqt = reinterpret_cast<const zstd::SeqTables*>(seqt_.p);
+    p.lits = lits_.p;
+    p.seqs = reinterpret_cast<uint64_t*>(seqs_.p);
+    p.snseq = reinterpret_cast<uint32_t*>(snseq_.p);
+    p.snlit = reinterpret_cast<uint32_t*>(snlit_.p);
+    p.stail = reinterpret_cast<uint32_t*>(stail_.p);
+    p.bltype = bltype_.p;
+    p.bseqb = reinterpret_cast<uint32_t*>(bseqb_.p);
+    p.bnlit = reinterpret_cast<uint32_t*>(bnlit_.p);
+    p.hist = reinterpret_cast<uint32_t*>(hist_.p);
+    p.bkind = bkind_.p;
+    p.bpay = reinterpret_cast<uint32_t*>(bpay_.p);
+    p.bpos = reinterpret_cast<uint32_t*>(bpos_.p);
+    p.scratch = scratch_.p;
+    p.tab = reinterpret_cast<ZstdSegTable*>(tab_.p);
+    p.carrier = reinterpret_cast<uint32_t*>(carrier_.p);
+    p.ssize = reinterpret_cast<uint32_t*>(ssize_.p);
+    p.sraw = sraw_.p;
+    p.spos = reinterpret_cast<uint32_t*>(spos_.p);
+    p.fsize = reinterpret_cast<uint32_t*>(fsize_.p);
+    p.mode = mode_.p;
+    p.order = order;
+    p.offsets = offsets;
+    p.cstart = reinterpret_cast<uint64_t*>(cstart_.p);
+    p.out = out;
+    hip_check(launch_zstd(p, stream), "zstd launch");
+}
+
 void
 Stage::ensure_comp_slots(StageLevel& L)
 {
@@ -1632,6 +1747,15 @@ Stage::ensure_comp_slots(StageLevel& L)
         hip_check(hipEventCreateWithFlags(&L.zin_ev[s], hipEventDisableTiming),
                   "hipEventCreate");
     }
+}
+
+// the zstd codecs run on the device unless AQZ_ZSTD_HOST=1 (device shuffle
+// + host libzstd pool, aqz_hostzstd.hh)
+static bool
+zstd_on_host()
+{
+    const char* s = std::getenv("AQZ_ZSTD_HOST");
+    return s && std::atoi(s) != 0;
 }
 
 // host threads for the zstd codecs (AQZ_ZSTD_THREADS)
@@ -1735,7 +1859,7 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
     const uint32_t slot = uint32_t(layer % L.n_slots);
     if (L.slot_layer[slot] != int64_t(layer))
         throw Error(3, "chunk layer not resident");
-    if (c.codec == 2 || c.codec == 3) {
+    if ((c.codec == 2 || c.codec == 3) && zstd_on_host()) {
         compress_layer_host(L, slot, layer, c);
         return;
     }

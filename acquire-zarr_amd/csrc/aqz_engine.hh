@@ -77,19 +77,22 @@ struct PinnedBuf
 // codec values of ZarrCompressionCodec).
 struct Compression
 {
-    int32_t codec = 0;   // 0 none, 1 blosc-lz4 (2 blosc-zstd, 3 zstd: not on device)
-    int32_t clevel = 1;  // blosc clevel; 0 stores every chunk uncompressed
+    int32_t codec = 0;   // 0 none, 1 blosc-lz4, 2 blosc-zstd, 3 zstd
+    int32_t clevel = 1;  // blosc clevel (0 stores every chunk uncompressed);
+                         // zstd level (the device encoder has one setting)
     int32_t shuffle = 1; // 0 none, 1 byte, 2 bit
 };
 
-// blosc1/LZ4 frames of arrays of equally sized device chunks (aqz_codec.hip).
+// Device frames of arrays of equally sized device chunks (aqz_codec.hip):
+// blosc1-lz4, blosc1-zstd or plain zstd.
 class Compressor
 {
   public:
     Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compression& c);
+    // bytes that always hold the frames of n_chunks chunks (any codec)
     static uint64_t max_bytes(uint64_t chunk_bytes, uint32_t n_chunks)
     {
-        return uint64_t(n_chunks) * (chunk_bytes + 16);
+        return uint64_t(n_chunks) * (chunk_bytes + 32 + 3 * (chunk_bytes / 32768 + 1));
     }
     // Enqueue on `stream`: the frames of n_chunks chunks (chunk i at
     // chunks + i * pitch; skipped unless flags[i] == tag when flags is
@@ -103,13 +106,26 @@ class Compressor
     // device bytes of the scratch buffers allocated so far
     uint64_t device_bytes() const
     {
-        return scratch_.n + ssize_.n + spos_.n + fsize_.n + mode_.n + cstart_.n;
+        uint64_t n = scratch_.n + ssize_.n + spos_.n + fsize_.n + mode_.n + cstart_.n;
+        for (const DevBuf* b : { &zin_, &hist_, &bkind_, &bpay_, &bpos_, &tab_, &carrier_,
+                                 &sraw_, &lits_, &seqs_, &snseq_, &snlit_, &stail_, &bltype_,
+                                 &bseqb_, &bnlit_, &seqt_ })
+            n += b->n;
+        return n;
     }
 
   private:
-    BloscGeom g_;
+    void run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
+                  const uint32_t* flags, uint32_t tag, uint8_t* out, uint64_t* offsets,
+                  hipStream_t stream, const uint32_t* order);
+    Compression c_;
+    uint64_t nbytes_ = 0;
+    uint32_t typesize_ = 1;
+    BloscGeom g_{};
     bool store_only_;
     DevBuf scratch_, ssize_, spos_, fsize_, mode_, cstart_;
+    DevBuf zin_, hist_, bkind_, bpay_, bpos_, tab_, carrier_, sraw_; // zstd
+    DevBuf lits_, seqs_, snseq_, snlit_, stail_, bltype_, bseqb_, bnlit_, seqt_;
 };
 
 struct ArrayDesc

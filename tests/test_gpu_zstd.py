@@ -1,14 +1,21 @@
 """GPU stage with the zstd codecs (SURVEY §8f rank 2 remainder): blosc1
 frames with codec zstd (zarr.common.cpp:106-140 with "zstd") and plain zstd
 frames (zarr.common.cpp:142-166), as Chunk::compress_and_take_buffer
-dispatches them (chunk.cpp:78-106).  The device shuffles every block of the
-resident layer and the host zstd pool compresses (aqz_hostzstd.hh).
+dispatches them (chunk.cpp:78-106).  Two engines: the device encoder
+(default; aqz_codec.hip zstd_* kernels over aqz_zstd.hh) and, with
+AQZ_ZSTD_HOST=1, the device shuffle + host libzstd pool (aqz_hostzstd.hh).
+The device frames are also compared byte for byte with the serial model of
+the same encoder (tests/zstd/libzstd_host.so), which libzstd decodes on the
+CPU suite.
 
 Bar: every frame decodes to the oracle's chunk exactly -- blosc-zstd with a
 restated blosc1 decoder over libzstd (codec_helpers.blosc_zstd_decode) and
 with c-blosc 1.21.0 itself, plain zstd with libzstd -- chunks without data
 are skipped, incompressible chunks become memcpyed frames (blosc's rule),
 and the ratio on camera-like data stays close to c-blosc's zstd."""
+import ctypes as C
+import os
+
 import numpy as np
 import pytest
 
@@ -21,6 +28,24 @@ from oracle_bindings import MEAN, SPACE, TIME, U8, U16, F32, synthetic_frames
 pytestmark = pytest.mark.gpu
 
 needs_zstd = pytest.mark.skipif(libzstd() is None, reason="no libzstd to decode with")
+MODEL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "zstd", "libzstd_host.so")
+
+
+@pytest.fixture(params=["device", "host"])
+def engine(request, monkeypatch):
+    monkeypatch.setenv("AQZ_ZSTD_HOST", "1" if request.param == "host" else "0")
+    return request.param
+
+
+def model_frame(data: bytes, lz: int = 0) -> bytes:
+    L = C.CDLL(MODEL)
+    L.zh_encode_frame.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_void_p, C.c_uint64]
+    L.zh_encode_frame.restype = C.c_uint64
+    src = np.frombuffer(data, np.uint8)
+    out = np.zeros(len(data) + 4096, np.uint8)
+    n = L.zh_encode_frame(src.ctypes.data, len(data), lz, out.ctypes.data, out.size)
+    assert n > 0
+    return out[:n].tobytes()
 
 
 def _frames(dtype, n, h, w, seed):
@@ -90,28 +115,34 @@ def _run(gpu, dtype, codec, clevel, shuffle):
 @needs_zstd
 @pytest.mark.parametrize("dtype", [U8, U16, F32], ids=["u8", "u16", "f32"])
 @pytest.mark.parametrize("shuffle", [0, 1, 2])
-def test_stage_blosc_zstd_layers(gpu, dtype, shuffle):
+def test_stage_blosc_zstd_layers(gpu, engine, dtype, shuffle):
     _run(gpu, dtype, 2, 5, shuffle)
 
 
+DEVICE_RATIO_BOUND = 1.20
+
+
 @needs_zstd
-def test_stage_blosc_zstd_clevel0_memcpyed(gpu):
+def test_stage_blosc_zstd_clevel0_memcpyed(gpu, engine):
     assert _run(gpu, U16, 2, 0, 1) > 0
 
 
 @needs_zstd
 @pytest.mark.parametrize("level", [1, 3, 9])
-def test_stage_plain_zstd_layers(gpu, level):
+def test_stage_plain_zstd_layers(gpu, engine, level):
     _run(gpu, U16, 3, level, 0)
 
 
 @needs_zstd
 @pytest.mark.skipif(libblosc() is None, reason="c-blosc not in this image")
-def test_blosc_zstd_ratio_close_to_cblosc(gpu):
+def test_blosc_zstd_ratio_close_to_cblosc(gpu, engine):
     """One C2-shaped chunk layer level (256x256 chunks, 8 frames) of
-    camera-like u16 data: the device+host frames are at most 10% larger than
-    c-blosc zstd clevel 5 on the same chunks; plain zstd at level 3 within 5%
-    of ZSTD_compress (the same library, bigger single frames here)."""
+    camera-like u16 data: the host-engine frames are at most 10% larger
+    than c-blosc zstd clevel 5 (ZSTD_compress level 5 for plain zstd) on the
+    same chunks; the device encoder (one fixed operating point: Huffman
+    literals, greedy matches, predefined sequence tables) within its
+    documented bound."""
+    bound = 1.10 if engine == "host" else DEVICE_RATIO_BOUND
     dims = [(TIME, 0, 8, 1), (SPACE, 512, 256, 1), (SPACE, 512, 256, 1)]
     rng = np.random.default_rng(8)
     frames = camera_like(rng, 8 * 512 * 512, np.uint16).reshape(8, 512, 512)
@@ -127,5 +158,63 @@ def test_blosc_zstd_ratio_close_to_cblosc(gpu):
         data, off = st.copy_compressed(0, 0)
         ours = int(off[-1])
         theirs = sum(len(ref(ch)) for ch in chunks)
-        assert ours <= 1.10 * theirs, (codec, shuffle, ours, theirs)
+        print(f"{engine} codec {codec} shuffle {shuffle}: {ours} vs {theirs} bytes "
+              f"({ours / theirs:.3f}x)")
+        assert ours <= bound * theirs, (codec, shuffle, ours, theirs)
     st.close()
+
+
+@needs_zstd
+@pytest.mark.skipif(not os.path.exists(MODEL), reason="tests/zstd not built")
+@pytest.mark.parametrize("codec,shuffle", [(3, 0), (2, 1), (2, 2)])
+def test_device_frames_equal_serial_model(gpu, monkeypatch, codec, shuffle):
+    """Literal-only frames: the device encoder's bytes equal the serial
+    model's (same Huffman construction, same block decisions), frame by
+    frame -- plain zstd per chunk, blosc-zstd per record of a shuffled
+    block."""
+    monkeypatch.setenv("AQZ_ZSTD_HOST", "0")
+    monkeypatch.setenv("AQZ_ZSTD_MATCH", "0")
+    dims = [(TIME, 0, 4, 1), (SPACE, 512, 256, 1), (SPACE, 384, 128, 1)]
+    frames = _frames(U16, 4, 512, 384, 77)
+    st = gpu.Stage(dims, U16, MEAN, multiscale=False, layer_slots=2, max_batch_frames=4)
+    st.append(frames)
+    layer, flags = st.copy_layer(0, 0)
+    bpc = st.layout(0)["bytes_per_chunk"]
+    st.compress_layer(0, 0, codec=codec, clevel=5, shuffle=shuffle)
+    data, _ = st.copy_compressed(0, 0)
+    ent = st.compressed_entries(0, 0)
+    st.close()
+    checked = 0
+    for c, _, _, o, nb in ent:
+        fr = data[o:o + nb].tobytes()
+        if not flags[c]:
+            continue
+        chunk = layer[c * bpc:(c + 1) * bpc].tobytes()
+        if codec == 3:
+            assert fr == model_frame(chunk), c
+            checked += 1
+            continue
+        h = header(fr)
+        if h["flags"] & 0x2:
+            continue
+        bs = h["blocksize"]
+        nblk = -(-bpc // bs)
+        for j in range(nblk):
+            blk = chunk[j * bs:(j + 1) * bs]
+            sh = shuffle_block(shuffle, 2, blk)
+            start = int.from_bytes(fr[16 + 4 * j:20 + 4 * j], "little")
+            cs = int.from_bytes(fr[start:start + 4], "little")
+            rec = fr[start + 4:start + 4 + cs]
+            if cs == len(blk):
+                assert rec == sh, (c, j)
+            else:
+                assert rec == model_frame(sh), (c, j)
+            checked += 1
+    assert checked > 0
+
+
+def shuffle_block(kind, ts, blk):
+    from codec_helpers import shuffle
+    if kind == 0:
+        return blk
+    return shuffle({1: "shuffle", 2: "bitshuffle"}[kind], ts, blk)
