@@ -806,7 +806,7 @@ aqz_compressor_max_bytes(uint64_t chunk_bytes, uint32_t n_chunks)
 uint32_t
 aqz_compressor_blocksize(const aqz_compressor* c)
 {
-    return c && c->c ? c->c->geom().blocksize : 0;
+    return c && c->c ? c->c->blocksize() : 0;
 }
 
 aqz_status
@@ -817,7 +817,7 @@ aqz_compressor_run(aqz_compressor* c, const void* chunks, uint64_t pitch,
     if (!c || !chunks || !dst || !offsets)
         return AQZ_STATUS_INVALID_ARGUMENT;
     return guard_sticky(c, [&] {
-        const uint64_t nb = c->c->geom().nbytes;
+        const uint64_t nb = c->c->chunk_bytes();
         if (pitch < nb)
             throw Error(1, "chunk pitch below the chunk size");
         if (dst_cap < Compressor::max_bytes(nb, n_chunks))

@@ -625,7 +625,19 @@ shuffle_blocks(const ShuffleParams p)
             const uint32_t vec = 16 / ts; // elements per 16-B load
             const bool dst_ok = (reinterpret_cast<uintptr_t>(dst) % vec) == 0 && ne % vec == 0;
             if (dst_ok) {
-                for (uint32_t w = t; w < ne / vec; w += 256) {
+                // Every workgroup starts at a different offset of its block
+                // (rotated rounds): blocks are 2^k bytes apart, and all
+                // workgroups walking their blocks in step hit the same HBM
+                // channels (1 TB/s measured before the rotation).
+                const uint32_t nw = ne / vec, rounds = (nw + 255) / 256;
+                const uint32_t rot = ((blockIdx.x + blockIdx.y * gridDim.x) * 37u) % rounds;
+#pragma unroll 4
+                for (uint32_t r0 = 0; r0 < rounds; ++r0) {
+                    uint32_t r = r0 + rot;
+                    r = r >= rounds ? r - rounds : r;
+                    const uint32_t w = r * 256 + t;
+                    if (w >= nw)
+                        continue;
                     const uint4 v = *reinterpret_cast<const uint4*>(src + 16ull * w);
                     uint8_t e[16];
                     __builtin_memcpy(e, &v, 16);
@@ -662,6 +674,7 @@ shuffle_blocks(const ShuffleParams p)
     }
     if (p.shuffle == 2 && ne % 8 == 0 && ne * ts == bsize) {
         const uint32_t row = ne / 8;
+#pragma unroll 4
         for (uint32_t m = t; m < row; m += 256) {
             const uint8_t* g = src + uint64_t(8) * m * ts; // 8 elements
             for (uint32_t jj = 0; jj < ts; ++jj) {
@@ -701,7 +714,11 @@ shuffle_blocks(const ShuffleParams p)
 //   zstd_chunk   per chunk: blosc record offsets / memcpyed rule, frame bytes
 //   zstd_write   per zstd block: headers, tree, payload or raw bytes
 constexpr uint32_t kZMinHuf = 64; // fewer literals: raw (as the host model)
-constexpr uint32_t kZStreamWords = (zstd::kBlock / 4 * zstd::kHufMaxBits) / 32 + 2;
+// a Huffman stream is kept only when it is not larger than its literals:
+// room for 8 bits per literal (+ end mark and the word a code straddles)
+constexpr uint32_t kZStreamWords = (zstd::kBlock / 4 * 8) / 32 + 4;
+static_assert(4 * kZStreamWords <= 4096, "stream buffers fit the encode kernel's LDS");
+static_assert(kZSubBlocks * kZSubSeq * 8 + 4096 <= 4096 * 4, "staged sequences fit");
 
 struct ZBlock
 {
@@ -952,9 +969,12 @@ __global__ __launch_bounds__(64) void
 zstd_table(const ZstdParams p)
 {
     __shared__ zstd::HufWork w;
+    __shared__ zstd::TreeWork tw;
     __shared__ uint64_t key[256];
     __shared__ uint8_t len[256];
-    __shared__ uint32_t npresent;
+    __shared__ uint16_t code[256];
+    __shared__ uint8_t tree[160];
+    __shared__ uint32_t npresent, tree_n, mode;
     const uint32_t s = blockIdx.x, t = threadIdx.x;
     if (zchunk_skip(p, s / p.nseg))
         return;
@@ -968,6 +988,7 @@ zstd_table(const ZstdParams p)
         w.cnt[k] = a;
         key[k] = uint64_t(a) << 8 | k;
         len[k] = 0;
+        code[k] = 0;
         if (a)
             atomicAdd(&npresent, 1u);
     }
@@ -991,25 +1012,73 @@ zstd_table(const ZstdParams p)
     for (uint32_t k = t; k < n; k += 64)
         w.sorted[k] = uint16_t(key[256 - n + k] & 255u);
     __syncthreads();
-    if (t != 0)
-        return;
-    ZstdSegTable& T = p.tab[s];
-    T.mode = n == 1 ? 1 : 0;
-    T.tree_n = 0;
-    if (n >= 2) {
-        zstd::huf_lengths_sorted(w, n, len, zstd::kHufMaxBits);
-        uint16_t code[256];
-        const uint32_t mb = zstd::huf_codes(len, code);
-        uint8_t tree[160];
-        T.tree_n = zstd::huf_write_tree(len, mb, tree);
-        T.mode = T.tree_n ? 2 : 0;
-        for (uint32_t k = 0; k < 256; ++k) {
-            T.code[k] = code[k];
-            T.len[k] = len[k];
+    // the serial construction on lane 0, every array in LDS
+    if (t == 0) {
+        mode = n == 1 ? 1 : 0;
+        tree_n = 0;
+        if (n >= 2) {
+            zstd::huf_lengths_sorted(w, n, len, zstd::kHufMaxBits);
+            const uint32_t mb = zstd::huf_codes(len, code, tw);
+            tree_n = zstd::huf_write_tree(len, mb, tree, tw);
+            mode = tree_n ? 2 : 0;
         }
-        for (uint32_t k = 0; k < T.tree_n; ++k)
-            T.tree[k] = tree[k];
     }
+    __syncthreads();
+    ZstdSegTable& T = p.tab[s];
+    for (uint32_t k = t; k < 256; k += 64) {
+        T.code[k] = code[k];
+        T.len[k] = len[k];
+    }
+    for (uint32_t k = t; k < tree_n; k += 64)
+        T.tree[k] = tree[k];
+    if (t == 0) {
+        T.mode = mode;
+        T.tree_n = tree_n;
+    }
+}
+
+// A sequence's codes and extra bits in one word: llc (6) | mlc (6) | ofc (5)
+// | ll extra (16) | ml extra (16) | offset extra (15).
+__device__ __forceinline__ uint64_t
+zseq_codes(const zstd::Seq& v)
+{
+    const uint32_t llc = zstd::ll_code(v.lit), mlc = zstd::ml_code(v.len);
+    const uint32_t ofv = v.off + 3, ofc = zstd::highbit(ofv);
+    return uint64_t(llc) | uint64_t(mlc) << 6 | uint64_t(ofc) << 12 |
+           uint64_t(v.lit - zstd::ll_base(llc)) << 17 |
+           uint64_t(v.len - zstd::ml_base(mlc)) << 33 | uint64_t(ofv - (1u << ofc)) << 49;
+}
+
+// zstd::encode_sequences over pre-coded sequences (same bitstream)
+__device__ uint32_t
+zseq_encode(const zstd::SeqTables& t, const uint64_t* sv, uint32_t n, uint8_t* out,
+            uint32_t cap)
+{
+    zstd::BitW w;
+    w.init(out, cap);
+    uint64_t v = sv[n - 1];
+    uint32_t llc = uint32_t(v & 63u), mlc = uint32_t((v >> 6) & 63u), ofc = uint32_t((v >> 12) & 31u);
+    uint32_t sml = zstd::fse_init(t.ml, mlc), sof = zstd::fse_init(t.of, ofc),
+             sll = zstd::fse_init(t.ll, llc);
+    w.add((v >> 17) & 0xFFFFu, zstd::ll_bits(llc));
+    w.add((v >> 33) & 0xFFFFu, zstd::ml_bits(mlc));
+    w.add(v >> 49, ofc);
+    for (int i = int(n) - 2; i >= 0; --i) {
+        v = sv[i];
+        llc = uint32_t(v & 63u);
+        mlc = uint32_t((v >> 6) & 63u);
+        ofc = uint32_t((v >> 12) & 31u);
+        zstd::fse_enc(w, sof, t.of, ofc);
+        zstd::fse_enc(w, sml, t.ml, mlc);
+        zstd::fse_enc(w, sll, t.ll, llc);
+        w.add((v >> 17) & 0xFFFFu, zstd::ll_bits(llc));
+        w.add((v >> 33) & 0xFFFFu, zstd::ml_bits(mlc));
+        w.add(v >> 49, ofc);
+    }
+    zstd::fse_flush(w, sml, t.ml);
+    zstd::fse_flush(w, sof, t.of);
+    zstd::fse_flush(w, sll, t.ll);
+    return w.close();
 }
 
 // literal i of block g: the block's bytes (literals only) or the parse
@@ -1032,13 +1101,16 @@ struct ZLits
 __global__ __launch_bounds__(256) void
 zstd_encode(const ZstdParams p)
 {
-    __shared__ uint32_t buf[4][kZStreamWords];
+    // the 4 Huffman streams, later the staged sequences and their stream
+    __shared__ uint32_t zbuf[4096];
+    uint32_t(*buf)[kZStreamWords] = reinterpret_cast<uint32_t(*)[kZStreamWords]>(zbuf);
     __shared__ uint16_t code[256];
     __shared__ uint8_t clen[256];
     __shared__ int32_t rle;
     __shared__ uint32_t ssz[4];
     __shared__ uint32_t pre[kZSubBlocks + 1], spre[kZSubBlocks + 1], carry[kZSubBlocks];
     __shared__ uint32_t dec[4]; // kind, literal type, literal payload, sequence bytes
+    __shared__ zstd::SeqTables seqt;
     const uint32_t g = blockIdx.x, t = threadIdx.x;
     const ZBlock z = zblock(p, g);
     if (z.len == 0 || zchunk_skip(p, z.c)) {
@@ -1066,6 +1138,9 @@ zstd_encode(const ZstdParams p)
             }
         }
     }
+    if (p.match)
+        for (uint32_t i = t; i < sizeof(zstd::SeqTables) / 4; i += 256)
+            reinterpret_cast<uint32_t*>(&seqt)[i] = reinterpret_cast<const uint32_t*>(p.seqt)[i];
     __syncthreads();
     const uint32_t nl = pre[kZSubBlocks], nseq = spre[kZSubBlocks];
     if (nl > 0 && p.hist[uint64_t(g) * 256 + t] == nl)
@@ -1086,41 +1161,65 @@ zstd_encode(const ZstdParams p)
         code[t] = T.code[t];
         clen[t] = T.len[t];
         for (uint32_t i = t; i < 4 * kZStreamWords; i += 256)
-            (&buf[0][0])[i] = 0;
+            zbuf[i] = 0;
     }
     __syncthreads();
     if (try_huf) {
+        // stream w on wave w; literals are read coalesced (lane l takes
+        // literal s + l of each run of 64) and placed by a suffix scan of
+        // their code lengths: a stream is written last literal first
         const uint32_t w = t >> 6, lane = t & 63u;
         const uint32_t seg4 = zstd::lit_segment(nl);
         const uint32_t a = min(nl, w * seg4), e = min(nl, (w + 1) * seg4);
-        const uint32_t slen = e - a, per = (slen + 63) / 64;
-        const uint32_t la = a + min(slen, lane * per), le = a + min(slen, (lane + 1) * per);
+        uint32_t k = 0; // parse unit of this lane's literal (match mode)
+        auto sym_at = [&](uint32_t i) -> uint8_t {
+            if (!lit.pre)
+                return lit.base[i];
+            while (k + 1 < kZSubBlocks && pre[k + 1] <= i)
+                ++k;
+            while (i < pre[k])
+                --k;
+            return lit.base[uint64_t(k) * kZSub + (i - pre[k])];
+        };
         uint32_t bits = 0;
-        for (uint32_t i = la; i < le; ++i)
-            bits += clen[lit(i)];
-        // bits of the lanes above: the stream is written last literal first
-        uint32_t x = bits;
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_down(x, d);
-            if (lane + uint32_t(d) < 64)
-                x += y;
+        for (uint32_t i = a + lane; i < e; i += 64)
+            bits += clen[sym_at(i)];
+        for (int d = 32; d > 0; d >>= 1)
+            bits += __shfl_xor(bits, d);
+        const bool fits = bits + 1 <= 8 * (e - a) + 32;
+        if (fits) {
+            uint32_t* sb = buf[w];
+            uint32_t base = 0;
+            for (uint32_t cs = e; cs > a;) {
+                const uint32_t s0 = cs > a + 64 ? cs - 64 : a;
+                const uint32_t i = s0 + lane;
+                uint32_t n = 0, v = 0;
+                if (i < cs) {
+                    const uint8_t sym = sym_at(i);
+                    n = clen[sym];
+                    v = code[sym];
+                }
+                uint32_t x = n; // inclusive suffix sum over the run
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t y = __shfl_down(x, d);
+                    if (lane + uint32_t(d) < 64)
+                        x += y;
+                }
+                const uint32_t pos = base + x - n;
+                if (n) {
+                    const uint32_t o = pos & 31u;
+                    atomicOr(&sb[pos >> 5], v << o);
+                    if (o + n > 32)
+                        atomicOr(&sb[(pos >> 5) + 1], v >> (32 - o));
+                }
+                base += __shfl(x, 0);
+                cs = s0;
+            }
+            if (lane == 0)
+                atomicOr(&sb[bits >> 5], 1u << (bits & 31u)); // end mark
         }
-        const uint32_t total = __shfl(x, 0);
-        uint32_t pos = x - bits;
-        uint32_t* sb = buf[w];
-        for (uint32_t i = le; i-- > la;) {
-            const uint8_t sym = lit(i);
-            const uint32_t v = code[sym], n = clen[sym];
-            const uint32_t o = pos & 31u;
-            atomicOr(&sb[pos >> 5], v << o);
-            if (o + n > 32)
-                atomicOr(&sb[(pos >> 5) + 1], v >> (32 - o));
-            pos += n;
-        }
-        if (lane == 0) {
-            atomicOr(&sb[total >> 5], 1u << (total & 31u)); // end mark
-            ssz[w] = total / 8 + 1;
-        }
+        if (lane == 0)
+            ssz[w] = fits ? bits / 8 + 1 : 0x7fffffffu;
     }
     __syncthreads();
     uint8_t* d = p.scratch + uint64_t(g) * zstd::kBlock;
@@ -1128,7 +1227,8 @@ zstd_encode(const ZstdParams p)
         // literals: Huffman when it beats raw counted with the tree
         uint32_t ltype = 0, lpay = nl, lsec = zstd::lit_header_raw_bytes(nl) + nl;
         if (try_huf) {
-            const uint32_t pay = 6 + ssz[0] + ssz[1] + ssz[2] + ssz[3];
+            const uint64_t pay64 = 6ull + ssz[0] + ssz[1] + ssz[2] + ssz[3];
+            const uint32_t pay = uint32_t(min(pay64, uint64_t(0x7fffffffu)));
             const uint32_t wt = T.tree_n + pay;
             const uint32_t hs = zstd::lit_header_huf_bytes(nl, wt) + wt;
             if (hs < lsec) {
@@ -1137,46 +1237,19 @@ zstd_encode(const ZstdParams p)
                 lsec = hs;
             }
         }
-        // sequences section after the literal payload
-        uint32_t sq = 0;
-        if (lpay < zstd::kBlock) {
-            uint8_t* o = d + lpay;
-            const uint32_t cap = zstd::kBlock - lpay;
-            if (cap >= 4) {
-                sq = zstd::write_seq_header(o, nseq);
-                if (nseq) {
-                    const uint64_t* sv = p.seqs + uint64_t(g) * kZSubBlocks * kZSubSeq;
-                    const uint32_t bits = zstd::encode_sequences(
-                      *p.seqt,
-                      [&](uint32_t i) {
-                          uint32_t k = 0;
-                          while (k + 1 < kZSubBlocks && spre[k + 1] <= i)
-                              ++k;
-                          zstd::Seq v =
-                            zstd::unpack_seq(sv[uint64_t(k) * kZSubSeq + (i - spre[k])]);
-                          if (i == spre[k])
-                              v.lit += carry[k];
-                          return v;
-                      },
-                      nseq, o + sq, cap - sq);
-                    sq = bits ? sq + bits : 0;
-                }
-            }
-        }
-        const bool ok = sq != 0 && lsec + sq < z.len;
-        dec[0] = ok ? 2 : 0;
         dec[1] = ltype;
         dec[2] = lpay;
-        dec[3] = sq;
+        dec[0] = lsec;
     }
     __syncthreads();
-    if (dec[0] != 2) {
+    const uint32_t ltype = dec[1], lpay = dec[2], lsec = dec[0];
+    if (lsec + 1 >= z.len) { // not smaller even without sequences
         if (t == 0)
             p.bkind[g] = 0;
         return;
     }
-    const uint32_t lpay = dec[2];
-    if (dec[1] == 2) {
+    // the literal payload -> scratch[0, lpay)
+    if (ltype == 2) {
         if (t == 0) {
             zstd::put_le(d, ssz[0], 2);
             zstd::put_le(d + 2, ssz[1], 2);
@@ -1193,11 +1266,47 @@ zstd_encode(const ZstdParams p)
         for (uint32_t i = t; i < nl; i += 256)
             d[i] = lit(i);
     }
+    __syncthreads(); // the stream buffers are free from here
+    // the block's sequences staged in LDS with their codes and extra bits,
+    // so the one serial lane only runs the FSE states and the bit packing
+    uint64_t* sv = reinterpret_cast<uint64_t*>(zbuf);
+    uint8_t* so = reinterpret_cast<uint8_t*>(sv + kZSubBlocks * kZSubSeq);
+    const uint32_t so_cap = uint32_t(sizeof(zbuf) - kZSubBlocks * kZSubSeq * 8);
+    if (nseq) {
+        const uint64_t* gs = p.seqs + uint64_t(g) * kZSubBlocks * kZSubSeq;
+        for (uint32_t i = t; i < nseq; i += 256) {
+            uint32_t k = 0;
+            while (k + 1 < kZSubBlocks && spre[k + 1] <= i)
+                ++k;
+            zstd::Seq v = zstd::unpack_seq(gs[uint64_t(k) * kZSubSeq + (i - spre[k])]);
+            if (i == spre[k])
+                v.lit += carry[k];
+            sv[i] = zseq_codes(v);
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t sq = zstd::write_seq_header(so, nseq);
+        if (nseq) {
+            const uint32_t bits = zseq_encode(seqt, sv, nseq, so + sq, so_cap - sq);
+            sq = bits ? sq + bits : 0;
+        }
+        dec[3] = (sq != 0 && lpay + sq <= zstd::kBlock && lsec + sq < z.len) ? sq : 0;
+    }
+    __syncthreads();
+    const uint32_t sq = dec[3];
+    if (sq == 0) {
+        if (t == 0)
+            p.bkind[g] = 0;
+        return;
+    }
+    for (uint32_t i = t; i < sq; i += 256)
+        d[lpay + i] = so[i];
     if (t == 0) {
         p.bkind[g] = 2;
-        p.bltype[g] = uint8_t(dec[1]);
+        p.bltype[g] = uint8_t(ltype);
         p.bpay[g] = lpay;
-        p.bseqb[g] = dec[3];
+        p.bseqb[g] = sq;
         p.bnlit[g] = nl;
     }
 }

@@ -103,6 +103,16 @@ class Compressor
              const uint32_t* flags, uint32_t tag, uint8_t* out, uint64_t* offsets,
              hipStream_t stream, const uint32_t* order = nullptr);
     const BloscGeom& geom() const { return g_; }
+    uint64_t chunk_bytes() const { return nbytes_; }
+    // the blosc block size recorded in the frames (0: plain zstd)
+    uint32_t blocksize() const
+    {
+        if (c_.codec == 1)
+            return g_.blocksize;
+        if (c_.codec == 2)
+            return make_zstd_blosc_geom(uint32_t(nbytes_), typesize_).blocksize;
+        return 0;
+    }
     // device bytes of the scratch buffers allocated so far
     uint64_t device_bytes() const
     {

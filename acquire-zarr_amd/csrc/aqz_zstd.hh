@@ -29,8 +29,12 @@
 namespace aqz {
 namespace zstd {
 
-// content bytes of one zstd block (parallel unit of the device encoder)
-constexpr uint32_t kBlock = 32 * 1024;
+// content bytes of one zstd block, the parallel unit of the device encoder:
+// one workgroup, whose sequences are FSE-coded by one lane -- 8 KiB keeps
+// that serial chain short and four times as many of them in flight as
+// 32 KiB blocks did (encode 4.6 -> see DESIGN.md), for ~15 bytes of block
+// and literal headers per block
+constexpr uint32_t kBlock = 8 * 1024;
 constexpr uint32_t kHufMaxBits = 11;
 constexpr uint32_t kWeightsLog = 6; // FSE accuracy of the Huffman weights
 
@@ -108,14 +112,20 @@ struct FseCT
 
 // norm: normalized counts of symbols 0..maxsym (-1 = "less than 1"),
 // summing to 1 << al.  false when the distribution is not valid.
+struct FseBuildWork
+{
+    uint8_t sym[1u << kFseMaxLog];
+    uint32_t cumul[kFseMaxSym + 1];
+};
+
 __host__ __device__ inline bool
-fse_build(FseCT& ct, const int16_t* norm, uint32_t maxsym, uint32_t al)
+fse_build(FseCT& ct, const int16_t* norm, uint32_t maxsym, uint32_t al, FseBuildWork& bw)
 {
     if (al > kFseMaxLog || maxsym >= kFseMaxSym)
         return false;
     const uint32_t ts = 1u << al, mask = ts - 1, step = (ts >> 1) + (ts >> 3) + 3;
-    uint8_t sym[1u << kFseMaxLog];
-    uint32_t cumul[kFseMaxSym + 1];
+    uint8_t* sym = bw.sym;
+    uint32_t* cumul = bw.cumul;
     uint32_t high = ts - 1;
     cumul[0] = 0;
     for (uint32_t s = 0; s <= maxsym; ++s) {
@@ -162,6 +172,13 @@ fse_build(FseCT& ct, const int16_t* norm, uint32_t maxsym, uint32_t al)
     }
     ct.al = al;
     return true;
+}
+
+__host__ __device__ inline bool
+fse_build(FseCT& ct, const int16_t* norm, uint32_t maxsym, uint32_t al)
+{
+    FseBuildWork bw;
+    return fse_build(ct, norm, maxsym, al, bw);
 }
 
 // first (= last encoded) symbol: the smallest state, no bits out
@@ -320,26 +337,41 @@ huf_lengths(const uint32_t* cnt_in, uint8_t* len, uint32_t maxbits)
     return n;
 }
 
+// Workspace of the tree description (LDS in the kernel).
+struct TreeWork
+{
+    uint8_t w[256];
+    uint8_t tmp[160];
+    FseCT ct;
+    FseBuildWork bw;
+    int16_t norm[kHufMaxBits + 1];
+    uint32_t wc[kHufMaxBits + 1];
+    uint32_t nper[kHufMaxBits + 2];
+    uint32_t start[kHufMaxBits + 2];
+};
+
 // Canonical codes (RFC 8878 4.2.2: longest codes first, symbol order within
 // a length).  Returns the largest length.
 __host__ __device__ inline uint32_t
-huf_codes(const uint8_t* len, uint16_t* code)
+huf_codes(const uint8_t* len, uint16_t* code, TreeWork& tw)
 {
-    uint32_t nper[kHufMaxBits + 2] = { 0 };
+    for (uint32_t L = 0; L < kHufMaxBits + 2; ++L) {
+        tw.nper[L] = 0;
+        tw.start[L] = 0;
+    }
     uint32_t mx = 0;
     for (uint32_t s = 0; s < 256; ++s) {
-        nper[len[s]]++;
+        tw.nper[len[s]]++;
         if (len[s] > mx)
             mx = len[s];
     }
-    uint32_t start[kHufMaxBits + 2] = { 0 };
     uint32_t v = 0;
     for (uint32_t L = mx; L >= 1; --L) {
-        start[L] = v;
-        v = (v + nper[L]) >> 1;
+        tw.start[L] = v;
+        v = (v + tw.nper[L]) >> 1;
     }
     for (uint32_t s = 0; s < 256; ++s)
-        code[s] = len[s] ? uint16_t(start[len[s]]++) : 0;
+        code[s] = len[s] ? uint16_t(tw.start[len[s]]++) : 0;
     return mx;
 }
 
@@ -349,15 +381,17 @@ huf_codes(const uint8_t* len, uint16_t* code)
 // Returns bytes written (<= 129), 0 when it cannot be described (> 128
 // weights that FSE does not compress): the caller stores raw literals.
 __host__ __device__ inline uint32_t
-huf_write_tree(const uint8_t* len, uint32_t maxbits, uint8_t* out)
+huf_write_tree(const uint8_t* len, uint32_t maxbits, uint8_t* out, TreeWork& tw)
 {
     uint32_t last = 0;
     for (uint32_t s = 0; s < 256; ++s)
         if (len[s])
             last = s;
     const uint32_t nw = last; // weights transmitted
-    uint8_t w[256];
-    uint32_t wc[kHufMaxBits + 1] = { 0 };
+    uint8_t* w = tw.w;
+    uint32_t* wc = tw.wc;
+    for (uint32_t v = 0; v <= kHufMaxBits; ++v)
+        wc[v] = 0;
     uint32_t wmax = 0;
     for (uint32_t s = 0; s < nw; ++s) {
         w[s] = len[s] ? uint8_t(maxbits + 1 - len[s]) : 0;
@@ -366,14 +400,13 @@ huf_write_tree(const uint8_t* len, uint32_t maxbits, uint8_t* out)
             wmax = w[s];
     }
     // FSE-compressed weights (2 interleaved states, as FSE_compress)
-    uint32_t fsz = 0;
     if (nw > 2) {
         bool single = false;
         for (uint32_t v = 0; v <= wmax; ++v)
             single |= wc[v] == nw;
         if (!single) {
             const uint32_t al = kWeightsLog, ts = 1u << al;
-            int16_t norm[kHufMaxBits + 1];
+            int16_t* norm = tw.norm;
             uint32_t sum = 0, big = 0;
             for (uint32_t v = 0; v <= wmax; ++v) {
                 uint32_t q = uint32_t((uint64_t(wc[v]) * ts) / nw);
@@ -387,14 +420,14 @@ huf_write_tree(const uint8_t* len, uint32_t maxbits, uint8_t* out)
             const int fix = int(norm[big]) + int(ts) - int(sum);
             if (fix >= 1) {
                 norm[big] = int16_t(fix);
-                FseCT ct;
-                uint8_t tmp[160];
-                const uint32_t hn = fse_build(ct, norm, wmax, al)
-                                      ? fse_write_ncount(tmp, sizeof(tmp), norm, wmax, al)
+                FseCT& ct = tw.ct;
+                uint8_t* tmp = tw.tmp;
+                const uint32_t hn = fse_build(ct, norm, wmax, al, tw.bw)
+                                      ? fse_write_ncount(tmp, sizeof(tw.tmp), norm, wmax, al)
                                       : 0;
                 if (hn) {
                     BitW bw;
-                    bw.init(tmp + hn, sizeof(tmp) - hn);
+                    bw.init(tmp + hn, sizeof(tw.tmp) - hn);
                     uint32_t s1, s2;
                     int i = int(nw);
                     if (nw & 1) {
@@ -413,7 +446,7 @@ huf_write_tree(const uint8_t* len, uint32_t maxbits, uint8_t* out)
                     fse_flush(bw, s1, ct);
                     const uint32_t sn = bw.close();
                     if (sn && hn + sn < 128 && (nw > 128 || hn + sn < (nw + 1) / 2)) {
-                        fsz = hn + sn;
+                        const uint32_t fsz = hn + sn;
                         out[0] = uint8_t(fsz);
                         for (uint32_t k = 0; k < fsz; ++k)
                             out[1 + k] = tmp[k];
@@ -429,6 +462,20 @@ huf_write_tree(const uint8_t* len, uint32_t maxbits, uint8_t* out)
     for (uint32_t i = 0; i < nw; i += 2)
         out[1 + i / 2] = uint8_t(w[i] << 4 | (i + 1 < nw ? w[i + 1] : 0));
     return 1 + (nw + 1) / 2;
+}
+
+// host-side conveniences (their own workspace)
+inline uint32_t
+huf_codes(const uint8_t* len, uint16_t* code)
+{
+    TreeWork tw;
+    return huf_codes(len, code, tw);
+}
+inline uint32_t
+huf_write_tree(const uint8_t* len, uint32_t maxbits, uint8_t* out)
+{
+    TreeWork tw;
+    return huf_write_tree(len, maxbits, out, tw);
 }
 
 // ---- headers ---------------------------------------------------------------

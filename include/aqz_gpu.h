@@ -343,15 +343,22 @@ aqz_status aqz_stage_device_layer(aqz_stage* st, uint32_t level,
  *  - AQZ_CODEC_BLOSC_LZ4: blosc1 frames made on the device (shuffle +
  *    LZ4); clevel 0 stores every chunk as a memcpyed frame, levels 1-9 run
  *    the same GPU match finder.
- *  - AQZ_CODEC_BLOSC_ZSTD: the device shuffles every block, the layer goes
- *    D2H and a host pool runs zstd per block (blosc clevel -> zstd level as
- *    c-blosc maps it) into blosc1 frames.
- *  - AQZ_CODEC_ZSTD: plain zstd frames of the chunk bytes at level clevel
- *    (ZSTD_compress, zarr.common.cpp:142-166), on the host pool.
- *  The zstd codecs need the system's libzstd.so.1 (loaded on first use;
- *  absent -> AQZ_STATUS_NOT_YET_IMPLEMENTED).  Frames decode (any blosc1 /
- *  zstd decoder) to the chunk bytes exactly; their compressed bytes differ
- *  from c-blosc's (block size, match finder, no stream split for zstd). */
+ *  - AQZ_CODEC_BLOSC_ZSTD: blosc1 frames made on the device: every block
+ *    (256 KiB) shuffled, then one zstd frame per block (zarr.common.cpp:
+ *    106-140 with "zstd"); blosc clevel 0 stores memcpyed frames.
+ *  - AQZ_CODEC_ZSTD: one zstd frame per chunk (ZSTD_compress,
+ *    zarr.common.cpp:142-166), made on the device.
+ *  The device zstd encoder has one operating point for every level: Huffman
+ *  literals (one table per frame), a greedy LZ parse in 4 KiB units and
+ *  the predefined sequence tables; ratios on camera-like u16 data are within
+ *  ~8% (blosc-zstd) and ~16% (plain zstd) of libzstd at level 5.  With
+ *  AQZ_ZSTD_HOST=1 in the environment the zstd codecs run on a host pool
+ *  instead (device shuffle, D2H, the system's libzstd.so.1 at the clevel ->
+ *  zstd level map of c-blosc; absent library ->
+ *  AQZ_STATUS_NOT_YET_IMPLEMENTED), byte for byte what libzstd makes.
+ *  Frames decode (any blosc1 / zstd decoder) to the chunk bytes exactly;
+ *  their compressed bytes differ from c-blosc's and libzstd's (block size,
+ *  match finder, no stream split for blosc-zstd). */
 #define AQZ_CODEC_NONE 0
 #define AQZ_CODEC_BLOSC_LZ4 1
 #define AQZ_CODEC_BLOSC_ZSTD 2
@@ -378,9 +385,9 @@ aqz_status aqz_stage_compress_layer(aqz_stage* st, uint32_t level, uint64_t laye
  * offsets[chunks_per_layer] = total bytes.  n >= chunks_per_layer + 1. */
 aqz_status aqz_stage_compressed_offsets(aqz_stage* st, uint32_t level,
                                         uint64_t layer, uint64_t* offsets, size_t n);
-/* Copy of the layer's frames (total bytes) to dst.  blosc-lz4: dst host or
- * device, asynchronous, complete after aqz_stage_wait_copies.  blosc-zstd /
- * zstd (frames made on the host): dst is host memory, filled before the
+/* Copy of the layer's frames (total bytes) to dst: host or device,
+ * asynchronous, complete after aqz_stage_wait_copies.  With AQZ_ZSTD_HOST=1
+ * (zstd frames made on the host) dst is host memory, filled before the
  * call returns. */
 aqz_status aqz_stage_copy_compressed_async(aqz_stage* st, uint32_t level,
                                            uint64_t layer, void* dst, size_t cap);
@@ -418,7 +425,7 @@ aqz_status aqz_shard_table(const uint64_t* offsets, const uint64_t* extents,
                            uint32_t chunks_per_shard, void* out, size_t cap);
 uint32_t aqz_crc32c(const void* data, size_t n);
 
-/* Stand-alone compressor (blosc-lz4 only) for device-resident chunk arrays: chunk i of
+/* Stand-alone compressor (any AQZ_CODEC_*) for device-resident chunk arrays: chunk i of
  * n_chunks at chunks + i * pitch, chunk_bytes each; frames back to back at
  * dst (device, >= aqz_compressor_max_bytes), offsets (device, n_chunks + 1
  * uint64) as above.  Enqueued on `stream` (hipStream_t; NULL = default). */
@@ -430,7 +437,8 @@ uint64_t aqz_compressor_max_bytes(uint64_t chunk_bytes, uint32_t n_chunks);
 aqz_status aqz_compressor_run(aqz_compressor* c, const void* chunks, uint64_t pitch,
                               uint32_t n_chunks, void* dst, size_t dst_cap,
                               uint64_t* offsets, void* stream);
-/* The block size of the frames (recorded in each frame header). */
+/* The blosc block size of the frames (recorded in each frame header; 0 for
+ * plain zstd). */
 uint32_t aqz_compressor_blocksize(const aqz_compressor* c);
 
 /* Zero the not-yet-written frames of every level's last partial layer so

@@ -138,8 +138,13 @@ def chunk_payloads(rng, dtype, n_px: int, kinds=("camera", "zeros", "random",
 
 
 # ---- zstd (blosc-zstd and plain zstd frames) ------------------------------
-_LIBZSTD_PATHS = (os.path.join(ORACLE_DIR, "_ref", "lib", "libzstd.so.1"),
-                  "/opt/conda/lib/libzstd.so.1", "libzstd.so.1")
+# the process's libzstd.so.1 first: PyTorch's HIP runtime (pre-loaded
+# RTLD_GLOBAL by aqz) already holds the system copy, and a second copy of
+# the same soname opened by path binds its internal calls to the first one
+# (ZSTD_compress then frees with the wrong struct layout); the reference's
+# 1.4.9 (conda) when no copy is loaded yet
+_LIBZSTD_PATHS = ("libzstd.so.1", os.path.join(ORACLE_DIR, "_ref", "lib", "libzstd.so.1"),
+                  "/opt/conda/lib/libzstd.so.1")
 _zstd = None
 
 

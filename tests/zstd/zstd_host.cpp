@@ -55,6 +55,13 @@ huf_streams(const Table& t, const uint8_t* lit, uint32_t n, uint8_t* out, uint32
     uint32_t at = 6, sz[4];
     for (uint32_t k = 0; k < 4; ++k) {
         const uint32_t a = std::min(n, k * seg), b = std::min(n, (k + 1) * seg);
+        // the device keeps a stream only when it fits 8 bits per literal
+        // (+ 32): the same rule here
+        uint64_t bits = 0;
+        for (uint32_t i = a; i < b; ++i)
+            bits += t.len[lit[i]];
+        if (bits + 1 > 8ull * (b - a) + 32)
+            return 0;
         BitW w;
         w.init(out + at, cap > at ? cap - at : 0);
         for (uint32_t i = b; i-- > a;)

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""Dev harness (not product): device blosc1/LZ4 compressor throughput on a
-C2 level-0 chunk layer (64 chunks of 256x256x64 u16 = 8 MiB) for several
-payloads, next to c-blosc 1.21.0 (lz4, clevel 5, one thread) on the host.
+"""Dev harness (not product): device compressor throughput (blosc-lz4,
+blosc-zstd or plain zstd) on a C2 level-0 chunk layer (64 chunks of
+256x256x64 u16 = 8 MiB) for several payloads, next to c-blosc 1.21.0 /
+libzstd (clevel 5, one thread) on the host.
 
-  python3 tools/codec_bench.py [--reps 5] [--shuffle 1]
+  python3 tools/codec_bench.py [--reps 5] [--shuffle 1] [--codec lz4|blosc-zstd|zstd]
 """
 import argparse
 import os
@@ -42,20 +43,22 @@ def main():
     ap.add_argument("--shuffle", type=int, default=1)
     ap.add_argument("--clevel", type=int, default=5)
     ap.add_argument("--kinds", default="camera,dim,zeros,random")
+    ap.add_argument("--codec", default="lz4", choices=["lz4", "blosc-zstd", "zstd"])
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     n_chunks, cb = 64, 256 * 256 * 64 * 2
-    comp = aqz.Compressor(cb, 2, clevel=args.clevel, shuffle=args.shuffle)
+    codec = {"lz4": 1, "blosc-zstd": 2, "zstd": 3}[args.codec]
+    comp = aqz.Compressor(cb, 2, codec=codec, clevel=args.clevel, shuffle=args.shuffle)
     cap = comp.max_bytes(n_chunks)
     dst = torch.empty(cap, dtype=torch.uint8, device=dev)
     off = torch.empty(n_chunks + 1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream()
     try:
-        from codec_helpers import libblosc, libblosc_compress
+        from codec_helpers import libblosc, libblosc_compress, zstd_compress
         have_blosc = libblosc() is not None
     except Exception:
         have_blosc = False
-    print(f"layer: {n_chunks} chunks x {cb >> 20} MiB u16, shuffle {args.shuffle}, "
+    print(f"layer: {n_chunks} chunks x {cb >> 20} MiB u16, {args.codec}, shuffle {args.shuffle}, "
           f"blocksize {comp.blocksize}")
     for kind in args.kinds.split(","):
         src = payload(kind, n_chunks, cb, dev)
@@ -76,9 +79,13 @@ def main():
         if have_blosc:
             chunk = src[:cb].cpu().numpy().tobytes()
             t0 = time.perf_counter()
-            fr = libblosc_compress(chunk, 2, args.clevel, args.shuffle)
+            if codec == 3:
+                fr = zstd_compress(chunk, args.clevel)
+            else:
+                fr = libblosc_compress(chunk, 2, args.clevel, args.shuffle,
+                                       b"zstd" if codec == 2 else b"lz4")
             dt = time.perf_counter() - t0
-            line += f"   | c-blosc 1 thread {cb / dt / 1e9:6.2f} GB/s ratio {cb / len(fr):6.3f}"
+            line += f"   | host 1 thread {cb / dt / 1e9:6.2f} GB/s ratio {cb / len(fr):6.3f}"
         print(line, flush=True)
     comp.close()
 
