@@ -207,6 +207,7 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
         src_ptr, mem = src_arr.ctypes.data, aqz.MEM_HOST
     rng = np.random.default_rng(7 + rank)
     codec = {"none": 0, "lz4": 1, "blosc-zstd": 2, "zstd": 3}[args.codec]
+    host_zstd = os.environ.get("AQZ_ZSTD_HOST", "0") not in ("", "0")
     if codec:
         # compressible camera-like frames (smooth background + noise)
         n_px = src_arr.size // bpp
@@ -231,8 +232,9 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
             i = layer % 4
             off = st.compressed_offsets(l, layer)
             st.copy_compressed_async(l, layer, dst[l][i].ptr, cap[l])
-            # PCIe bytes: the frames (device lz4) or the shuffled layer (host zstd)
-            d2h[0] += int(off[-1]) if codec == 1 else lbytes[l]
+            # PCIe bytes: the frames (device codecs) or the shuffled layer
+            # (AQZ_ZSTD_HOST=1: zstd on the host pool)
+            d2h[0] += lbytes[l] if codec != 1 and host_zstd else int(off[-1])
             out_bytes[0] += int(off[-1])
 
     def hand_off():
@@ -285,9 +287,12 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
         "metric": "end-to-end input GB/s, host frames -> H2D -> multiscale stage -> "
                   + ({1: "device blosc-lz4 compression (shuffle %d) -> D2H of every "
                          "compressed chunk layer" % args.compress,
-                      2: "device shuffle (%d) -> D2H -> host blosc-zstd of every chunk "
-                         "layer" % args.compress,
-                      3: "D2H -> host zstd (level 3) of every chunk layer"}[codec]
+                      2: ("device shuffle (%d) -> D2H -> host blosc-zstd of every chunk "
+                          "layer" if host_zstd else "device blosc-zstd compression "
+                          "(shuffle %d) -> D2H of every compressed chunk layer") % args.compress,
+                      3: ("D2H -> host zstd (level 3) of every chunk layer" if host_zstd
+                          else "device zstd compression -> D2H of every compressed chunk "
+                          "layer")}[codec]
                      if codec else "D2H of every chunk layer"),
         "value": round(world * in_bytes / el / 1e9, 3), "unit": "GB/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
