@@ -138,6 +138,7 @@ def lib():
     sig = {
         "aqz_version": ([], C.c_char_p),
         "aqz_status_message": ([i32], C.c_char_p),
+        "aqz_last_error": ([], C.c_char_p),
         "aqz_device_count": ([C.POINTER(i32)], i32),
         "aqz_dims_create": ([D, sz, i32, C.POINTER(sz), C.POINTER(vp)], i32),
         "aqz_dims_destroy": ([vp], None),
@@ -225,7 +226,8 @@ def lib():
 
 def _check(status: int, what: str) -> None:
     if status != 0:
-        raise AqzError(status, what)
+        msg = lib().aqz_last_error()
+        raise AqzError(status, what + (": " + msg.decode() if msg else ""))
 
 
 def device_count() -> int:

@@ -7,6 +7,7 @@
 
 #include <cstring>
 #include <new>
+#include <string>
 
 using namespace aqz;
 
@@ -32,6 +33,8 @@ struct aqz_compressor
 
 namespace {
 
+thread_local std::string t_last_error;
+
 template<typename F>
 aqz_status
 guard(F&& f)
@@ -40,10 +43,16 @@ guard(F&& f)
         f();
         return AQZ_STATUS_SUCCESS;
     } catch (const Error& e) {
+        t_last_error = e.what();
         return e.status;
     } catch (const std::bad_alloc&) {
+        t_last_error = "out of memory";
         return AQZ_STATUS_OUT_OF_MEMORY;
+    } catch (const std::exception& e) {
+        t_last_error = e.what();
+        return AQZ_STATUS_INTERNAL_ERROR;
     } catch (...) {
+        t_last_error = "unknown exception";
         return AQZ_STATUS_INTERNAL_ERROR;
     }
 }
@@ -55,8 +64,10 @@ guard_sticky(O* o, F&& f)
 {
     if (!o)
         return AQZ_STATUS_INVALID_ARGUMENT;
-    if (o->sticky != AQZ_STATUS_SUCCESS)
+    if (o->sticky != AQZ_STATUS_SUCCESS) {
+        t_last_error = "object is in a sticky error state from an earlier call";
         return o->sticky;
+    }
     const aqz_status s = guard(std::forward<F>(f));
     if (s == AQZ_STATUS_INTERNAL_ERROR || s == AQZ_STATUS_OUT_OF_MEMORY)
         o->sticky = s;
@@ -119,6 +130,12 @@ const char*
 aqz_version(void)
 {
     return "0.1.0";
+}
+
+const char*
+aqz_last_error(void)
+{
+    return t_last_error.c_str();
 }
 
 const char*

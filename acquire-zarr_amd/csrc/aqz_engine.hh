@@ -89,10 +89,14 @@ class Compressor
 {
   public:
     Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compression& c);
-    // bytes that always hold the frames of n_chunks chunks (any codec)
+    // bytes that always hold the frames of n_chunks chunks (any codec).
+    // blosc frames never pass nbytes + 16 (the memcpyed rule); a plain zstd
+    // frame of incompressible data is its header (<= 13 B) plus one raw
+    // block (3-B header) per zstd::kBlock of input.
     static uint64_t max_bytes(uint64_t chunk_bytes, uint32_t n_chunks)
     {
-        return uint64_t(n_chunks) * (chunk_bytes + 32 + 3 * (chunk_bytes / 32768 + 1));
+        return uint64_t(n_chunks) *
+               (chunk_bytes + 32 + 3 * (chunk_bytes / zstd::kBlock + 1));
     }
     // Enqueue on `stream`: the frames of n_chunks chunks (chunk i at
     // chunks + i * pitch; skipped unless flags[i] == tag when flags is

@@ -51,7 +51,8 @@ namespace {
 [[noreturn]] void
 die(const char* what, aqz_status s = 0)
 {
-    std::fprintf(stderr, "stream_to_filesystem: %s (%s)\n", what, aqz_status_message(s));
+    std::fprintf(stderr, "stream_to_filesystem: %s (%s)%s%s\n", what, aqz_status_message(s),
+                 s ? ": " : "", s ? aqz_last_error() : "");
     std::exit(1);
 }
 

@@ -102,6 +102,10 @@ typedef struct
 
 const char* aqz_version(void);
 const char* aqz_status_message(aqz_status status);
+/* The message of the last failed call on this thread ("" if none): what
+ * the reference passes to LOG_ERROR before mapping an exception to a status
+ * (src/streaming/zarr.stream.cpp:1704-1719, src/logger/logger.hh). */
+const char* aqz_last_error(void);
 /* Number of HIP devices visible (0 when no GPU). */
 aqz_status aqz_device_count(int32_t* count);
 

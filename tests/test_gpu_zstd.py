@@ -134,6 +134,33 @@ def test_stage_plain_zstd_layers(gpu, engine, level):
 
 
 @needs_zstd
+def test_plain_zstd_incompressible_large_chunks(gpu):
+    """Incompressible 2 MiB chunks (BASELINE configs[0]'s 128x128x64 u16
+    chunk): every plain zstd frame is raw blocks, one 3-byte header per
+    8 KiB device block, so the layer stays within aqz_compressor_max_bytes
+    (the device output buffer) and decodes exactly (regression: the bound
+    once assumed 32 KiB blocks and the frames overran it)."""
+    dims = [(TIME, 0, 64, 1), (SPACE, 256, 128, 2), (SPACE, 256, 128, 2)]
+    frames = synthetic_frames(U16, 64, 256, 256, 77)
+    exp, _, _ = expected_stage_layers(dims, U16, MEAN, frames)
+    st = gpu.Stage(dims, U16, MEAN, layer_slots=1, max_batch_frames=64)
+    st.append(np.ascontiguousarray(frames))
+    st.compress_layer(0, 0, codec=3, clevel=1, shuffle=0)
+    data, off = st.copy_compressed(0, 0)
+    ent = st.compressed_entries(0, 0)
+    lay = st.layout(0)
+    bpc, n = lay["bytes_per_chunk"], lay["chunks_per_layer"]
+    st.close()
+    assert bpc == 2 << 20 and n == 4
+    assert int(off[-1]) <= gpu.lib().aqz_compressor_max_bytes(bpc, n)
+    assert int(off[-1]) > n * bpc  # raw blocks: the headers cost bytes
+    buf, _ = exp[(0, 0)]
+    for c, _, _, o, nb in ent:
+        fr = data[o:o + nb].tobytes()
+        assert zstd_decode(fr, bpc) == buf[c * bpc:(c + 1) * bpc].tobytes(), c
+
+
+@needs_zstd
 @pytest.mark.skipif(libblosc() is None, reason="c-blosc not in this image")
 def test_blosc_zstd_ratio_close_to_cblosc(gpu, engine):
     """One C2-shaped chunk layer level (256x256 chunks, 8 frames) of

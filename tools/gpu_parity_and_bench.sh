@@ -9,4 +9,4 @@ tail -15 gpurun_out/pytest_gpu.log
 echo "pytest rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && cat gpurun_out/smoke.log && \
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-seconds 5 > gpurun_out/bench1.log 2>&1; rc=$?; tail -3 gpurun_out/bench1.log; exit $rc
+timeout -k 10 300 python bench.py > gpurun_out/bench1.log 2>&1; rc=$?; tail -3 gpurun_out/bench1.log; exit $rc
