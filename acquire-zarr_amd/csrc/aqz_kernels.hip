@@ -838,6 +838,24 @@ region_of_block(const FusedParams& p)
     return b < (per << 3) ? (b & 7u) * per + (b >> 3) : b;
 }
 
+// Region q of a frame -> (row, column) of regions: row-major, or
+// column-major, so that consecutive workgroups walk down one column of
+// chunk tiles and write each tile's rows as one contiguous run.  Tuning knob
+// 1024 flips the kernel's default (same-stage A/B, tools/knob_ab.py: the
+// 2-D strip kernel is 2-3% faster row-major, the 2x2x2 strip kernel 2%
+// faster column-major).
+__device__ __forceinline__ void
+region_xy(const FusedParams& p, uint32_t q, uint32_t& by, uint32_t& bx, bool colmajor)
+{
+    if (colmajor != ((p.knobs & 1024u) != 0)) {
+        bx = q / p.nby_in;
+        by = q - bx * p.nby_in;
+    } else {
+        by = fdiv(q, p.d_nbx_in);
+        bx = q - by * p.nbx_in;
+    }
+}
+
 // Interior regions, one per workgroup (region r of n_frames * nby_in * nbx_in).
 // The rows of up to kPassBatch passes are loaded before any is reduced, so a
 // wave keeps its whole region in flight; then level 0 goes to its tiles,
@@ -925,9 +943,10 @@ fused_pyramid_strip(const FusedParams p)
     const uint32_t r = region_of_block(p);
     const uint32_t f = fdiv(r, p.d_nreg_in);
     const uint32_t q = r - f * (p.nbx_in * p.nby_in);
-    const uint32_t by = fdiv(q, p.d_nbx_in);
+    uint32_t by, bx;
+    region_xy(p, q, by, bx, false);
     const uint32_t y0 = by << 6;
-    const uint32_t x0 = (q - by * p.nbx_in) * RW;
+    const uint32_t x0 = bx * RW;
     const uint32_t w = threadIdx.x >> 6;
     const uint32_t hw = (threadIdx.x >> 5) & 1u;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1348,6 +1367,286 @@ fused_pyramid_3d(const FusedParams p)
 }
 
 // ---------------------------------------------------------------------------
+// 2x2x2 pyramid with the strip kernel's register cascade (64-row interior
+// regions, pixels <= 4 B, at most 4 fused levels).  One workgroup owns one
+// region of G consecutive planes and walks them in order.  Per plane, wave w
+// holds the region's rows [16w, 16w+16) as the strip kernel does: level 0 is
+// stored from registers, level 1 is a 2x2 in registers, level 2 meets the
+// row below through a lane^32 swap, levels 3-4 combine rows the lane already
+// holds.  A z-halving level k keeps its earlier plane's XY result in
+// registers (h1..h4) and emits mean2(earlier, later) on the odd plane
+// (downsampler.cpp:366-385, average_two_frames :208-246), so the cascade
+// needs no LDS and no barrier.  NTM as fused_pyramid_strip.  Host
+// guarantees as fused_pyramid_3d, plus rh_log2 == 6 and n_fused <= 4.
+// ---------------------------------------------------------------------------
+template<typename T, int M, int NTM, int PF>
+__global__ __launch_bounds__(256) void
+fused_pyramid_strip3d(const FusedParams p)
+{
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+    constexpr int VEC = 16 / sizeof(T);
+    constexpr int HV = VEC / 2;
+    constexpr int QV = VEC / 4;
+    constexpr uint32_t RW = 32 * VEC;
+    static_assert(QV >= 1, "strip 3-D kernel needs <= 4-byte pixels");
+    constexpr int N3 = QV >= 2 ? QV / 2 : 1;
+    constexpr int S3 = QV >= 2 ? 1 : 2;
+    constexpr int N4 = N3 >= 2 ? N3 / 2 : 1;
+    constexpr int S4 = N3 >= 2 ? S3 : 2 * S3;
+
+    const uint32_t nreg = p.nbx_in * p.nby_in;
+    const uint32_t blk = region_of_block(p);
+    const uint32_t grp = fdiv(blk, p.d_nreg_in);
+    const uint32_t r = blk - grp * nreg;
+    uint32_t by, bx;
+    region_xy(p, r, by, bx, true);
+    const uint32_t y0 = by << 6;
+    const uint32_t x0 = bx * RW;
+    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t hw = (threadIdx.x >> 5) & 1u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t cv = threadIdx.x & 31u;
+    const uint32_t trow = p.tw * uint32_t(sizeof(T));
+    const uint32_t nf = p.n_fused;
+    const uint32_t G = p.G;
+    const uint32_t zm = p.zmask;
+    const uint32_t ry = 16 * w + 2 * hw;
+    const uint64_t row = uint64_t(p.W[0]) * sizeof(T);
+    const uint8_t* src0 = p.src + uint64_t(grp * G) * p.src_stride +
+                          uint64_t(y0 + ry) * row + uint64_t(x0 + cv * VEC) * sizeof(T);
+    const bool v3ok = lane < 32 && (cv % S3) == 0;
+    const bool v4ok = lane < 32 && (cv % S4) == 0;
+
+    // earlier planes of the z pairs, packed (a lane's level-1 row is 8 B, its
+    // level-2 row 4 B): 16 VGPRs instead of 48 for u8
+    uint2 h1[4];
+    uint32_t h2[4];
+    T h3[2][N3], h4[N4];
+    const uint32_t g1 = G >> ((zm >> 1) & 1u);
+    const uint32_t g2 = g1 >> ((zm >> 2) & 1u);
+    const uint32_t g3 = g2 >> ((zm >> 3) & 1u);
+    const uint32_t g4 = g3 >> ((zm >> 4) & 1u);
+    // plane pl's rows are in ra/rb; the next plane's loads are issued as soon
+    // as this plane's level-0 stores and level-1 sums no longer need them, so
+    // they are in flight while levels 1-4 are formed and stored
+    uint4 ra[4], rb[4];
+    auto load_plane = [&](uint32_t pl) {
+        const uint8_t* s = src0 + uint64_t(pl) * p.src_stride;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u32x4v a = gload<(NTM & 1) != 0, u32x4v>(s + uint64_t(4 * i) * row);
+            const u32x4v b = gload<(NTM & 1) != 0, u32x4v>(s + uint64_t(4 * i + 1) * row);
+            ra[i] = uint4{ a.x, a.y, a.z, a.w };
+            rb[i] = uint4{ b.x, b.y, b.z, b.w };
+        }
+    };
+    if (PF)
+        load_plane(0);
+    for (uint32_t pl = 0; pl < G; ++pl) {
+        if (!PF)
+            load_plane(pl);
+        // which levels emit a frame at this plane, and its index there (a
+        // z-halving level emits on the later plane of each pair); uniform
+        uint32_t i1 = pl, i2, i3, i4;
+        bool e1 = nf >= 1, e2, e3, e4;
+        if (zm & 2u) {
+            e1 = e1 && (i1 & 1u);
+            i1 >>= 1;
+        }
+        i2 = i1;
+        e2 = e1 && nf >= 2;
+        if (zm & 4u) {
+            e2 = e2 && (i2 & 1u);
+            i2 >>= 1;
+        }
+        i3 = i2;
+        e3 = e2 && nf >= 3;
+        if (zm & 8u) {
+            e3 = e3 && (i3 & 1u);
+            i3 >>= 1;
+        }
+        i4 = i3;
+        e4 = e3 && nf >= 4;
+        if (zm & 16u) {
+            e4 = e4 && (i4 & 1u);
+            i4 >>= 1;
+        }
+        // level 0
+        {
+            FastTile t0 = fast_tile<T>(p, 0, grp * G + pl, y0 + ry, x0 + cv * VEC);
+            if (t0.p) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    gstore<(NTM & 2) != 0>(t0.p + uint64_t(4 * i) * trow,
+                                           u32x4v{ ra[i].x, ra[i].y, ra[i].z, ra[i].w });
+                    gstore<(NTM & 2) != 0>(t0.p + uint64_t(4 * i + 1) * trow,
+                                           u32x4v{ rb[i].x, rb[i].y, rb[i].z, rb[i].w });
+                    t0.nz |= ((ra[i].x | ra[i].y | ra[i].z | ra[i].w) |
+                              (rb[i].x | rb[i].y | rb[i].z | rb[i].w)) != 0u;
+                }
+            }
+            flush_tile_flag(t0);
+        }
+        // level-1 2x2 sums of this plane (8 B per row pair)
+        uint2 o1[4];
+        if (nf >= 1) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                T r0[VEC], r1[VEC], o[HV];
+                __builtin_memcpy(r0, &ra[i], 16);
+                __builtin_memcpy(r1, &rb[i], 16);
+#pragma unroll
+                for (int j = 0; j < HV; ++j)
+                    o[j] = reduce4<M, T>(r0[2 * j], r0[2 * j + 1], r1[2 * j], r1[2 * j + 1]);
+                __builtin_memcpy(&o1[i], o, 8);
+            }
+        }
+        if (PF && pl + 1 < G)
+            load_plane(pl + 1);
+        if (nf < 1)
+            continue;
+        // levels 1-2, one level-1 row (8w + hw + 2i) at a time
+        FastTile t1{}, t2{};
+        if (e1)
+            t1 = fast_tile<T>(p, 1, grp * g1 + i1, (y0 >> 1) + 8 * w + hw, (x0 >> 1) + cv * HV);
+        if (e2 && lane < 32)
+            t2 = fast_tile<T>(p, 2, grp * g2 + i2, (y0 >> 2) + 4 * w, (x0 >> 2) + cv * QV);
+        uint32_t q2w[4]; // level-2 rows 4w + i of this lane, packed
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            T o[HV];
+            __builtin_memcpy(o, &o1[i], 8);
+            if (zm & 2u) {
+                if (!e1) {
+                    __builtin_memcpy(&h1[i], o, 8);
+                    continue;
+                }
+                T a[HV];
+                __builtin_memcpy(a, &h1[i], 8);
+#pragma unroll
+                for (int j = 0; j < HV; ++j)
+                    o[j] = reduce2<M, T>(a[j], o[j]);
+            }
+            if (t1.p) {
+                gstore_px<T, HV, (NTM & 4) != 0>(t1.p + uint64_t(2 * i) * trow, o);
+                t1.nz |= any_nonzero<T, HV>(o);
+            }
+            if (nf < 2)
+                continue;
+            uint2 mine, below;
+            __builtin_memcpy(&mine, o, 8);
+            below.x = __shfl_xor(mine.x, 32);
+            below.y = __shfl_xor(mine.y, 32);
+            T b[HV], q[QV];
+            __builtin_memcpy(b, &below, 8);
+#pragma unroll
+            for (int j = 0; j < QV; ++j)
+                q[j] = reduce4<M, T>(o[2 * j], o[2 * j + 1], b[2 * j], b[2 * j + 1]);
+            if (zm & 4u) {
+                if (!e2) {
+                    __builtin_memcpy(&h2[i], q, 4);
+                    continue;
+                }
+                T a[QV];
+                __builtin_memcpy(a, &h2[i], 4);
+#pragma unroll
+                for (int j = 0; j < QV; ++j)
+                    q[j] = reduce2<M, T>(a[j], q[j]);
+            }
+            if (t2.p) {
+                gstore_px<T, QV, (NTM & 4) != 0>(t2.p + uint64_t(i) * trow, q);
+                t2.nz |= any_nonzero<T, QV>(q);
+            }
+            __builtin_memcpy(&q2w[i], q, 4);
+        }
+        flush_tile_flag(t1);
+        flush_tile_flag(t2);
+        if (!e2 || nf < 3)
+            continue;
+        // level 3: rows 2w + rr from level-2 rows 2rr, 2rr+1 of this lane
+        T v3[2][N3];
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+            T a[QV], c[QV];
+            __builtin_memcpy(a, &q2w[2 * rr], 4);
+            __builtin_memcpy(c, &q2w[2 * rr + 1], 4);
+            if constexpr (QV >= 2) {
+#pragma unroll
+                for (int j = 0; j < N3; ++j)
+                    v3[rr][j] = reduce4<M, T>(a[2 * j], a[2 * j + 1], c[2 * j], c[2 * j + 1]);
+            } else {
+                const T ar = shfl_down_t(a[0], 1), cr = shfl_down_t(c[0], 1);
+                v3[rr][0] = reduce4<M, T>(a[0], ar, c[0], cr);
+            }
+        }
+        if (zm & 8u) {
+            if (!e3) {
+#pragma unroll
+                for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+                    for (int j = 0; j < N3; ++j)
+                        h3[rr][j] = v3[rr][j];
+                continue;
+            }
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+                for (int j = 0; j < N3; ++j)
+                    v3[rr][j] = reduce2<M, T>(h3[rr][j], v3[rr][j]);
+        }
+        {
+            FastTile t3{};
+            if (v3ok)
+                t3 = fast_tile<T>(p, 3, grp * g3 + i3, (y0 >> 3) + 2 * w,
+                                  (x0 >> 3) + (cv / S3) * N3);
+            if (t3.p) {
+#pragma unroll
+                for (int rr = 0; rr < 2; ++rr) {
+                    gstore_px<T, N3, false>(t3.p + uint64_t(rr) * trow, v3[rr]);
+                    t3.nz |= any_nonzero<T, N3>(v3[rr]);
+                }
+            }
+            flush_tile_flag(t3);
+        }
+        if (nf < 4)
+            continue;
+        // level 4: row w
+        T v4[N4];
+        if constexpr (N3 >= 2) {
+#pragma unroll
+            for (int j = 0; j < N4; ++j)
+                v4[j] = reduce4<M, T>(v3[0][2 * j], v3[0][2 * j + 1], v3[1][2 * j],
+                                      v3[1][2 * j + 1]);
+        } else {
+            const T ar = shfl_down_t(v3[0][0], S3), cr = shfl_down_t(v3[1][0], S3);
+            v4[0] = reduce4<M, T>(v3[0][0], ar, v3[1][0], cr);
+        }
+        if (zm & 16u) {
+            if (!e4) {
+#pragma unroll
+                for (int j = 0; j < N4; ++j)
+                    h4[j] = v4[j];
+                continue;
+            }
+#pragma unroll
+            for (int j = 0; j < N4; ++j)
+                v4[j] = reduce2<M, T>(h4[j], v4[j]);
+        }
+        {
+            FastTile t4{};
+            if (v4ok)
+                t4 = fast_tile<T>(p, 4, grp * g4 + i4, (y0 >> 4) + w,
+                                  (x0 >> 4) + (cv / S4) * N4);
+            if (t4.p) {
+                gstore_px<T, N4, false>(t4.p, v4);
+                t4.nz |= any_nonzero<T, N4>(v4);
+            }
+            flush_tile_flag(t4);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Generic one-level step.  grid = (ceil(W*H/256), n_ops); one output pixel
 // per thread.
 // ---------------------------------------------------------------------------
@@ -1510,14 +1809,26 @@ launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
         return hipErrorInvalidValue;
     if (blocks == 0)
         return hipSuccess;
+    // the register-cascade kernel takes 64-row regions down to 4 fused levels
+    const bool strip = p.rh_log2 == 6 && p.n_fused <= 4 && !(p.knobs & 256u);
 #define CALL(T, MM)                                                            \
     do {                                                                       \
-        if (p.nt)                                                              \
-            hipLaunchKernelGGL((fused_pyramid_3d<T, MM, 7>), dim3(uint32_t(blocks)), \
-                               dim3(256), 0, stream, p);                      \
-        else                                                                   \
-            hipLaunchKernelGGL((fused_pyramid_3d<T, MM, 0>), dim3(uint32_t(blocks)), \
-                               dim3(256), 0, stream, p);                      \
+        const dim3 gd{ uint32_t(blocks), 1, 1 };                              \
+        if (strip && p.nt && (p.knobs & 512u))                                \
+            hipLaunchKernelGGL((fused_pyramid_strip3d<T, MM, 7, 0>), gd, dim3(256), 0, \
+                               stream, p);                                    \
+        else if (strip && p.nt)                                               \
+            hipLaunchKernelGGL((fused_pyramid_strip3d<T, MM, 7, 1>), gd, dim3(256), 0, \
+                               stream, p);                                    \
+        else if (strip)                                                       \
+            hipLaunchKernelGGL((fused_pyramid_strip3d<T, MM, 0, 1>), gd, dim3(256), 0, \
+                               stream, p);                                    \
+        else if (p.nt)                                                        \
+            hipLaunchKernelGGL((fused_pyramid_3d<T, MM, 7>), gd, dim3(256), 0,  \
+                               stream, p);                                    \
+        else                                                                  \
+            hipLaunchKernelGGL((fused_pyramid_3d<T, MM, 0>), gd, dim3(256), 0,  \
+                               stream, p);                                    \
     } while (0)
     switch (dtype) {
         case 0: AQZ_DISPATCH_M(uint8_t, method, CALL); break;

@@ -307,13 +307,24 @@ def test_stage_timing_marks(gpu):
 # ---------------------------------------------------------------------------
 # 2x2x2 fused path (regular z schedule) and z-slab sharding
 # ---------------------------------------------------------------------------
+# the register-cascade kernel (fused_pyramid_strip3d; tuning knob 512: its
+# variant without the next-plane prefetch) and, with knob 256, the
+# LDS-cascade kernel it replaced (fused_pyramid_3d)
+KERNELS_3D = {"strip3d": ("0", "fused_pyramid_strip3d"),
+              "strip3d_nopf": ("512", "fused_pyramid_strip3d"),
+              "lds3d": ("256", "fused_pyramid_3d")}
+
+
+@pytest.mark.parametrize("kernel", sorted(KERNELS_3D))
 @pytest.mark.parametrize("dtype", [U8, U16, I16, U32, F32], ids=lambda d: DTYPE_NAMES[d])
-def test_stage_3d_fused_regular(gpu, dtype):
+def test_stage_3d_fused_regular(gpu, monkeypatch, dtype, kernel):
     # every level halves x, y and z: G = 8 planes per workgroup
+    knobs, name = KERNELS_3D[kernel]
+    monkeypatch.setenv("AQZ_KNOBS", knobs)
     dims = [(TIME, 0, 1, 1), (CHANNEL, 2, 1, 1), (SPACE, 32, 4, 1),
             (SPACE, 512, 64, 1), (SPACE, 512, 64, 1)]
     st = gpu.Stage(dims, dtype, MEAN)
-    assert st.dominant_kernel() == "fused_pyramid_3d"
+    assert st.dominant_kernel() == name
     st.close()
     for m in ALL_METHODS:
         frames = _frames(dtype, 2 * 32, 512, 512, 40 + m + dtype)
@@ -321,16 +332,36 @@ def test_stage_3d_fused_regular(gpu, dtype):
         _check_stage(gpu, dims, dtype, m, frames, batch=16, chunks=[3, 13, 32, 16])
 
 
-def test_stage_c4_volume(gpu):
+@pytest.mark.parametrize("kernel", sorted(KERNELS_3D))
+def test_stage_c4_volume(gpu, monkeypatch, kernel):
     # BASELINE configs[3] level structure (z 64 -> 32 -> 16 -> 16 with
     # 16-plane z chunks; xy 2048 -> 256 with 256-px chunks): fused 2x2x2
+    knobs, name = KERNELS_3D[kernel]
+    monkeypatch.setenv("AQZ_KNOBS", knobs)
     dims = [(TIME, 0, 1, 1), (SPACE, 64, 16, 1), (SPACE, 2048, 256, 1),
             (SPACE, 2048, 256, 1)]
     frames = synthetic_frames(U16, 64, 2048, 2048, 77)
     st = gpu.Stage(dims, U16, MEAN)
-    assert st.dominant_kernel() == "fused_pyramid_3d"
+    assert st.dominant_kernel() == name
     st.close()
     _check_stage(gpu, dims, U16, MEAN, frames, batch=32)
+
+
+@pytest.mark.parametrize("dtype", [U8, U16, F32], ids=lambda d: DTYPE_NAMES[d])
+def test_stage_3d_five_levels(gpu, dtype):
+    """Five levels (four fused: xy 1024 -> 64 with 64-px chunks), z halving
+    at levels 1-3 only (64 -> 8 with 8-plane z chunks; level 4 keeps 8
+    planes): the strip 3-D kernel's level-4 row and a level that halves XY
+    but not z after three that halve both."""
+    dims = [(TIME, 0, 1, 1), (SPACE, 64, 8, 1), (SPACE, 1024, 64, 1), (SPACE, 1024, 64, 1)]
+    st = gpu.Stage(dims, dtype, MEAN)
+    assert st.dominant_kernel() == "fused_pyramid_strip3d"
+    assert st.n_levels() == 5
+    assert [st.level_dims(l)[1][1] for l in range(5)] == [64, 32, 16, 8, 8]
+    st.close()
+    for m in ALL_METHODS:
+        frames = _frames(dtype, 64, 1024, 1024, 90 + m + dtype)
+        _check_stage(gpu, dims, dtype, m, frames, batch=16)
 
 
 def test_stage_z_slab_sharding(gpu):

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Dev probe (not product): kernel-variant A/B on the SAME stage (same
+placement) via aqz_stage_set_tuning(knobs, nt).  Knobs of the 2x2x2 path:
+256 = the LDS-cascade fused_pyramid_3d, 512 = strip3d without the next-plane
+prefetch.  Prints ms per launch (best of 2 rounds) per stage instance."""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "acquire-zarr_amd"))
+
+import aqz  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c4")
+    ap.add_argument("--instances", type=int, default=3)
+    ap.add_argument("--knobs", default="0,512,256")
+    ap.add_argument("--nt", type=int, default=7)
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    c = bench.CONFIGS[args.config]
+    B = c["batch"]
+    h, w = c["dims"][-2][1], c["dims"][-1][1]
+    fbytes = h * w * {0: 1, 1: 2, 8: 4}[c["dtype"]]
+    src = torch.empty(2 * B * fbytes, dtype=torch.uint8, device="cuda")
+    src.view(torch.int16).random_(-32768, 32767)
+    knobs = [int(x) for x in args.knobs.split(",")]
+    for inst in range(args.instances):
+        st = aqz.Stage(c["dims"], c["dtype"], c["method"], max_batch_frames=B, layer_slots=2,
+                       force_levels=c["force_levels"])
+        row = []
+        for rnd in range(2):
+            for j, k in enumerate(knobs):
+                st.set_tuning(k, args.nt)
+                for i in range(2):
+                    st.append_ptr(src.data_ptr() + (i % 2) * B * fbytes, B)
+                st.synchronize()
+                st.timing_mark(0)
+                for i in range(args.reps):
+                    st.append_ptr(src.data_ptr() + (i % 2) * B * fbytes, B)
+                st.timing_mark(1)
+                ms = st.timing_elapsed() / args.reps
+                row = row + [ms] if rnd == 0 else row
+                row[j] = min(row[j], ms)
+        print(f"{args.config} inst{inst} {st.placement()['candidates_ms']} " +
+              " ".join(f"k{k}={v:.4f}" for k, v in zip(knobs, row)), flush=True)
+        st.close()
+
+
+if __name__ == "__main__":
+    main()
