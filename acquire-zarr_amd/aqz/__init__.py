@@ -198,6 +198,7 @@ def lib():
         "aqz_stage_timing_mark": ([vp, i32], i32),
         "aqz_stage_timing_elapsed": ([vp, C.POINTER(C.c_double)], i32),
         "aqz_stage_dominant_kernel": ([vp], C.c_char_p),
+        "aqz_probe_hbm": ([i32, i32, u64, u32, C.POINTER(C.c_double), C.POINTER(u64)], i32),
         "aqz_stage_placement": ([vp, C.POINTER(C.c_double), sz, C.POINTER(sz),
                                  C.POINTER(u32)], i32),
         "aqz_stage_host_affinity": ([vp, C.POINTER(i32), C.POINTER(u32)], i32),
@@ -228,6 +229,20 @@ def _check(status: int, what: str) -> None:
     if status != 0:
         msg = lib().aqz_last_error()
         raise AqzError(status, what + (": " + msg.decode() if msg else ""))
+
+
+PROBE_READ, PROBE_COPY, PROBE_COPY_THIRD, PROBE_READ_THIRD = 0, 1, 2, 3
+PROBE_PLAIN_STORES = 0x100
+
+
+def probe_hbm(shape: int, nbytes: int = 512 << 20, reps: int = 20, device: int = 0):
+    """(ms per launch, bytes read per launch) of the streaming probe
+    (aqz_probe_hbm, include/aqz_gpu_bench.h): this device's practical HBM
+    rate for one of the stage's access shapes."""
+    ms, rd = C.c_double(0), C.c_uint64(0)
+    _check(lib().aqz_probe_hbm(device, shape, nbytes, reps, C.byref(ms), C.byref(rd)),
+           "aqz_probe_hbm")
+    return ms.value, rd.value
 
 
 def device_count() -> int:

@@ -1,0 +1,151 @@
+// aqz_probe.hip -- practical HBM rates of this device for the stage's access
+// shapes (include/aqz_gpu_bench.h aqz_probe_hbm).  Measurement only: the
+// bench reports the stage's rates next to these ceilings, measured in the
+// same process on the same device.
+#include "aqz_gpu_bench.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// U 16-B vectors per lane, loaded before any is used (the stage's kernels
+// keep 128 B per lane in flight); U divisible by 3 for the 1/3 shapes
+constexpr int kU = 6;
+
+template<int MODE, bool NTS>
+__device__ __forceinline__ void
+put(u32x4* p, u32x4 v)
+{
+    if constexpr (NTS)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+template<int MODE, bool NTS>
+__global__ __launch_bounds__(256) void
+probe_stream(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+             u32x4* __restrict__ dst3, uint32_t* __restrict__ sink)
+{
+    const uint64_t base = uint64_t(blockIdx.x) * (kU * 256) + threadIdx.x;
+    u32x4 v[kU];
+#pragma unroll
+    for (int i = 0; i < kU; ++i)
+        v[i] = __builtin_nontemporal_load(src + base + i * 256);
+    if constexpr (MODE == AQZ_PROBE_READ) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < kU; ++i)
+            acc ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
+        if (acc == 0x9e3779b9u) // never: keeps the loads alive
+            sink[0] = acc;
+        return;
+    }
+    if constexpr (MODE == AQZ_PROBE_COPY || MODE == AQZ_PROBE_COPY_THIRD) {
+#pragma unroll
+        for (int i = 0; i < kU; ++i)
+            put<MODE, NTS>(dst + base + i * 256, v[i]);
+    }
+    if constexpr (MODE == AQZ_PROBE_COPY_THIRD || MODE == AQZ_PROBE_READ_THIRD) {
+        const uint64_t b3 = uint64_t(blockIdx.x) * (kU * 256 / 3) + threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < kU / 3; ++i)
+            put<MODE, NTS>(dst3 + b3 + i * 256, v[3 * i] ^ v[3 * i + 1] ^ v[3 * i + 2]);
+    }
+}
+
+struct DevMem
+{
+    void* p = nullptr;
+    ~DevMem()
+    {
+        if (p)
+            (void)hipFree(p);
+    }
+};
+
+} // namespace
+
+extern "C" aqz_status
+aqz_probe_hbm(int32_t device, int32_t shape, uint64_t bytes, uint32_t reps, double* ms,
+              uint64_t* read_bytes)
+{
+    const int32_t kind = shape & 0xff;
+    const bool plain = (shape & AQZ_PROBE_PLAIN_STORES) != 0;
+    if (!ms || kind < AQZ_PROBE_READ || kind > AQZ_PROBE_READ_THIRD || reps == 0 ||
+        (shape & ~(0xff | AQZ_PROBE_PLAIN_STORES)) != 0)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    const uint64_t per_wg = uint64_t(kU) * 256 * 16;
+    const uint64_t grid = bytes / per_wg;
+    if (grid == 0 || grid > 0x7fffffffull)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    const uint64_t rd = grid * per_wg;
+    constexpr int kRing = 4; // the source ring, well past the 256 MiB MALL
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    aqz_status st = AQZ_STATUS_SUCCESS;
+    {
+        DevMem src, dst, dst3, sink;
+        hipStream_t s = nullptr;
+        hipEvent_t a = nullptr, b = nullptr;
+        auto ok = [&](hipError_t e) {
+            if (e != hipSuccess && st == AQZ_STATUS_SUCCESS)
+                st = e == hipErrorOutOfMemory ? AQZ_STATUS_OUT_OF_MEMORY
+                                              : AQZ_STATUS_INTERNAL_ERROR;
+            return e == hipSuccess;
+        };
+        if (ok(hipMalloc(&src.p, rd * kRing)) && ok(hipMalloc(&dst.p, rd)) &&
+            ok(hipMalloc(&dst3.p, rd / 3 + per_wg)) && ok(hipMalloc(&sink.p, 64)) &&
+            ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) &&
+            ok(hipEventCreate(&a)) && ok(hipEventCreate(&b)) &&
+            ok(hipMemsetAsync(src.p, 1, rd * kRing, s))) {
+            auto launch = [&](uint32_t r) {
+                const auto* in = static_cast<const u32x4*>(src.p) + (r % kRing) * (rd / 16);
+                auto* o = static_cast<u32x4*>(dst.p);
+                auto* o3 = static_cast<u32x4*>(dst3.p);
+                auto* k = static_cast<uint32_t*>(sink.p);
+                const dim3 g{ uint32_t(grid), 1, 1 };
+#define PROBE_LAUNCH(MODE)                                                     \
+    if (plain)                                                                 \
+        hipLaunchKernelGGL((probe_stream<MODE, false>), g, dim3(256), 0, s, in, o, o3, k); \
+    else                                                                       \
+        hipLaunchKernelGGL((probe_stream<MODE, true>), g, dim3(256), 0, s, in, o, o3, k)
+                switch (kind) {
+                    case AQZ_PROBE_READ: PROBE_LAUNCH(AQZ_PROBE_READ); break;
+                    case AQZ_PROBE_COPY: PROBE_LAUNCH(AQZ_PROBE_COPY); break;
+                    case AQZ_PROBE_COPY_THIRD: PROBE_LAUNCH(AQZ_PROBE_COPY_THIRD); break;
+                    default: PROBE_LAUNCH(AQZ_PROBE_READ_THIRD);
+                }
+#undef PROBE_LAUNCH
+            };
+            for (uint32_t r = 0; r < 3; ++r)
+                launch(r);
+            float t = 0;
+            if (ok(hipGetLastError()) && ok(hipEventRecord(a, s))) {
+                for (uint32_t r = 0; r < reps; ++r)
+                    launch(r);
+                if (ok(hipEventRecord(b, s)) && ok(hipEventSynchronize(b)) &&
+                    ok(hipEventElapsedTime(&t, a, b))) {
+                    *ms = double(t) / reps;
+                    if (read_bytes)
+                        *read_bytes = rd;
+                }
+            }
+        }
+        if (s)
+            (void)hipStreamSynchronize(s);
+        if (a)
+            (void)hipEventDestroy(a);
+        if (b)
+            (void)hipEventDestroy(b);
+        if (s)
+            (void)hipStreamDestroy(s);
+    }
+    (void)hipSetDevice(prev);
+    return st;
+}

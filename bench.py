@@ -24,10 +24,6 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "acquire-zarr_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# probed ceiling of the pyramid-only access shape (each input byte read once
-# with nt loads, 1/3 of it written): tools/copy_probe.hip MODE 3,
-# profiles/r02_copy_probe.txt "read+1/3w ntl" -- 5105 GB/s read, 6807 GB/s bus
-PYR_PROBE_READ_GBS = 5105.0
 
 SPACE, CHANNEL, TIME = 0, 1, 2
 U8, U16, F32 = 0, 1, 8
@@ -67,6 +63,28 @@ CONFIGS = {
                dims=[(TIME, 0, 4, 1), (SPACE, 8192, 128, 1), (SPACE, 8192, 128, 1)],
                dtype=F32, method=MEAN, force_levels=0, batch=4, ring=12),
 }
+
+
+def hbm_probe(aqz, device):
+    """Live streaming probe of this device (aqz_probe_hbm): 512 MiB read per
+    launch from a 2 GiB ring, 16-B nontemporal lane loads, 24 KiB per
+    workgroup, the better of nontemporal and plain stores; GB/s of each
+    access shape the stage runs."""
+    out = {}
+    for key, shape, wr in (("read_gbs", aqz.PROBE_READ, 0.0),
+                           ("copy_bus_gbs", aqz.PROBE_COPY, 1.0),
+                           ("copy_third_bus_gbs", aqz.PROBE_COPY_THIRD, 4.0 / 3.0),
+                           ("read_third_bus_gbs", aqz.PROBE_READ_THIRD, 1.0 / 3.0)):
+        flavours = (0,) if shape == aqz.PROBE_READ else (0, aqz.PROBE_PLAIN_STORES)
+        runs = [aqz.probe_hbm(shape | f, 512 << 20, 20, device)
+                for _ in range(2) for f in flavours]
+        ms, rd = min(r[0] for r in runs), runs[0][1]
+        out[key] = round(rd * (1 + wr) / (ms * 1e-3) / 1e9, 1)
+        if shape == aqz.PROBE_READ_THIRD:
+            out["read_third_input_gbs"] = round(rd / (ms * 1e-3) / 1e9, 1)
+    out["read_frac_of_spec"] = round(out["read_gbs"] / HBM_PEAK_GBS, 4)
+    out["source"] = "aqz_probe_hbm (include/aqz_gpu_bench.h), measured in this run"
+    return out
 
 
 def level_sizes(stage):
@@ -451,6 +469,8 @@ def main():
                     help="end-to-end mode: frames start in host memory (pinned or "
                          "pageable), every completed chunk layer is handed back to "
                          "pinned host buffers (DESIGN.md 'End to end')")
+    ap.add_argument("--no-hbm-probe", action="store_true",
+                    help="skip the live streaming probe of this device's HBM rates")
     ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.codec == "none" and args.compress:
@@ -583,6 +603,9 @@ def main():
     side = None
     if not args.pyramid_only and not args.no_pyramid_only_line:
         side = run(True, max(5, args.steps // 2), 2)
+    probe = None
+    if not args.no_hbm_probe:
+        probe = hbm_probe(aqz, dev.index)
     sizes, elapsed, value = main_run["sizes"], main_run["elapsed"], main_run["value"]
     kernel, avg_ms, achieved = main_run["kernel"], main_run["avg_ms"], main_run["achieved"]
     alg_per_launch = main_run["alg"]
@@ -620,6 +643,14 @@ def main():
                      "placement": main_run["placement"]},
         "input_rate_frac_of_peak": round(value / world / HBM_PEAK_GBS, 4),
     }
+    if probe:
+        # this device's practical HBM rates, measured in this run (SURVEY
+        # 8(d)): the dominant kernel against a plain streaming kernel of the
+        # same read:write shape
+        result["hbm_probe"] = probe
+        result["roofline"]["probed_ceiling_same_shape"] = probe["copy_third_bus_gbs"]
+        result["roofline"]["frac_of_probed_ceiling"] = round(
+            achieved / probe["copy_third_bus_gbs"], 4)
     if side:
         # the downsample alone (no level-0 tile split): reads each frame once
         # and writes 1/3 of it; its input rate against the HBM read peak is
@@ -628,12 +659,18 @@ def main():
             "value": round(side["value"], 2), "unit": "GB/s",
             "kernel_avg_ms": round(side["avg_ms"], 5),
             "achieved": round(side["achieved"], 1),
-            "input_rate_frac_of_peak": round(side["value"] / world / HBM_PEAK_GBS, 4),
-            # the same shape's probed ceiling on a plain streaming kernel
-            "probed_ceiling_input_gbs": PYR_PROBE_READ_GBS,
-            "input_rate_frac_of_probed_ceiling": round(
-                side["value"] / world / PYR_PROBE_READ_GBS, 4),
-            "probed_ceiling_source": "profiles/r02_copy_probe.txt read+1/3w ntl"}
+            "input_rate_frac_of_peak": round(side["value"] / world / HBM_PEAK_GBS, 4)}
+        if probe:
+            # the same shape's ceiling on a plain streaming kernel, this run
+            pr = probe["read_third_input_gbs"]
+            result["pyramid_only"].update({
+                "probed_ceiling_input_gbs": pr,
+                "input_rate_frac_of_probed_ceiling": round(side["value"] / world / pr, 4),
+                # kernel time only (no launch gaps): input bytes per launch
+                # over the event-timed launch duration
+                "kernel_input_frac_of_probed_ceiling": round(
+                    B * side["fbytes"] / (side["avg_ms"] * 1e-3) / 1e9 / pr, 4),
+                "probed_ceiling_source": "hbm_probe.read_third_input_gbs"})
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:

@@ -66,6 +66,31 @@ aqz_status aqz_stage_placement(const aqz_stage* st, double* ms, size_t cap,
 aqz_status aqz_stage_host_affinity(const aqz_stage* st, int32_t* numa_node,
                                    uint32_t* n_cpus);
 
+/* Streaming probe of this device's practical HBM rates, for the access
+ * shapes the stage runs ("verify on the box with a read-only
+ * stream kernel, and report the measured practical peak").  Every
+ * workgroup streams one contiguous 24 KiB block with 16-B lane accesses
+ * (nontemporal loads, nontemporal stores) over a source ring of 4 x bytes:
+ *   AQZ_PROBE_READ         read only
+ *   AQZ_PROBE_COPY         1 read : 1 write
+ *   AQZ_PROBE_COPY_THIRD   1 read : 4/3 write (the full stage)
+ *   AQZ_PROBE_READ_THIRD   1 read : 1/3 write (the pyramid-only stage)
+ * | AQZ_PROBE_PLAIN_STORES: plain instead of nontemporal stores (which of
+ * the two is faster depends on the shape; a ceiling is the better one).
+ * ms = mean launch time over reps launches (after 3 warm-ups) on device
+ * `device`; read_bytes = bytes read per launch (<= bytes).  Allocates and
+ * frees ~6 x bytes of device memory. */
+enum
+{
+    AQZ_PROBE_READ = 0,
+    AQZ_PROBE_COPY = 1,
+    AQZ_PROBE_COPY_THIRD = 2,
+    AQZ_PROBE_READ_THIRD = 3,
+    AQZ_PROBE_PLAIN_STORES = 0x100
+};
+aqz_status aqz_probe_hbm(int32_t device, int32_t shape, uint64_t bytes, uint32_t reps,
+                         double* ms, uint64_t* read_bytes);
+
 #ifdef __cplusplus
 }
 #endif

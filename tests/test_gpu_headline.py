@@ -182,3 +182,19 @@ def test_bench_two_ranks_self_launched(gpu):
     assert len(lines) == 1, r.stdout
     d = lines[0]
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["value"] > 0
+
+
+def test_hbm_probe_shapes(gpu):
+    """The live streaming probe the bench reports its ceilings from
+    (aqz_probe_hbm): every shape runs, reads what it says, and lands in a
+    plausible band for one MI355X (0.5-8.5 TB/s of bus); bad shapes are
+    refused."""
+    for shape, wr in ((gpu.PROBE_READ, 0.0), (gpu.PROBE_COPY, 1.0),
+                      (gpu.PROBE_COPY_THIRD, 4 / 3), (gpu.PROBE_READ_THIRD, 1 / 3),
+                      (gpu.PROBE_COPY | gpu.PROBE_PLAIN_STORES, 1.0)):
+        ms, rd = gpu.probe_hbm(shape, 256 << 20, 5)
+        assert 0 < rd <= 256 << 20 and rd > 255 << 20
+        bus = rd * (1 + wr) / (ms * 1e-3) / 1e9
+        assert 500 < bus < 8500, (shape, bus)
+    with pytest.raises(gpu.AqzError):
+        gpu.probe_hbm(7, 1 << 20, 1)
