@@ -10,7 +10,7 @@ TAG=${2:-r02}
 # calibration launches (<= 24, same kernel) move the average by < 1%
 STEPS=${STEPS:-200}
 NAME=$CFG
-EXTRA="--no-cpu-baseline --no-pyramid-only-line"
+EXTRA="--no-cpu-baseline --no-pyramid-only-line --no-hbm-probe"
 if [ "$3" = "pyr" ]; then NAME=$CFG-pyr; EXTRA="$EXTRA --pyramid-only"; fi
 OUT=gpurun_out/prof_${TAG}_${NAME}
 mkdir -p $OUT
