@@ -713,8 +713,10 @@ shuffle_blocks(const ShuffleParams p)
 //                streams, one wave each (lane-parallel bit packing: each lane
 //                owns a run of literals, a suffix scan of their bit counts
 //                places it -- a stream is written last literal first); the
-//                sequences bitstream (one lane, backwards); compressed iff
-//                smaller than the block counted with the tree
+//                sequences pre-coded (codes + extra bits) and compacted
+//   zstd_seqenc  one lane per block: the sequences' FSE bitstream
+//                (backwards); compressed iff smaller than the block counted
+//                with the tree
 //   zstd_segment per segment: which block carries the tree, block offsets,
 //                frame bytes; a blosc record larger than its block is raw
 //   zstd_chunk   per chunk: blosc record offsets / memcpyed rule, frame bytes
@@ -1069,8 +1071,11 @@ zseq_encode(const zstd::SeqTables& t, const uint64_t* sv, uint32_t n, uint8_t* o
     w.add((v >> 17) & 0xFFFFu, zstd::ll_bits(llc));
     w.add((v >> 33) & 0xFFFFu, zstd::ml_bits(mlc));
     w.add(v >> 49, ofc);
+    uint64_t nx = n >= 2 ? sv[n - 2] : 0;
     for (int i = int(n) - 2; i >= 0; --i) {
-        v = sv[i];
+        v = nx;
+        if (i > 0)
+            nx = sv[i - 1]; // in flight while this sequence is coded
         llc = uint32_t(v & 63u);
         mlc = uint32_t((v >> 6) & 63u);
         ofc = uint32_t((v >> 12) & 31u);
@@ -1115,8 +1120,7 @@ zstd_encode(const ZstdParams p)
     __shared__ int32_t rle;
     __shared__ uint32_t ssz[4];
     __shared__ uint32_t pre[kZSubBlocks + 1], spre[kZSubBlocks + 1], carry[kZSubBlocks];
-    __shared__ uint32_t dec[4]; // kind, literal type, literal payload, sequence bytes
-    __shared__ zstd::SeqTables seqt;
+    __shared__ uint32_t dec[4]; // literal section bytes, literal type, literal payload
     const uint32_t g = blockIdx.x, t = threadIdx.x;
     const ZBlock z = zblock(p, g);
     if (z.len == 0 || zchunk_skip(p, z.c)) {
@@ -1144,9 +1148,6 @@ zstd_encode(const ZstdParams p)
             }
         }
     }
-    if (p.match)
-        for (uint32_t i = t; i < sizeof(zstd::SeqTables) / 4; i += 256)
-            reinterpret_cast<uint32_t*>(&seqt)[i] = reinterpret_cast<const uint32_t*>(p.seqt)[i];
     __syncthreads();
     const uint32_t nl = pre[kZSubBlocks], nseq = spre[kZSubBlocks];
     if (nl > 0 && p.hist[uint64_t(g) * 256 + t] == nl)
@@ -1272,50 +1273,90 @@ zstd_encode(const ZstdParams p)
         for (uint32_t i = t; i < nl; i += 256)
             d[i] = lit(i);
     }
-    __syncthreads(); // the stream buffers are free from here
-    // the block's sequences staged in LDS with their codes and extra bits,
-    // so the one serial lane only runs the FSE states and the bit packing
-    uint64_t* sv = reinterpret_cast<uint64_t*>(zbuf);
-    uint8_t* so = reinterpret_cast<uint8_t*>(sv + kZSubBlocks * kZSubSeq);
-    const uint32_t so_cap = uint32_t(sizeof(zbuf) - kZSubBlocks * kZSubSeq * 8);
-    if (nseq) {
-        const uint64_t* gs = p.seqs + uint64_t(g) * kZSubBlocks * kZSubSeq;
-        for (uint32_t i = t; i < nseq; i += 256) {
+    // the sequences: pre-coded (codes + extra bits, one word each) and
+    // compacted in place into the block's first sequence slots; the FSE
+    // bitstream is built by zstd_seqenc, one lane per block
+    if (nseq == 0) {
+        if (t == 0) {
+            d[lpay] = 0; // sequence section header: no sequences
+            p.bkind[g] = 2;
+            p.bltype[g] = uint8_t(ltype);
+            p.bpay[g] = lpay;
+            p.bseqb[g] = 1;
+            p.bnlit[g] = nl;
+        }
+        return;
+    }
+    static_assert(kZSubBlocks * kZSubSeq <= 512, "two sequences per thread");
+    uint64_t* gs = p.seqs + uint64_t(g) * kZSubBlocks * kZSubSeq;
+    uint64_t cw[2] = { 0, 0 };
+#pragma unroll
+    for (uint32_t j = 0; j < 2; ++j) {
+        const uint32_t i = t + 256 * j;
+        if (i < nseq) {
             uint32_t k = 0;
             while (k + 1 < kZSubBlocks && spre[k + 1] <= i)
                 ++k;
             zstd::Seq v = zstd::unpack_seq(gs[uint64_t(k) * kZSubSeq + (i - spre[k])]);
             if (i == spre[k])
                 v.lit += carry[k];
-            sv[i] = zseq_codes(v);
+            cw[j] = zseq_codes(v);
         }
     }
-    __syncthreads();
+    __syncthreads(); // every slot read before any is overwritten
+#pragma unroll
+    for (uint32_t j = 0; j < 2; ++j)
+        if (t + 256 * j < nseq)
+            gs[t + 256 * j] = cw[j];
     if (t == 0) {
-        uint32_t sq = zstd::write_seq_header(so, nseq);
-        if (nseq) {
-            const uint32_t bits = zseq_encode(seqt, sv, nseq, so + sq, so_cap - sq);
-            sq = bits ? sq + bits : 0;
-        }
-        dec[3] = (sq != 0 && lpay + sq <= zstd::kBlock && lsec + sq < z.len) ? sq : 0;
-    }
-    __syncthreads();
-    const uint32_t sq = dec[3];
-    if (sq == 0) {
-        if (t == 0)
-            p.bkind[g] = 0;
-        return;
-    }
-    for (uint32_t i = t; i < sq; i += 256)
-        d[lpay + i] = so[i];
-    if (t == 0) {
-        p.bkind[g] = 2;
+        p.bkind[g] = 4; // sequences pending (zstd_seqenc)
         p.bltype[g] = uint8_t(ltype);
         p.bpay[g] = lpay;
-        p.bseqb[g] = sq;
+        p.bseqb[g] = nseq;
         p.bnlit[g] = nl;
     }
 }
+
+// The FSE sequence bitstream of every block with pending sequences, one
+// lane per block: the state chain is serial within a block, so 64 blocks
+// advance together per wave instead of one lane per 256-thread workgroup.
+// The predefined tables sit in LDS; each lane reads its block's pre-coded
+// sequences (last first, one ahead) and writes the bitstream after the
+// block's literal payload in scratch.  Then the block's kind: compressed
+// iff the whole block (literal section + sequences) beats raw.
+__global__ __launch_bounds__(64) void
+zstd_seqenc(const ZstdParams p)
+{
+    __shared__ zstd::SeqTables seqt;
+    for (uint32_t i = threadIdx.x; i < sizeof(zstd::SeqTables) / 4; i += 64)
+        reinterpret_cast<uint32_t*>(&seqt)[i] = reinterpret_cast<const uint32_t*>(p.seqt)[i];
+    __syncthreads();
+    const uint64_t g = uint64_t(blockIdx.x) * 64 + threadIdx.x;
+    if (g >= uint64_t(p.n_chunks) * p.nseg * p.bps || p.bkind[g] != 4)
+        return;
+    const ZBlock z = zblock(p, uint32_t(g));
+    const uint32_t nseq = p.bseqb[g], lpay = p.bpay[g], nl = p.bnlit[g];
+    uint32_t lsec;
+    if (p.bltype[g] == 2) {
+        const uint32_t wt = p.tab[z.seg].tree_n + lpay;
+        lsec = zstd::lit_header_huf_bytes(nl, wt) + wt;
+    } else {
+        lsec = zstd::lit_header_raw_bytes(nl) + nl;
+    }
+    uint8_t* so = p.scratch + g * zstd::kBlock + lpay;
+    const uint32_t cap = zstd::kBlock - lpay;
+    uint32_t sq = zstd::write_seq_header(so, nseq);
+    const uint32_t bits = zseq_encode(seqt, p.seqs + g * kZSubBlocks * kZSubSeq, nseq,
+                                      so + sq, cap > sq ? cap - sq : 0);
+    sq = bits ? sq + bits : 0;
+    if (sq != 0 && lsec + sq < z.len) {
+        p.bkind[g] = 2;
+        p.bseqb[g] = sq;
+    } else {
+        p.bkind[g] = 0;
+    }
+}
+
 
 __global__ __launch_bounds__(64) void
 zstd_segment(const ZstdParams p)
@@ -1525,6 +1566,9 @@ launch_zstd(const ZstdParams& p, hipStream_t stream)
         }
         hipLaunchKernelGGL(zstd_table, dim3(uint32_t(nseg)), dim3(64), 0, stream, p);
         hipLaunchKernelGGL(zstd_encode, dim3(uint32_t(nblk)), dim3(256), 0, stream, p);
+        if (p.match)
+            hipLaunchKernelGGL(zstd_seqenc, dim3(uint32_t((nblk + 63) / 64)), dim3(64), 0,
+                               stream, p);
         hipLaunchKernelGGL(zstd_segment, dim3(uint32_t(nseg)), dim3(64), 0, stream, p);
     }
     hipLaunchKernelGGL(zstd_chunk, dim3(p.n_chunks), dim3(256), 0, stream, p);
