@@ -135,6 +135,7 @@ struct ZstdParams
     uint32_t* snseq, *snlit, *stail;
     // per zstd block ([n_chunks * nseg * bps])
     uint32_t* hist;         // [.. * 256] literal histogram
+    uint32_t* shist;        // per segment [nseg * 256] (segments of > 32 blocks)
     uint8_t* bkind;         // 0 raw, 1 RLE, 2 compressed, 3 none, 4 sequences pending
     uint8_t* bltype;        // compressed: literals 0 raw, 2 Huffman
     uint32_t* bpay;         // compressed: literal payload bytes; RLE: the byte

@@ -973,6 +973,26 @@ zstd_hist(const ZstdParams p)
     p.hist[uint64_t(g) * 256 + t] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
 }
 
+// Segments of many blocks (plain zstd: a whole chunk, 1024 blocks of a
+// C2 chunk): their literal histograms summed in parallel, kSegHistBlocks
+// blocks per workgroup, into shist (zeroed by the launcher).
+constexpr uint32_t kSegHistBlocks = 32;
+
+__global__ __launch_bounds__(256) void
+zstd_seghist(const ZstdParams p)
+{
+    const uint32_t s = blockIdx.x, t = threadIdx.x;
+    if (zchunk_skip(p, s / p.nseg))
+        return;
+    const uint32_t b0 = blockIdx.y * kSegHistBlocks;
+    const uint32_t b1 = min(p.bps, b0 + kSegHistBlocks);
+    uint32_t a = 0;
+    for (uint32_t b = b0; b < b1; ++b)
+        a += p.hist[(uint64_t(s) * p.bps + b) * 256 + t];
+    if (a)
+        atomicAdd(&p.shist[uint64_t(s) * 256 + t], a);
+}
+
 __global__ __launch_bounds__(64) void
 zstd_table(const ZstdParams p)
 {
@@ -991,8 +1011,11 @@ zstd_table(const ZstdParams p)
     __syncthreads();
     for (uint32_t k = t; k < 256; k += 64) {
         uint32_t a = 0;
-        for (uint32_t b = 0; b < p.bps; ++b)
-            a += p.hist[(uint64_t(s) * p.bps + b) * 256 + k];
+        if (p.bps > kSegHistBlocks)
+            a = p.shist[uint64_t(s) * 256 + k];
+        else
+            for (uint32_t b = 0; b < p.bps; ++b)
+                a += p.hist[(uint64_t(s) * p.bps + b) * 256 + k];
         w.cnt[k] = a;
         key[k] = uint64_t(a) << 8 | k;
         len[k] = 0;
@@ -1358,47 +1381,68 @@ zstd_seqenc(const ZstdParams p)
 }
 
 
+// One wave per segment: the block carrying the tree (the first Huffman
+// block), each block's bytes, their offsets (a wave scan, 64 blocks per
+// step) and the frame size.
 __global__ __launch_bounds__(64) void
 zstd_segment(const ZstdParams p)
 {
-    const uint32_t s = blockIdx.x;
-    if (threadIdx.x != 0)
-        return;
+    const uint32_t s = blockIdx.x, lane = threadIdx.x;
     if (zchunk_skip(p, s / p.nseg)) {
-        p.ssize[s] = 0;
+        if (lane == 0)
+            p.ssize[s] = 0;
         return;
     }
     const ZBlock z0 = zblock(p, s * p.bps);
     const uint32_t tree_n = p.tab[s].tree_n;
-    uint32_t carrier = ~0u, pos = 0;
-    for (uint32_t b = 0; b < z0.nb; ++b) {
-        const uint32_t g = s * p.bps + b;
-        const uint32_t blen = min(zstd::kBlock, z0.seglen - b * zstd::kBlock);
-        const uint32_t k = p.bkind[g];
+    uint32_t carrier = ~0u;
+    for (uint32_t b0 = 0; b0 < z0.nb && carrier == ~0u; b0 += 64) {
+        const uint32_t b = b0 + lane;
+        const bool huf = b < z0.nb && p.bkind[s * p.bps + b] == 2 &&
+                         p.bltype[s * p.bps + b] == 2;
+        const uint64_t m = __ballot(huf);
+        if (m)
+            carrier = b0 + uint32_t(__ffsll(static_cast<long long>(m))) - 1;
+    }
+    uint32_t pos = 0;
+    for (uint32_t b0 = 0; b0 < z0.nb; b0 += 64) {
+        const uint32_t b = b0 + lane;
         uint32_t sz = 0;
-        if (k == 0) {
-            sz = 3 + blen;
-        } else if (k == 1) {
-            sz = 4;
-        } else if (k == 2) {
-            const uint32_t nl = p.bnlit[g];
-            if (p.bltype[g] == 2) {
-                if (carrier == ~0u)
-                    carrier = b;
-                const uint32_t cs = p.bpay[g] + (carrier == b ? tree_n : 0);
-                sz = 3 + zstd::lit_header_huf_bytes(nl, cs) + cs + p.bseqb[g];
-            } else {
-                sz = 3 + zstd::lit_header_raw_bytes(nl) + nl + p.bseqb[g];
+        if (b < z0.nb) {
+            const uint32_t g = s * p.bps + b;
+            const uint32_t blen = min(zstd::kBlock, z0.seglen - b * zstd::kBlock);
+            const uint32_t k = p.bkind[g];
+            if (k == 0) {
+                sz = 3 + blen;
+            } else if (k == 1) {
+                sz = 4;
+            } else if (k == 2) {
+                const uint32_t nl = p.bnlit[g];
+                if (p.bltype[g] == 2) {
+                    const uint32_t cs = p.bpay[g] + (carrier == b ? tree_n : 0);
+                    sz = 3 + zstd::lit_header_huf_bytes(nl, cs) + cs + p.bseqb[g];
+                } else {
+                    sz = 3 + zstd::lit_header_raw_bytes(nl) + nl + p.bseqb[g];
+                }
             }
         }
-        p.bpos[g] = pos;
-        pos += sz;
+        uint32_t x = sz; // inclusive prefix sum over the wave
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d);
+            if (lane >= uint32_t(d))
+                x += y;
+        }
+        if (b < z0.nb)
+            p.bpos[s * p.bps + b] = pos + x - sz;
+        pos += __shfl(x, 63);
     }
-    p.carrier[s] = carrier;
-    const uint32_t frame = zstd::frame_header_bytes(z0.seglen) + pos;
-    const bool raw = p.blosc && frame >= z0.seglen;
-    p.sraw[s] = raw ? 1 : 0;
-    p.ssize[s] = raw ? z0.seglen : frame;
+    if (lane == 0) {
+        p.carrier[s] = carrier;
+        const uint32_t frame = zstd::frame_header_bytes(z0.seglen) + pos;
+        const bool raw = p.blosc && frame >= z0.seglen;
+        p.sraw[s] = raw ? 1 : 0;
+        p.ssize[s] = raw ? z0.seglen : frame;
+    }
 }
 
 __global__ __launch_bounds__(256) void
@@ -1563,6 +1607,14 @@ launch_zstd(const ZstdParams& p, hipStream_t stream)
                                stream, p);
         } else {
             hipLaunchKernelGGL(zstd_hist, dim3(uint32_t(nblk)), dim3(256), 0, stream, p);
+        }
+        if (p.bps > kSegHistBlocks) {
+            hipError_t e = hipMemsetAsync(p.shist, 0, nseg * 256 * 4, stream);
+            if (e != hipSuccess)
+                return e;
+            hipLaunchKernelGGL(zstd_seghist,
+                               dim3(uint32_t(nseg), (p.bps + kSegHistBlocks - 1) / kSegHistBlocks),
+                               dim3(256), 0, stream, p);
         }
         hipLaunchKernelGGL(zstd_table, dim3(uint32_t(nseg)), dim3(64), 0, stream, p);
         hipLaunchKernelGGL(zstd_encode, dim3(uint32_t(nblk)), dim3(256), 0, stream, p);

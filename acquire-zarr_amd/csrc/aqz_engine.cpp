@@ -1684,6 +1684,7 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
         bseqb_.alloc(nblk * 4);
         bnlit_.alloc(nblk * 4);
         hist_.alloc(nblk * 256 * 4);
+        shist_.alloc(nseg * 256 * 4);
         bkind_.alloc(nblk);
         bpay_.alloc(nblk * 4);
         bpos_.alloc(nblk * 4);
@@ -1707,6 +1708,7 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
     p.bseqb = reinterpret_cast<uint32_t*>(bseqb_.p);
     p.bnlit = reinterpret_cast<uint32_t*>(bnlit_.p);
     p.hist = reinterpret_cast<uint32_t*>(hist_.p);
+    p.shist = reinterpret_cast<uint32_t*>(shist_.p);
     p.bkind = bkind_.p;
     p.bpay = reinterpret_cast<uint32_t*>(bpay_.p);
     p.bpos = reinterpret_cast<uint32_t*>(bpos_.p);

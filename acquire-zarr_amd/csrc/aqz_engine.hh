@@ -121,7 +121,7 @@ class Compressor
     uint64_t device_bytes() const
     {
         uint64_t n = scratch_.n + ssize_.n + spos_.n + fsize_.n + mode_.n + cstart_.n;
-        for (const DevBuf* b : { &zin_, &hist_, &bkind_, &bpay_, &bpos_, &tab_, &carrier_,
+        for (const DevBuf* b : { &zin_, &hist_, &shist_, &bkind_, &bpay_, &bpos_, &tab_, &carrier_,
                                  &sraw_, &lits_, &seqs_, &snseq_, &snlit_, &stail_, &bltype_,
                                  &bseqb_, &bnlit_, &seqt_ })
             n += b->n;
@@ -138,7 +138,7 @@ class Compressor
     BloscGeom g_{};
     bool store_only_;
     DevBuf scratch_, ssize_, spos_, fsize_, mode_, cstart_;
-    DevBuf zin_, hist_, bkind_, bpay_, bpos_, tab_, carrier_, sraw_; // zstd
+    DevBuf zin_, hist_, shist_, bkind_, bpay_, bpos_, tab_, carrier_, sraw_; // zstd
     DevBuf lits_, seqs_, snseq_, snlit_, stail_, bltype_, bseqb_, bnlit_, seqt_;
 };
 
