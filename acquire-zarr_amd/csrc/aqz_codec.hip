@@ -783,25 +783,62 @@ zstd_parse(const ZstdParams p)
     }
     const uint8_t* src = zblock_src(p, z) + so;
     uint8_t* sb = reinterpret_cast<uint8_t*>(sw);
-    if ((reinterpret_cast<uintptr_t>(src) & 3u) == 0) {
-        const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
-        for (uint32_t w = lane; w < L / 4; w += 64)
-            sw[w] = s4[w];
-        for (uint32_t i = (L & ~3u) + lane; i < L; i += 64)
-            sb[i] = src[i];
-    } else {
-        for (uint32_t i = lane; i < L; i += 64)
-            sb[i] = src[i];
-    }
-    for (uint32_t i = L + lane; i < L + 8; i += 64)
-        sb[i] = 0;
     for (uint32_t b = lane; b < 256; b += 64)
         lh[b] = 0;
     for (uint32_t i = lane; i < kHashSize / 2; i += 64)
         reinterpret_cast<uint32_t*>(table)[i] = 0;
-    __syncthreads();
-    for (uint32_t i = lane; i < L; i += 64)
-        atomicAdd(&lh[sb[i]], 1u);
+    const bool whole = L == kZSub && (reinterpret_cast<uintptr_t>(src) & 15u) == 0;
+    if (whole) {
+        // lane l holds bytes [64l, 64l + 64): staged to LDS and counted from
+        // registers, one LDS atomic per run of equal bytes (the high byte
+        // planes of shuffled camera data are long runs; per-byte atomics on
+        // them serialised on one address)
+        const uint4* s16 = reinterpret_cast<const uint4*>(src) + 4 * lane;
+        uint4 r[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            r[j] = s16[j];
+        __syncthreads(); // lh zeroed
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            reinterpret_cast<uint4*>(sw)[4 * lane + j] = r[j];
+        uint32_t cur = r[0].x & 255u, run = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t wd[4] = { r[j].x, r[j].y, r[j].z, r[j].w };
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t v = (wd[k] >> (8 * b)) & 255u;
+                    if (v != cur) {
+                        atomicAdd(&lh[cur], run);
+                        cur = v;
+                        run = 0;
+                    }
+                    ++run;
+                }
+        }
+        atomicAdd(&lh[cur], run);
+        if (lane < 2)
+            sw[kZSub / 4 + lane] = 0;
+    } else {
+        if ((reinterpret_cast<uintptr_t>(src) & 3u) == 0) {
+            const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
+            for (uint32_t w = lane; w < L / 4; w += 64)
+                sw[w] = s4[w];
+            for (uint32_t i = (L & ~3u) + lane; i < L; i += 64)
+                sb[i] = src[i];
+        } else {
+            for (uint32_t i = lane; i < L; i += 64)
+                sb[i] = src[i];
+        }
+        for (uint32_t i = L + lane; i < L + 8; i += 64)
+            sb[i] = 0;
+        __syncthreads();
+        for (uint32_t i = lane; i < L; i += 64)
+            atomicAdd(&lh[sb[i]], 1u);
+    }
     __syncthreads();
     float e = 0.f;
     for (uint32_t b = lane; b < 256; b += 64)
@@ -812,10 +849,8 @@ zstd_parse(const ZstdParams p)
     for (int d = 32; d > 0; d >>= 1)
         e += __shfl_xor(e, d);
     const uint32_t minlen = zstd::min_match(e, kLenCap);
-    __syncthreads();
-    for (uint32_t b = lane; b < 256; b += 64)
-        lh[b] = 0;
-    __syncthreads();
+    // lh keeps the unit's byte histogram: it is the literal histogram
+    // when the parse finds no sequence
 
     // greedy parse: probe four 64-position windows, walk the matches
     uint32_t nseq = 0, anchor = 0, p0 = 0, misses = 0;
@@ -910,6 +945,29 @@ zstd_parse(const ZstdParams p)
     __syncthreads();
     // literal runs -> the unit's literal slot, and their histogram
     uint8_t* lo = p.lits + uint64_t(q) * kZSub;
+    if (nseq == 0) {
+        // every byte is a literal: the unit's histogram is the literal one
+        if (whole) {
+            for (uint32_t w = lane; w < kZSub / 16; w += 64)
+                reinterpret_cast<uint4*>(lo)[w] = reinterpret_cast<const uint4*>(sw)[w];
+        } else {
+            for (uint32_t i = lane; i < L; i += 64)
+                lo[i] = sb[i];
+        }
+        __syncthreads();
+        for (uint32_t b = lane; b < 256; b += 64)
+            if (lh[b])
+                atomicAdd(&p.hist[uint64_t(g) * 256 + b], lh[b]);
+        if (lane == 0) {
+            p.snseq[q] = 0;
+            p.snlit[q] = L;
+            p.stail[q] = L;
+        }
+        return;
+    }
+    for (uint32_t b = lane; b < 256; b += 64)
+        lh[b] = 0;
+    __syncthreads();
     uint32_t at = 0, pos = 0;
     for (uint32_t s = 0; s < nseq; ++s) {
         const zstd::Seq v = zstd::unpack_seq(sseq[s]);
