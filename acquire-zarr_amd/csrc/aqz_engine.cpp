@@ -457,13 +457,14 @@ Stage::place_level(StageLevel& L)
 // three bands (C2: 0.39 / 0.41 / 0.43 ms, profiles/r02_va_probe.txt; the
 // same virtual addresses land in different bands), so the search stops
 // early only once the spread shows the fast band (>= 12% better than the
-// slowest seen).  A candidate costs a few ms.  Only for large rings
+// slowest seen; one C2 bench run found it only at the 9th candidate).  A
+// candidate costs a few ms and holds its rings until the search ends.  Only for large rings
 // (>= 256 MiB), where the stage is a long-lived streaming engine.
-// AQZ_PLACEMENT_TRIES (default 10; 1 = off).
+// AQZ_PLACEMENT_TRIES (default 16; 1 = off).
 void
 Stage::calibrate_placement()
 {
-    uint32_t tries = 10;
+    uint32_t tries = 16;
     if (const char* e = std::getenv("AQZ_PLACEMENT_TRIES"))
         tries = uint32_t(std::max(1, std::atoi(e)));
     uint64_t ring_bytes = 0;
