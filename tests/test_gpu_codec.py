@@ -221,3 +221,29 @@ def test_stage_shards_from_device_frames(gpu):
                 assert oracle_decode(fr) == w, (l, row, s, i)
                 checked += 1
     assert checked > 0
+
+
+def test_compressed_handoff_pinned_and_pageable(gpu):
+    """aqz_stage_copy_compressed_async into pinned memory of the codec bound
+    (aqz_compressor_max_bytes) gives the same bytes as into pageable memory,
+    for lz4, blosc-zstd and zstd, and writes nothing past the frames."""
+    dims = [(TIME, 0, 4, 1), (SPACE, 256, 64, 1), (SPACE, 192, 64, 1)]
+    frames = synthetic_frames(U16, 4, 256, 192, 12)
+    frames[:, :64] = 0  # chunks without data
+    for codec, shuffle in ((1, 1), (2, 2), (3, 0)):
+        st = gpu.Stage(dims, U16, MEAN, layer_slots=2, max_batch_frames=4)
+        st.append(np.ascontiguousarray(frames))
+        lay = st.layout(0)
+        st.compress_layer(0, 0, codec=codec, clevel=5, shuffle=shuffle)
+        bound = gpu.lib().aqz_compressor_max_bytes(lay["bytes_per_chunk"],
+                                                   lay["chunks_per_layer"])
+        pinned = gpu.HostBuffer(bound)
+        pinned.array[:] = 0xAB
+        st.copy_compressed_async(0, 0, pinned.ptr, bound)
+        st.wait_copies()
+        ref, off = st.copy_compressed(0, 0)  # into pageable memory
+        total = int(off[-1])
+        assert total > 0
+        assert np.array_equal(pinned.array[:total], ref), codec
+        assert (pinned.array[total:total + 64] == 0xAB).all()  # nothing past the frames
+        st.close()
