@@ -347,6 +347,29 @@ def test_stage_c4_volume(gpu, monkeypatch, kernel):
     _check_stage(gpu, dims, U16, MEAN, frames, batch=32)
 
 
+@pytest.mark.parametrize("kernel", sorted(KERNELS_3D))
+@pytest.mark.parametrize("dims,levels", [
+    # 2 levels (one fused level, G = 2); 512 px: a u8 region is 512 px wide
+    ([(TIME, 0, 1, 1), (SPACE, 8, 4, 1), (SPACE, 512, 256, 1), (SPACE, 512, 256, 1)], 2),
+    # 3 levels (two fused levels, G = 4)
+    ([(TIME, 0, 1, 1), (SPACE, 8, 2, 1), (SPACE, 1024, 256, 1), (SPACE, 1024, 256, 1)], 3),
+], ids=["2lvl", "3lvl"])
+def test_stage_3d_shallow(gpu, monkeypatch, kernel, dims, levels):
+    """Shallow 2x2x2 pyramids (1 or 2 fused levels) through every 2x2x2
+    kernel: the strip kernel's early exits after level 1 / level 2."""
+    knobs, name = KERNELS_3D[kernel]
+    monkeypatch.setenv("AQZ_KNOBS", knobs)
+    h = dims[-2][1]
+    for dtype in (U8, U16, F32):
+        st = gpu.Stage(dims, dtype, MEAN)
+        assert st.dominant_kernel() == name
+        assert st.n_levels() == levels
+        st.close()
+        for m in ALL_METHODS:
+            frames = _frames(dtype, 16, h, h, 7 + m + dtype)
+            _check_stage(gpu, dims, dtype, m, frames, batch=8)
+
+
 @pytest.mark.parametrize("dtype", [U8, U16, F32], ids=lambda d: DTYPE_NAMES[d])
 def test_stage_3d_five_levels(gpu, dtype):
     """Five levels (four fused: xy 1024 -> 64 with 64-px chunks), z halving
