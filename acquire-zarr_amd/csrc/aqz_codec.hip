@@ -602,13 +602,15 @@ write_frames(const BloscParams p)
     copy_bytes(rec + 4, p.scratch + uint64_t(gid) * p.g.slot, n);
 }
 
-// One workgroup per (block, chunk): the c-blosc 1.x byte shuffle (byte jj
-// of element i -> jj * ne + i) or bitshuffle (bit b of byte jj of element
-// 8m + k -> bit k of byte m of plane 8 jj + b) of one block.
+// One workgroup per (block, chunk, part): the c-blosc 1.x byte shuffle (byte
+// jj of element i -> jj * ne + i) or bitshuffle (bit b of byte jj of element
+// 8m + k -> bit k of byte m of plane 8 jj + b) of one block, the block's
+// elements split over gridDim.z parts (small layers: enough workgroups to
+// keep the loads in flight).  The scalar fallbacks run in part 0.
 __global__ __launch_bounds__(256) void
 shuffle_blocks(const ShuffleParams p)
 {
-    const uint32_t j = blockIdx.x, c = blockIdx.y;
+    const uint32_t j = blockIdx.x, c = blockIdx.y, part = blockIdx.z, np = gridDim.z;
     if (p.flags && p.flags[c] != p.tag)
         return;
     const uint32_t t = threadIdx.x;
@@ -628,21 +630,23 @@ shuffle_blocks(const ShuffleParams p)
             const uint32_t vec = 16 / ts; // elements per 16-B load
             const bool dst_ok = (reinterpret_cast<uintptr_t>(dst) % vec) == 0 && ne % vec == 0;
             if (dst_ok) {
-                // batches of 4 rounds: 4 independent 16-B loads per lane in
-                // flight, then their stores
-                const uint32_t nw = ne / vec, rounds = (nw + 255) / 256;
-                for (uint32_t r0 = 0; r0 < rounds; r0 += 4) {
+                // this part's 16-B words, in batches of 4 rounds: 4
+                // independent loads per lane in flight, then their stores
+                const uint32_t nw = ne / vec;
+                const uint32_t lo = uint32_t(uint64_t(nw) * part / np);
+                const uint32_t hi = uint32_t(uint64_t(nw) * (part + 1) / np);
+                for (uint32_t w0 = lo; w0 < hi; w0 += 4 * 256) {
                     uint4 v[4];
 #pragma unroll
                     for (uint32_t u = 0; u < 4; ++u) {
-                        const uint32_t w = (r0 + u) * 256 + t;
-                        if (r0 + u < rounds && w < nw)
+                        const uint32_t w = w0 + u * 256 + t;
+                        if (w < hi)
                             v[u] = *reinterpret_cast<const uint4*>(src + 16ull * w);
                     }
 #pragma unroll
                     for (uint32_t u = 0; u < 4; ++u) {
-                        const uint32_t w = (r0 + u) * 256 + t;
-                        if (!(r0 + u < rounds && w < nw))
+                        const uint32_t w = w0 + u * 256 + t;
+                        if (w >= hi)
                             continue;
                         uint8_t e[16];
                         __builtin_memcpy(e, &v[u], 16);
@@ -670,6 +674,8 @@ shuffle_blocks(const ShuffleParams p)
                 done = ne;
             }
         }
+        if (part != 0)
+            return;
         for (uint32_t x = t; x < (ne - done) * ts; x += 256) {
             const uint32_t i = done + x / ts, jj = x % ts;
             dst[uint64_t(jj) * ne + i] = src[uint64_t(i) * ts + jj];
@@ -680,8 +686,10 @@ shuffle_blocks(const ShuffleParams p)
     }
     if (p.shuffle == 2 && ne % 8 == 0 && ne * ts == bsize) {
         const uint32_t row = ne / 8;
+        const uint32_t lo = uint32_t(uint64_t(row) * part / np);
+        const uint32_t hi = uint32_t(uint64_t(row) * (part + 1) / np);
 #pragma unroll 4
-        for (uint32_t m = t; m < row; m += 256) {
+        for (uint32_t m = lo + t; m < hi; m += 256) {
             const uint8_t* g = src + uint64_t(8) * m * ts; // 8 elements
             for (uint32_t jj = 0; jj < ts; ++jj) {
                 uint64_t x = 0;
@@ -694,6 +702,8 @@ shuffle_blocks(const ShuffleParams p)
         }
         return;
     }
+    if (part != 0)
+        return;
     for (uint32_t x = t; x < bsize; x += 256)
         dst[x] = src[x];
 }
@@ -1626,7 +1636,12 @@ launch_shuffle_blocks(const ShuffleParams& p, hipStream_t stream)
         return hipSuccess;
     if (p.nblocks > 0x7fffffffu || p.n_chunks > 65535u)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(shuffle_blocks, dim3(p.nblocks, p.n_chunks), dim3(256), 0, stream, p);
+    // parts per block: at least ~2048 workgroups in all (a C2 level-1 layer
+    // is 32 blocks x 16 chunks), at most 16
+    const uint64_t wg = uint64_t(p.nblocks) * p.n_chunks;
+    const uint32_t parts = uint32_t(std::min<uint64_t>(16, std::max<uint64_t>(1, (2048 + wg - 1) / wg)));
+    hipLaunchKernelGGL(shuffle_blocks, dim3(p.nblocks, p.n_chunks, parts), dim3(256), 0, stream,
+                       p);
     return hipGetLastError();
 }
 

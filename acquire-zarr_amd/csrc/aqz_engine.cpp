@@ -399,7 +399,23 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
                       "hipStreamCreate");
         }
     }
-    hip_check(hipStreamCreateWithFlags(&comp_, hipStreamNonBlocking), "hipStreamCreate");
+    {
+        // compression stream: normal priority (AQZ_COMP_PRIORITY=1: greatest,
+        // 2: lowest) -- tuning knob
+        const char* e = std::getenv("AQZ_COMP_PRIORITY");
+        const int mode = e ? std::atoi(e) : 0;
+        int least = 0, greatest = 0;
+        hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest),
+                  "hipDeviceGetStreamPriorityRange");
+        for (hipStream_t* cs : { &comp_, &comp_lo_ }) {
+            if (mode == 0)
+                hip_check(hipStreamCreateWithFlags(cs, hipStreamNonBlocking), "hipStreamCreate");
+            else
+                hip_check(hipStreamCreateWithPriority(cs, hipStreamNonBlocking,
+                                                      mode == 2 ? least : greatest),
+                          "hipStreamCreate");
+        }
+    }
     for (auto& L : lv_) {
         hip_check(hipEventCreateWithFlags(&L.ops_ev, hipEventDisableTiming),
                   "hipEventCreate");
@@ -576,7 +592,7 @@ Stage::~Stage()
     zpool_.reset();
     if (stream_)
         (void)hipStreamSynchronize(stream_);
-    for (hipStream_t s : { h2d_, comp_, d2h_ })
+    for (hipStream_t s : { h2d_, comp_, comp_lo_, d2h_ })
         if (s) {
             (void)hipStreamSynchronize(s);
             (void)hipStreamDestroy(s);
@@ -664,6 +680,7 @@ Stage::synchronize()
     hip_check(hipStreamSynchronize(h2d_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(comp_), "hipStreamSynchronize");
+    hip_check(hipStreamSynchronize(comp_lo_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(d2h_), "hipStreamSynchronize");
     retire_consumed(true);
 }
@@ -728,6 +745,7 @@ void
 Stage::wait_copies()
 {
     hip_check(hipStreamSynchronize(comp_), "hipStreamSynchronize");
+    hip_check(hipStreamSynchronize(comp_lo_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(d2h_), "hipStreamSynchronize");
 }
 
@@ -1782,6 +1800,10 @@ void
 Stage::compress_layer_host(StageLevel& L, uint32_t slot, uint64_t layer,
                            const Compression& c)
 {
+    // level 0's layers compress on comp_; the small layers of the other
+    // levels on comp_lo_, overlapping level 0's (their kernels are few
+    // workgroups and latency-bound)
+    const hipStream_t cs = comp_stream(L);
     const ZstdLib& z = ZstdLib::get();
     if (!z.ok)
         throw Error(4, "libzstd.so.1 is not available: no zstd codecs");
@@ -1801,13 +1823,13 @@ Stage::compress_layer_host(StageLevel& L, uint32_t slot, uint64_t layer,
     // device frames of an earlier blosc-lz4 use of the slot may still be
     // on their way out
     if (L.cdone_pending[slot]) {
-        hip_check(hipStreamWaitEvent(comp_, L.cdone_ev[slot], 0), "hipStreamWaitEvent");
+        hip_check(hipStreamWaitEvent(cs, L.cdone_ev[slot], 0), "hipStreamWaitEvent");
         L.cdone_pending[slot] = 0;
     }
     L.h_zin[slot].alloc(L.layer_bytes);
     L.h_zhas[slot].alloc(L.n_chunks);
     hip_check(hipEventRecord(L.ready_ev[slot], stream_), "hipEventRecord");
-    hip_check(hipStreamWaitEvent(comp_, L.ready_ev[slot], 0), "hipStreamWaitEvent");
+    hip_check(hipStreamWaitEvent(cs, L.ready_ev[slot], 0), "hipStreamWaitEvent");
     const uint8_t* chunks = L.ring.p + slot * L.slot_bytes;
     const auto* flags = reinterpret_cast<const uint32_t*>(L.flags.p) + size_t(slot) * L.n_chunks;
     const uint32_t tag = uint32_t(layer / L.n_slots + 1);
@@ -1818,20 +1840,20 @@ Stage::compress_layer_host(StageLevel& L, uint32_t slot, uint64_t layer,
         ShuffleParams sp{ chunks, L.pitch, L.n_chunks, flags, tag, uint32_t(L.bpc),
                           uint32_t(bpp_), uint32_t(c.shuffle), g.blocksize, g.nblocks,
                           L.d_zshuf.p };
-        hip_check(launch_shuffle_blocks(sp, comp_), "shuffle launch");
+        hip_check(launch_shuffle_blocks(sp, cs), "shuffle launch");
         memcpy_pieces(L.h_zin[slot].p, L.d_zshuf.p, L.layer_bytes, hipMemcpyDeviceToHost,
-                      comp_);
+                      cs);
     } else {
         copy_chunks(L.h_zin[slot].p, chunks, L.bpc, L.pitch, L.n_chunks,
-                    hipMemcpyDeviceToHost, comp_);
+                    hipMemcpyDeviceToHost, cs);
     }
     uint8_t* fb = L.flag_bytes.p + size_t(slot) * L.n_chunks;
-    hip_check(launch_flags_to_bytes(flags, fb, L.n_chunks, tag, comp_), "flags launch");
-    hip_check(hipMemcpyAsync(L.h_zhas[slot].p, fb, L.n_chunks, hipMemcpyDeviceToHost, comp_),
+    hip_check(launch_flags_to_bytes(flags, fb, L.n_chunks, tag, cs), "flags launch");
+    hip_check(hipMemcpyAsync(L.h_zhas[slot].p, fb, L.n_chunks, hipMemcpyDeviceToHost, cs),
               "hipMemcpyAsync");
-    hip_check(hipEventRecord(L.zin_ev[slot], comp_), "hipEventRecord");
+    hip_check(hipEventRecord(L.zin_ev[slot], cs), "hipEventRecord");
     // the ring slot is rewritten only after this D2H
-    hip_check(hipEventRecord(L.copy_ev[slot], comp_), "hipEventRecord");
+    hip_check(hipEventRecord(L.copy_ev[slot], cs), "hipEventRecord");
     L.copy_pending[slot] = 1;
 
     HostLayerJob& j = *L.zjob[slot];
@@ -1860,6 +1882,10 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
     if (level >= lv_.size())
         throw Error(3, "level out of range");
     StageLevel& L = lv_[level];
+    // level 0's layers compress on comp_; the small layers of the other
+    // levels on comp_lo_, overlapping level 0's (their kernels are few
+    // workgroups and latency-bound)
+    const hipStream_t cs = comp_stream(L);
     if (!L.ring.p)
         throw Error(1, "level 0 split disabled for this stage");
     const uint32_t slot = uint32_t(layer % L.n_slots);
@@ -1871,7 +1897,7 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
     }
     if (!L.comp || L.comp_cfg.codec != c.codec || L.comp_cfg.clevel != c.clevel ||
         L.comp_cfg.shuffle != c.shuffle) {
-        hip_check(hipStreamSynchronize(comp_), "hipStreamSynchronize");
+        hip_check(hipStreamSynchronize(cs), "hipStreamSynchronize");
         hip_check(hipStreamSynchronize(d2h_), "hipStreamSynchronize");
         L.comp = std::make_unique<Compressor>(L.bpc, uint32_t(bpp_), c);
         L.comp_cfg = c;
@@ -1882,12 +1908,12 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
     L.comp_host[slot] = 0;
     // the slot's previous frames may still be on their way to the host
     if (L.cdone_pending[slot]) {
-        hip_check(hipStreamWaitEvent(comp_, L.cdone_ev[slot], 0), "hipStreamWaitEvent");
+        hip_check(hipStreamWaitEvent(cs, L.cdone_ev[slot], 0), "hipStreamWaitEvent");
         L.cdone_pending[slot] = 0;
     }
     const uint64_t cap = Compressor::max_bytes(L.bpc, L.n_chunks);
     if (L.cframes[slot].n < cap)
-        hip_check(hipStreamSynchronize(comp_), "hipStreamSynchronize"); // realloc below
+        hip_check(hipStreamSynchronize(cs), "hipStreamSynchronize"); // realloc below
     L.cframes[slot].alloc(cap);
     L.coffsets[slot].alloc((size_t(L.n_chunks) + 1) * 8);
     L.h_coffsets[slot].alloc((size_t(L.n_chunks) + 1) * 8);
@@ -1895,17 +1921,17 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
     // Compression runs on its own stream: it overlaps the D2H of the frames
     // of earlier layers on the hand-off stream.
     hip_check(hipEventRecord(L.ready_ev[slot], stream_), "hipEventRecord");
-    hip_check(hipStreamWaitEvent(comp_, L.ready_ev[slot], 0), "hipStreamWaitEvent");
+    hip_check(hipStreamWaitEvent(cs, L.ready_ev[slot], 0), "hipStreamWaitEvent");
     L.comp->run(L.ring.p + slot * L.slot_bytes, L.pitch, L.n_chunks,
                 reinterpret_cast<const uint32_t*>(L.flags.p) + size_t(slot) * L.n_chunks,
                 uint32_t(layer / L.n_slots + 1), L.cframes[slot].p,
-                reinterpret_cast<uint64_t*>(L.coffsets[slot].p), comp_,
+                reinterpret_cast<uint64_t*>(L.coffsets[slot].p), cs,
                 reinterpret_cast<const uint32_t*>(L.shard_order.p));
     hip_check(hipMemcpyAsync(L.h_coffsets[slot].p, L.coffsets[slot].p,
-                             (size_t(L.n_chunks) + 1) * 8, hipMemcpyDeviceToHost, comp_),
+                             (size_t(L.n_chunks) + 1) * 8, hipMemcpyDeviceToHost, cs),
               "hipMemcpyAsync");
-    hip_check(hipEventRecord(L.comp_ev[slot], comp_), "hipEventRecord");
-    hip_check(hipEventRecord(L.copy_ev[slot], comp_), "hipEventRecord");
+    hip_check(hipEventRecord(L.comp_ev[slot], cs), "hipEventRecord");
+    hip_check(hipEventRecord(L.copy_ev[slot], cs), "hipEventRecord");
     L.copy_pending[slot] = 1;
     L.comp_layer[slot] = int64_t(layer);
 }

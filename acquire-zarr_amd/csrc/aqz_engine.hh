@@ -362,6 +362,11 @@ class Stage
     // device compression of handed-off layers runs on comp_, so layer i+1
     // compresses while layer i's frames go D2H on d2h_
     hipStream_t comp_ = nullptr;
+    hipStream_t comp_lo_ = nullptr; // compression of levels >= 1
+    hipStream_t comp_stream(const StageLevel& L) const
+    {
+        return &L == &lv_[0] ? comp_ : comp_lo_;
+    }
     std::unique_ptr<CopyPool> pool_;
     std::unique_ptr<TaskPool> zpool_; // host zstd workers
     // CPUs of the device's NUMA node: the host pools run there (AQZ_NUMA=0
