@@ -162,9 +162,14 @@ def test_c4_z_slabs_over_4_stages(gpu, c4_volume):
 
 
 @pytest.mark.timeout(300)
-def test_bench_two_ranks_self_launched(gpu):
+@pytest.mark.parametrize("extra", [[], ["--config", "c4"],
+                                   ["--e2e", "pinned", "--compress", "1"]],
+                         ids=["c2", "c4-zslab", "e2e-lz4"])
+def test_bench_two_ranks_self_launched(gpu, extra):
     """`bench.py --gpus 2` with no launcher starts 2 ranks itself (both on
-    this box's one GPU, gloo for the barrier / max) and reports n_gpus 2."""
+    this box's one GPU, gloo for the barrier / max) and reports n_gpus 2:
+    the headline line, C4 with each rank on its own z slab, and the
+    end-to-end hand-off with device compression."""
     import json
     import os
     import subprocess
@@ -175,7 +180,7 @@ def test_bench_two_ranks_self_launched(gpu):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2",
                         "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
-                        "--no-pyramid-only-line"],
+                        "--no-pyramid-only-line", "--no-hbm-probe"] + extra,
                        capture_output=True, text=True, timeout=110, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
