@@ -472,8 +472,9 @@ Stage::place_level(StageLevel& L)
 // fastest is kept (the others are freed).  The launch times fall into about
 // three bands (C2: 0.39 / 0.41 / 0.43 ms, profiles/r02_va_probe.txt; the
 // same virtual addresses land in different bands), so the search stops
-// early only once the spread shows the fast band (>= 12% better than the
-// slowest seen; one C2 bench run found it only at the 9th candidate).  A
+// early only once the spread shows the fast band (>= 8% better than the
+// slowest seen: the bands are ~5% apart; one C2 bench run found the fast
+// band only at its 8th candidate).  A
 // candidate costs a few ms and holds its rings until the search ends.  Only for large rings
 // (>= 256 MiB), where the stage is a long-lived streaming engine.
 // AQZ_PLACEMENT_TRIES (default 16; 1 = off).
@@ -552,7 +553,7 @@ Stage::calibrate_placement()
             if (times.back() < times[best])
                 best = times.size() - 1;
             const double worst = *std::max_element(times.begin(), times.end());
-            if (times[best] < 0.88 * worst)
+            if (times[best] < 0.92 * worst)
                 break;
         }
     } catch (const Error& e) {

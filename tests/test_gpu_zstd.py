@@ -23,7 +23,7 @@ from codec_helpers import (blosc_zstd_decode, camera_like, header, libblosc,
                            libblosc_compress, libblosc_decode, libzstd, zstd_compress,
                            zstd_decode)
 from helpers import expected_stage_layers
-from oracle_bindings import MEAN, SPACE, TIME, U8, U16, F32, synthetic_frames
+from oracle_bindings import F32, F64, MEAN, SPACE, TIME, U8, U16, synthetic_frames
 
 pytestmark = pytest.mark.gpu
 
@@ -98,7 +98,7 @@ def _run(gpu, dtype, codec, clevel, shuffle):
                 continue
             h = header(fr)
             assert h["version"] == 2 and (h["flags"] >> 5) == 4 and h["nbytes"] == bpc
-            assert h["typesize"] == {U8: 1, U16: 2, F32: 4}[dtype]
+            assert h["typesize"] == {U8: 1, U16: 2, F32: 4, F64: 8}[dtype]
             assert h["cbytes"] == len(fr) and len(fr) <= bpc + 16
             if h["flags"] & 0x2:
                 n_memcpy += 1
@@ -113,7 +113,7 @@ def _run(gpu, dtype, codec, clevel, shuffle):
 
 
 @needs_zstd
-@pytest.mark.parametrize("dtype", [U8, U16, F32], ids=["u8", "u16", "f32"])
+@pytest.mark.parametrize("dtype", [U8, U16, F32, F64], ids=["u8", "u16", "f32", "f64"])
 @pytest.mark.parametrize("shuffle", [0, 1, 2])
 def test_stage_blosc_zstd_layers(gpu, engine, dtype, shuffle):
     _run(gpu, dtype, 2, 5, shuffle)
