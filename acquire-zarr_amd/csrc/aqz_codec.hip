@@ -635,16 +635,24 @@ shuffle_blocks(const ShuffleParams p)
                 const uint32_t nw = ne / vec;
                 const uint32_t lo = uint32_t(uint64_t(nw) * part / np);
                 const uint32_t hi = uint32_t(uint64_t(nw) * (part + 1) / np);
-                for (uint32_t w0 = lo; w0 < hi; w0 += 4 * 256) {
-                    uint4 v[4];
+                // 8 nontemporal 16-B loads in flight per lane, then their
+                // stores (4 plain loads: 0.70 ms per 512 MiB layer, 8 nt:
+                // 0.42 ms; nt stores: no gain)
+                constexpr uint32_t kB = 8;
+                for (uint32_t w0 = lo; w0 < hi; w0 += kB * 256) {
+                    uint4 v[kB];
 #pragma unroll
-                    for (uint32_t u = 0; u < 4; ++u) {
+                    for (uint32_t u = 0; u < kB; ++u) {
                         const uint32_t w = w0 + u * 256 + t;
-                        if (w < hi)
-                            v[u] = *reinterpret_cast<const uint4*>(src + 16ull * w);
+                        typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+                        if (w < hi) {
+                            const u32x4v a = __builtin_nontemporal_load(
+                              reinterpret_cast<const u32x4v*>(src + 16ull * w));
+                            v[u] = uint4{ a.x, a.y, a.z, a.w };
+                        }
                     }
 #pragma unroll
-                    for (uint32_t u = 0; u < 4; ++u) {
+                    for (uint32_t u = 0; u < kB; ++u) {
                         const uint32_t w = w0 + u * 256 + t;
                         if (w >= hi)
                             continue;
