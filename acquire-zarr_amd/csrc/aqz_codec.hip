@@ -1270,60 +1270,31 @@ zstd_encode(const ZstdParams p)
             zbuf[i] = 0;
     }
     __syncthreads();
+    // stream w on wave w; literals are read coalesced (lane l takes literal
+    // s + l of each run of 64).  First every stream's bit count, then --
+    // only if Huffman wins for the block -- the bits are placed by a suffix
+    // scan of their code lengths: a stream is written last literal first
+    const uint32_t w = t >> 6, lane = t & 63u;
+    const uint32_t seg4 = try_huf ? zstd::lit_segment(nl) : 0;
+    const uint32_t a = min(nl, w * seg4), e = min(nl, (w + 1) * seg4);
+    uint32_t k = 0; // parse unit of this lane's literal (match mode)
+    auto sym_at = [&](uint32_t i) -> uint8_t {
+        if (!lit.pre)
+            return lit.base[i];
+        while (k + 1 < kZSubBlocks && pre[k + 1] <= i)
+            ++k;
+        while (i < pre[k])
+            --k;
+        return lit.base[uint64_t(k) * kZSub + (i - pre[k])];
+    };
+    uint32_t bits = 0;
+    bool fits = false;
     if (try_huf) {
-        // stream w on wave w; literals are read coalesced (lane l takes
-        // literal s + l of each run of 64) and placed by a suffix scan of
-        // their code lengths: a stream is written last literal first
-        const uint32_t w = t >> 6, lane = t & 63u;
-        const uint32_t seg4 = zstd::lit_segment(nl);
-        const uint32_t a = min(nl, w * seg4), e = min(nl, (w + 1) * seg4);
-        uint32_t k = 0; // parse unit of this lane's literal (match mode)
-        auto sym_at = [&](uint32_t i) -> uint8_t {
-            if (!lit.pre)
-                return lit.base[i];
-            while (k + 1 < kZSubBlocks && pre[k + 1] <= i)
-                ++k;
-            while (i < pre[k])
-                --k;
-            return lit.base[uint64_t(k) * kZSub + (i - pre[k])];
-        };
-        uint32_t bits = 0;
         for (uint32_t i = a + lane; i < e; i += 64)
             bits += clen[sym_at(i)];
-        for (int d = 32; d > 0; d >>= 1)
-            bits += __shfl_xor(bits, d);
-        const bool fits = bits + 1 <= 8 * (e - a) + 32;
-        if (fits) {
-            uint32_t* sb = buf[w];
-            uint32_t base = 0;
-            for (uint32_t cs = e; cs > a;) {
-                const uint32_t s0 = cs > a + 64 ? cs - 64 : a;
-                const uint32_t i = s0 + lane;
-                uint32_t n = 0, v = 0;
-                if (i < cs) {
-                    const uint8_t sym = sym_at(i);
-                    n = clen[sym];
-                    v = code[sym];
-                }
-                uint32_t x = n; // inclusive suffix sum over the run
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = __shfl_down(x, d);
-                    if (lane + uint32_t(d) < 64)
-                        x += y;
-                }
-                const uint32_t pos = base + x - n;
-                if (n) {
-                    const uint32_t o = pos & 31u;
-                    atomicOr(&sb[pos >> 5], v << o);
-                    if (o + n > 32)
-                        atomicOr(&sb[(pos >> 5) + 1], v >> (32 - o));
-                }
-                base += __shfl(x, 0);
-                cs = s0;
-            }
-            if (lane == 0)
-                atomicOr(&sb[bits >> 5], 1u << (bits & 31u)); // end mark
-        }
+        for (int dd = 32; dd > 0; dd >>= 1)
+            bits += __shfl_xor(bits, dd);
+        fits = bits + 1 <= 8 * (e - a) + 32;
         if (lane == 0)
             ssz[w] = fits ? bits / 8 + 1 : 0x7fffffffu;
     }
@@ -1353,6 +1324,38 @@ zstd_encode(const ZstdParams p)
         if (t == 0)
             p.bkind[g] = 0;
         return;
+    }
+    if (ltype == 2) { // every stream fits (a stream that did not lost)
+        uint32_t* sb = buf[w];
+        uint32_t base = 0;
+        for (uint32_t cs = e; cs > a;) {
+            const uint32_t s0 = cs > a + 64 ? cs - 64 : a;
+            const uint32_t i = s0 + lane;
+            uint32_t n = 0, v = 0;
+            if (i < cs) {
+                const uint8_t sym = sym_at(i);
+                n = clen[sym];
+                v = code[sym];
+            }
+            uint32_t x = n; // inclusive suffix sum over the run
+            for (int dd = 1; dd < 64; dd <<= 1) {
+                const uint32_t y = __shfl_down(x, dd);
+                if (lane + uint32_t(dd) < 64)
+                    x += y;
+            }
+            const uint32_t pos = base + x - n;
+            if (n) {
+                const uint32_t o = pos & 31u;
+                atomicOr(&sb[pos >> 5], v << o);
+                if (o + n > 32)
+                    atomicOr(&sb[(pos >> 5) + 1], v >> (32 - o));
+            }
+            base += __shfl(x, 0);
+            cs = s0;
+        }
+        if (lane == 0)
+            atomicOr(&sb[bits >> 5], 1u << (bits & 31u)); // end mark
+        __syncthreads();
     }
     // the literal payload -> scratch[0, lpay)
     if (ltype == 2) {
