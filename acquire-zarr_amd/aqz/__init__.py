@@ -61,12 +61,22 @@ class ArrayDescC(C.Structure):
 
 class StageOptionsC(C.Structure):
     _fields_ = [("layer_slots", C.c_uint32), ("max_batch_frames", C.c_uint32),
-                ("first_frame", C.c_uint64)]
+                ("first_frame", C.c_uint64), ("z_slab_begin", C.c_uint32),
+                ("z_slab_end", C.c_uint32)]
 
 
 class StageBenchOptionsC(C.Structure):
     """aqz_stage_bench_options (include/aqz_gpu_bench.h): not drop-in ABI."""
-    _fields_ = [("force_levels", C.c_uint32), ("skip_level0_split", C.c_int32)]
+    _fields_ = [("force_levels", C.c_uint32), ("skip_level0_split", C.c_int32),
+                ("placement_tries", C.c_uint32), ("placement_mode", C.c_uint32),
+                ("placement_spacer_bytes", C.c_uint64)]
+
+
+class PlacementReportC(C.Structure):
+    """aqz_placement_report (include/aqz_gpu_bench.h)."""
+    _fields_ = [("n", C.c_uint32), ("kept", C.c_uint32), ("reps", C.c_uint32),
+                ("mode", C.c_uint32), ("ms", C.c_double * 32),
+                ("kept_ms_final", C.c_double), ("peak_device_bytes", C.c_uint64)]
 
 
 class MemoryUsageC(C.Structure):
@@ -176,6 +186,10 @@ def lib():
         "aqz_stage_memory_usage": ([vp, C.POINTER(MemoryUsageC)], i32),
         "aqz_stage_estimate_memory": ([C.POINTER(ArrayDescC), C.POINTER(StageOptionsC),
                                        C.POINTER(MemoryUsageC)], i32),
+        "aqz_stage_estimate_memory_bench": ([C.POINTER(ArrayDescC), C.POINTER(StageOptionsC),
+                                             C.POINTER(StageBenchOptionsC),
+                                             C.POINTER(MemoryUsageC)], i32),
+        "aqz_stage_placement_report": ([vp, C.POINTER(PlacementReportC)], i32),
         "aqz_stage_destroy": ([vp], None),
         "aqz_stage_n_levels": ([vp], u32),
         "aqz_stage_level_dims": ([vp, u32, D, sz, C.POINTER(sz)], i32),
@@ -343,13 +357,25 @@ def downsampling_metadata_json(method):
 
 
 def estimate_memory(dims, dtype, method, max_levels=0, layer_slots=0,
-                    max_batch_frames=0, storage_order=None):
-    """aqz_stage_estimate_memory: upper bound of a stage's footprint (no GPU)."""
+                    max_batch_frames=0, storage_order=None, force_levels=0,
+                    skip_level0_split=False, placement_tries=0, placement_mode=0,
+                    placement_spacer_bytes=0):
+    """aqz_stage_estimate_memory: upper bound of a stage's footprint (no GPU).
+    With bench options (force_levels, placement_*), the bench-header
+    aqz_stage_estimate_memory_bench, which includes the placement search's
+    creation peak."""
     d, keep = _desc(dims, dtype, method, max_levels, True, storage_order, 0)
     o = StageOptionsC(layer_slots, max_batch_frames, 0)
     m = MemoryUsageC()
-    _check(lib().aqz_stage_estimate_memory(C.byref(d), C.byref(o), C.byref(m)),
-           "aqz_stage_estimate_memory")
+    if force_levels or skip_level0_split or placement_tries:
+        b = StageBenchOptionsC(force_levels, 1 if skip_level0_split else 0,
+                               placement_tries, placement_mode, placement_spacer_bytes)
+        _check(lib().aqz_stage_estimate_memory_bench(C.byref(d), C.byref(o), C.byref(b),
+                                                     C.byref(m)),
+               "aqz_stage_estimate_memory_bench")
+    else:
+        _check(lib().aqz_stage_estimate_memory(C.byref(d), C.byref(o), C.byref(m)),
+               "aqz_stage_estimate_memory")
     return {"device_bytes": m.device_bytes, "pinned_bytes": m.pinned_bytes}
 
 
@@ -485,14 +511,17 @@ class Stage:
     def __init__(self, dims, dtype, method, max_levels=0, multiscale=True,
                  storage_order=None, device=0, layer_slots=0,
                  max_batch_frames=0, force_levels=0, skip_level0_split=False,
-                 first_frame=0):
+                 first_frame=0, placement_tries=0, placement_mode=0,
+                 placement_spacer_bytes=0, z_slab=None):
         self.dtype = dtype
         d, self._keep = _desc(dims, dtype, method, max_levels, multiscale,
                               storage_order, device)
-        o = StageOptionsC(layer_slots, max_batch_frames, first_frame)
+        zb, ze = z_slab if z_slab else (0, 0)
+        o = StageOptionsC(layer_slots, max_batch_frames, first_frame, zb, ze)
         h = C.c_void_p()
-        if force_levels or skip_level0_split:
-            b = StageBenchOptionsC(force_levels, 1 if skip_level0_split else 0)
+        if force_levels or skip_level0_split or placement_tries:
+            b = StageBenchOptionsC(force_levels, 1 if skip_level0_split else 0,
+                                   placement_tries, placement_mode, placement_spacer_bytes)
             rc = lib().aqz_stage_create_bench(C.byref(d), C.byref(o), C.byref(b), C.byref(h))
         else:
             rc = lib().aqz_stage_create(C.byref(d), C.byref(o), C.byref(h))
@@ -649,14 +678,15 @@ class Stage:
         return node.value, n.value
 
     def placement(self):
-        """Creation-time placement calibration: {"candidates_ms": [...],
-        "kept": i} (empty list when none ran)."""
-        arr = (C.c_double * 16)()
-        n, kept = C.c_size_t(0), C.c_uint32(0)
-        _check(lib().aqz_stage_placement(self.h, arr, 16, C.byref(n), C.byref(kept)),
-               "placement")
-        return {"candidates_ms": [round(arr[i], 5) for i in range(min(16, n.value))],
-                "kept": kept.value}
+        """Creation-time placement search (bench option placement_tries):
+        {"candidates_ms": [...], "kept": i, "kept_ms_final", "reps", "mode",
+        "peak_device_bytes"} (empty candidate list when none ran)."""
+        r = PlacementReportC()
+        _check(lib().aqz_stage_placement_report(self.h, C.byref(r)), "placement_report")
+        return {"candidates_ms": [round(r.ms[i], 5) for i in range(min(32, r.n))],
+                "kept": r.kept, "kept_ms_final": round(r.kept_ms_final, 5),
+                "reps": r.reps, "mode": r.mode,
+                "peak_device_bytes": r.peak_device_bytes}
 
     # ---- device compression of resident layers ----------------------------
     def compress_layer(self, level, layer, codec=CODEC_BLOSC_LZ4, clevel=5, shuffle=1):

@@ -441,6 +441,21 @@ aqz_downsampling_metadata_json(int32_t method, char* buf, size_t cap, size_t* le
 }
 
 // ---- stage ---------------------------------------------------------------------
+static void
+apply_bench(const aqz_stage_bench_options* bench, StageOptions& o)
+{
+    if (!bench)
+        return;
+    o.force_levels = bench->force_levels;
+    o.skip_level0_split = bench->skip_level0_split != 0;
+    o.placement_tries = bench->placement_tries;
+    o.placement_mode = bench->placement_mode;
+    if (o.placement_mode > 1)
+        throw Error(AQZ_STATUS_INVALID_ARGUMENT, "placement_mode must be 0 or 1");
+    if (bench->placement_spacer_bytes)
+        o.placement_spacer = bench->placement_spacer_bytes;
+}
+
 static aqz_status
 create_stage(const aqz_array_desc* desc, const aqz_stage_options* opt,
              const aqz_stage_bench_options* bench, aqz_stage** out)
@@ -455,11 +470,10 @@ create_stage(const aqz_array_desc* desc, const aqz_stage_options* opt,
             o.layer_slots = opt->layer_slots;
             o.max_batch_frames = opt->max_batch_frames;
             o.first_frame = opt->first_frame;
+            o.z_slab_begin = opt->z_slab_begin;
+            o.z_slab_end = opt->z_slab_end;
         }
-        if (bench) {
-            o.force_levels = bench->force_levels;
-            o.skip_level0_split = bench->skip_level0_split != 0;
-        }
+        apply_bench(bench, o);
         auto* s = new aqz_stage;
         try {
             s->st = std::make_unique<Stage>(a, o);
@@ -486,8 +500,8 @@ aqz_stage_create_bench(const aqz_array_desc* desc, const aqz_stage_options* opt,
 }
 
 aqz_status
-aqz_stage_estimate_memory(const aqz_array_desc* desc, const aqz_stage_options* opt,
-                          aqz_memory_usage* out)
+aqz_stage_estimate_memory_bench(const aqz_array_desc* desc, const aqz_stage_options* opt,
+                                const aqz_stage_bench_options* bench, aqz_memory_usage* out)
 {
     if (!out)
         return AQZ_STATUS_INVALID_ARGUMENT;
@@ -498,10 +512,20 @@ aqz_stage_estimate_memory(const aqz_array_desc* desc, const aqz_stage_options* o
             o.layer_slots = opt->layer_slots;
             o.max_batch_frames = opt->max_batch_frames;
             o.first_frame = opt->first_frame;
+            o.z_slab_begin = opt->z_slab_begin;
+            o.z_slab_end = opt->z_slab_end;
         }
+        apply_bench(bench, o);
         const Footprint f = Stage::estimate_memory(a, o);
         *out = aqz_memory_usage{ f.device, f.pinned };
     });
+}
+
+aqz_status
+aqz_stage_estimate_memory(const aqz_array_desc* desc, const aqz_stage_options* opt,
+                          aqz_memory_usage* out)
+{
+    return aqz_stage_estimate_memory_bench(desc, opt, nullptr, out);
 }
 
 aqz_status
@@ -733,6 +757,24 @@ aqz_stage_host_affinity(const aqz_stage* st, int32_t* numa_node, uint32_t* n_cpu
         *numa_node = st->st->numa_node();
     if (n_cpus)
         *n_cpus = uint32_t(st->st->numa_cpus());
+    return AQZ_STATUS_SUCCESS;
+}
+
+aqz_status
+aqz_stage_placement_report(const aqz_stage* st, aqz_placement_report* out)
+{
+    if (!st || !out)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    const PlacementReport& r = st->st->placement();
+    *out = aqz_placement_report{};
+    out->n = uint32_t(r.ms.size());
+    out->kept = uint32_t(r.kept);
+    out->reps = r.reps;
+    out->mode = r.mode;
+    for (size_t i = 0; i < r.ms.size() && i < 32; ++i)
+        out->ms[i] = r.ms[i];
+    out->kept_ms_final = r.kept_ms_final;
+    out->peak_device_bytes = r.peak_device;
     return AQZ_STATUS_SUCCESS;
 }
 

@@ -342,6 +342,8 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
     }
     if (const char* ev = std::getenv("AQZ_KNOBS")) // tuning knob
         knobs_ = uint32_t(std::atoi(ev));
+    if (const char* ev = std::getenv("AQZ_XCD_ROT")) // tuning knob
+        xcd_rot_ = uint32_t(std::atoi(ev));
     if (const char* ev = std::getenv("AQZ_NT")) // tuning knob
         nt_mode_ = uint32_t(std::atoi(ev)) & 7u;
     if (const char* ev = std::getenv("AQZ_REGION_ROWS_LOG2")) { // tuning knob
@@ -355,6 +357,23 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         max_frames_ = 1;
         for (size_t i = 0; i + 2 < n; ++i)
             max_frames_ *= lv_[0].dims[i].array_size_px;
+    }
+    // z-slab schedule: planes [begin, end) of every z stack
+    if (opt_.z_slab_begin != 0 || opt_.z_slab_end != 0) {
+        const uint64_t p0 = lv_[0].planes;
+        const uint64_t b0 = opt_.z_slab_begin, e0 = opt_.z_slab_end;
+        if (n < 4 || p0 == 0 || b0 >= e0 || e0 > p0)
+            throw Error(1, "z slab needs a z dimension and 0 <= begin < end <= planes");
+        if (opt_.first_frame % p0 != 0)
+            throw Error(1, "with a z slab, first_frame must start a z stack");
+        slab_len_ = e0 - b0;
+        for (auto& L : lv_) {
+            const uint64_t pk = L.planes;
+            if ((b0 * pk) % p0 != 0 || (e0 * pk) % p0 != 0)
+                throw Error(9, "z slab does not align with the z pyramid");
+            slab_skip_.push_back(pk - (e0 - b0) * pk / p0);
+        }
+        opt_.first_frame += b0;
     }
     // z-slab sharding: this stage continues a stream at first_frame
     if (opt_.first_frame > 0) {
@@ -463,30 +482,45 @@ Stage::place_level(StageLevel& L)
               "hipMemcpy");
 }
 
-// Placement calibration.  The fused kernels stream ~1 read : 1.3 write of
-// HBM, and how fast depends on where the chunk-layer rings landed: on one
-// box, stages that differ only by their allocations ran the same 128-frame
-// C2 launch in 0.427-0.481 ms, whatever the source ring
-// (profiles/r02_mode_probe.txt).  So at creation a few candidate placements
-// of the rings are timed with the real kernel on a scratch batch, and the
-// fastest is kept (the others are freed).  The launch times fall into about
-// three bands (C2: 0.39 / 0.41 / 0.43 ms, profiles/r02_va_probe.txt; the
-// same virtual addresses land in different bands), so the search stops
-// early only once the spread shows the fast band (>= 8% better than the
-// slowest seen: the bands are ~5% apart; one C2 bench run found the fast
-// band only at its 8th candidate).  A
-// candidate costs a few ms and holds its rings until the search ends.  Only for large rings
-// (>= 256 MiB), where the stage is a long-lived streaming engine.
-// AQZ_PLACEMENT_TRIES (default 16; 1 = off).
+// Placement search (bench-only, StageOptions::placement_tries > 1).  The
+// fused kernels' launch time depends on which physical memory the
+// chunk-layer rings land in: the same kernel on the same source ran a C2
+// launch in one of about three bands (0.39 / 0.41 / 0.43 ms) depending only
+// on the stage's allocations (profiles/r02_mode_probe.txt), and the same
+// virtual addresses land in different bands (r02_va_probe.txt).  Round 3
+// ruled out translation misses, extra HBM traffic, DRAM/TCC request stalls
+// (PMC per placement, profiles/r03_placement_pmc.txt), the chunk stride
+// (pitch pads), the XCD walk phase and plain streaming rates of the same
+// buffers (r03_placement_probes.txt): the effect is not observable from user
+// space, so it is searched, not predicted.  Each candidate is timed on
+// random frames over `reps` launches; a loser is freed and a spacer
+// allocation (held until the search ends) pushes the next candidate
+// elsewhere, so the peak is two ring sets plus the spacers (mode 0), or
+// every candidate is held (mode 1, the round-2 search).  The kept
+// placement is re-timed alone at the end (kept_ms_final).  Only for rings
+// >= 256 MiB on the fused paths.
 void
 Stage::calibrate_placement()
 {
-    uint32_t tries = 16;
-    if (const char* e = std::getenv("AQZ_PLACEMENT_TRIES"))
-        tries = uint32_t(std::max(1, std::atoi(e)));
-    uint64_t ring_bytes = 0;
-    for (const auto& L : lv_)
-        ring_bytes += L.ring.n;
+    uint32_t tries = opt_.placement_tries;
+    uint32_t mode = opt_.placement_mode;
+    uint64_t spacer = opt_.placement_spacer;
+    uint32_t reps = 10;
+    if (const char* e = std::getenv("AQZ_PLACEMENT_TRIES")) // tuning knobs
+        tries = uint32_t(std::max(0, std::atoi(e)));
+    if (const char* e = std::getenv("AQZ_PLACEMENT_MODE"))
+        mode = uint32_t(std::atoi(e));
+    if (const char* e = std::getenv("AQZ_PLACEMENT_SPACER_MB"))
+        spacer = uint64_t(std::max(0, std::atoi(e))) << 20;
+    if (const char* e = std::getenv("AQZ_PLACEMENT_REPS"))
+        reps = uint32_t(std::max(1, std::atoi(e)));
+    uint64_t ring_bytes = 0, set_bytes = 0;
+    std::vector<bool> has_ring(lv_.size());
+    for (size_t k = 0; k < lv_.size(); ++k) {
+        has_ring[k] = lv_[k].ring.p != nullptr;
+        ring_bytes += lv_[k].ring.n;
+        set_bytes += lv_[k].ring.n + lv_[k].flags.n + lv_[k].ref_table.n;
+    }
     uint32_t n = opt_.max_batch_frames;
     if (fused_3d_ && !fused_2d_)
         n = n / g3d_ * g3d_;
@@ -495,7 +529,10 @@ Stage::calibrate_placement()
         return;
     const uint64_t fb0 = uint64_t(lv_[0].W) * lv_[0].H * bpp_;
     DevBuf src(size_t(n) * fb0);
-    hip_check(hipMemsetAsync(src.p, 0x5a, src.n, stream_), "hipMemsetAsync");
+    hip_check(hipMemsetAsync(src.p, 0, src.n, stream_), "hipMemsetAsync");
+    hip_check(launch_fill_random(src.p, src.n, 0x5eedull, stream_), "fill launch");
+    uint64_t live = memory_usage().device + src.n;
+    uint64_t peak = live;
     hipEvent_t a = nullptr, b = nullptr;
     hip_check(hipEventCreate(&a), "hipEventCreate");
     hip_check(hipEventCreate(&b), "hipEventCreate");
@@ -507,7 +544,7 @@ Stage::calibrate_placement()
     auto measure = [&]() {
         run_batch(src.p, n); // warm-up
         hip_check(hipEventRecord(a, stream_), "hipEventRecord");
-        for (int r = 0; r < 3; ++r)
+        for (uint32_t r = 0; r < reps; ++r)
             run_batch(src.p, n);
         hip_check(hipEventRecord(b, stream_), "hipEventRecord");
         hip_check(hipEventSynchronize(b), "hipEventSynchronize");
@@ -518,7 +555,7 @@ Stage::calibrate_placement()
             lv_[k].level_frame_count = uint32_t(lfc0[k]);
             lv_[k].slot_layer.assign(lv_[k].n_slots, -1);
         }
-        return double(ms) / 3;
+        return double(ms) / reps;
     };
     struct Placement
     {
@@ -533,48 +570,68 @@ Stage::calibrate_placement()
         }
         return pl;
     };
-    // candidate i < held.size() is held[i]; the installed one is candidate
-    // times.size() - 1 when `current_ok`
-    std::vector<Placement> held;
-    std::vector<double> times;
-    size_t best = 0;
-    bool current_ok = false;
+    PlacementReport rep;
+    rep.reps = reps;
+    rep.mode = mode;
+    Placement best;
+    double best_ms = 0;
+    std::vector<Placement> held; // mode 1
+    std::vector<DevBuf> spacers; // mode 0
     try {
         for (uint32_t t = 0; t < tries; ++t) {
             if (t > 0) {
-                held.push_back(take()); // keep it: the next lands elsewhere
-                current_ok = false;
                 for (size_t k = 0; k < lv_.size(); ++k)
-                    if (held.back().ring[k].p)
+                    if (has_ring[k])
                         place_level(lv_[k]);
+                live += set_bytes;
+                peak = std::max(peak, live);
             }
-            times.push_back(measure());
-            current_ok = true;
-            if (times.back() < times[best])
-                best = times.size() - 1;
-            const double worst = *std::max_element(times.begin(), times.end());
-            if (times[best] < 0.92 * worst)
+            const double ms = measure();
+            rep.ms.push_back(ms);
+            const bool better = t == 0 || ms < best_ms;
+            Placement cur = take();
+            Placement& loser = better ? best : cur;
+            if (t > 0) { // a loser exists
+                if (mode == 1)
+                    held.push_back(std::move(loser));
+                else {
+                    loser = Placement{};
+                    live -= set_bytes;
+                }
+            }
+            if (better) {
+                best = std::move(cur);
+                best_ms = ms;
+                rep.kept = t;
+            }
+            const double worst = *std::max_element(rep.ms.begin(), rep.ms.end());
+            if (best_ms < 0.92 * worst || t + 1 == tries)
                 break;
+            if (mode == 0 && spacer > 0) {
+                spacers.emplace_back(spacer); // the next candidate lands elsewhere
+                live += spacer;
+                peak = std::max(peak, live);
+            }
         }
     } catch (const Error& e) {
-        if (e.status != 6 || held.empty()) // out of memory: keep the best so far
+        if (e.status != 6 || rep.ms.empty()) // out of memory: keep the best so far
             throw;
         (void)hipGetLastError();
     }
-    if (!current_ok || best + 1 != times.size()) {
-        // reinstall the fastest candidate; the current one is released below
-        Placement cur = take();
-        for (size_t k = 0; k < lv_.size(); ++k) {
-            lv_[k].ring = std::move(held[best].ring[k]);
-            lv_[k].flags = std::move(held[best].flags[k]);
-            lv_[k].ref_table = std::move(held[best].ref[k]);
-        }
-        held.push_back(std::move(cur));
-    }
     hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
     held.clear();
-    placement_ms_ = times;
-    placement_best_ = best;
+    spacers.clear();
+    {
+        Placement cur = take(); // a candidate placed but not measured (OOM)
+    }
+    for (size_t k = 0; k < lv_.size(); ++k) {
+        lv_[k].ring = std::move(best.ring[k]);
+        lv_[k].flags = std::move(best.flags[k]);
+        lv_[k].ref_table = std::move(best.ref[k]);
+    }
+    rep.kept_ms_final = measure();
+    rep.peak_device = peak;
+    placement_ = rep;
     // the calibration wrote frames and has_data tags: back to zero
     for (auto& L : lv_) {
         if (!L.ring.p)
@@ -582,6 +639,7 @@ Stage::calibrate_placement()
         hip_check(hipMemsetAsync(L.ring.p, 0, L.ring.n, stream_), "hipMemsetAsync");
         hip_check(hipMemsetAsync(L.flags.p, 0, L.flags.n, stream_), "hipMemsetAsync");
     }
+    hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
 }
@@ -767,7 +825,9 @@ Stage::append(const void* frames, uint64_t n_frames, int mem)
     const auto* src = static_cast<const uint8_t*>(frames);
     const uint32_t B = opt_.max_batch_frames;
     for (uint64_t done = 0; done < n_ok;) {
-        const uint32_t b = uint32_t(std::min<uint64_t>(B, n_ok - done));
+        uint32_t b = uint32_t(std::min<uint64_t>(B, n_ok - done));
+        if (slab_len_) // a batch never straddles two slabs
+            b = uint32_t(std::min<uint64_t>(b, slab_len_ - slab_done_));
         const uint8_t* p = src + done * fbytes;
         if (mem == kMemDevice) {
             run_batch(p, b);
@@ -808,6 +868,14 @@ Stage::append(const void* frames, uint64_t n_frames, int mem)
         else if (mem != kMemHostPinned)
             note_consumed(nullptr, b); // copied into staging before return
         done += b;
+        if (slab_len_ && (slab_done_ += b) == slab_len_) {
+            // next stack's slab: skip the planes other stages own
+            for (size_t k = 0; k < lv_.size(); ++k) {
+                lv_[k].frames_written += slab_skip_[k];
+                lv_[k].level_frame_count += uint32_t(slab_skip_[k]);
+            }
+            slab_done_ = 0;
+        }
     }
     if (n_ok < n_frames)
         throw Error(12, "append beyond the array's bounded extent");
@@ -972,6 +1040,8 @@ Stage::fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
     // XCD-contiguous region order pays on large launches (A/B: C2 -4.5%,
     // C5 -3.5%, C3 even) and not on small ones (C1 +4%)
     p.xcd_order = (uint64_t(n) * p.nbx_in * p.nby_in >= 8192 && !(knobs_ & 64u)) ? 1 : 0;
+    p.xcd_rot = (knobs_ >> 16) ? (knobs_ >> 16) : xcd_rot_; // knob bits 16-31: A/B
+    p.xskew = (knobs_ & 2048u) ? 1u : 0u;                    // launcher sets the mask
     p.d_nreg_in = make_fastdiv(std::max<uint32_t>(1, p.nbx_in * p.nby_in));
     p.d_nbx_in = make_fastdiv(std::max<uint32_t>(1, p.nbx_in));
     p.tw = L0.tw;
@@ -1331,7 +1401,10 @@ Stage::copy_band_async(uint32_t level, uint64_t layer, uint32_t band, void* dst,
     const uint32_t slot = uint32_t(layer % L.n_slots);
     if (L.slot_layer[slot] != int64_t(layer))
         throw Error(3, "chunk layer not resident");
-    if (!finalized_ && L.frames_written < layer * L.F + (uint64_t(band) + 1) * fpb)
+    // the trailing band of a ragged dim 1 is complete with its layer
+    // (flush_layer_remainder_, array.cpp:863-871, 884-886)
+    const uint64_t band_end = std::min<uint64_t>((uint64_t(band) + 1) * fpb, L.F);
+    if (!finalized_ && L.frames_written < layer * L.F + band_end)
         throw Error(3, "band not complete");
     if (dst && cap < L.bpc * cpb)
         throw Error(2, "destination too small for a band");
@@ -1417,6 +1490,7 @@ Stage::estimate_memory(const ArrayDesc& desc, const StageOptions& opt_in)
     const size_t n = base.ndims();
     const uint64_t B = opt.max_batch_frames;
     Footprint f;
+    uint64_t ring_bytes = 0, set_bytes = 0; // the placement search's unit
     for (size_t k = 0; k < levels.size(); ++k) {
         ArrayDimensions ad(levels[k], desc.dtype);
         const uint64_t W = levels[k][n - 1].array_size_px;
@@ -1427,10 +1501,12 @@ Stage::estimate_memory(const ArrayDesc& desc, const StageOptions& opt_in)
         const uint64_t slots = std::max<uint64_t>(opt.layer_slots, (B - 1 + F - 1) / F + 1);
         const uint64_t lfb = W * H * bpp;
         if (!(k == 0 && opt.skip_level0_split)) {
-            f.device += chunk_pitch(bpc, uint32_t(nc)) * nc * slots; // ring
-            f.device += nc * slots * 4;                              // has_data words
-            f.device += slots * F * sizeof(FrameRef);                // frame table
-            f.device += nc * slots;                                  // has_data bytes
+            const uint64_t ring = chunk_pitch(bpc, uint32_t(nc)) * nc * slots;
+            const uint64_t set = ring + nc * slots * 4 + slots * F * sizeof(FrameRef);
+            f.device += set;        // ring, has_data words, frame table
+            f.device += nc * slots; // has_data bytes
+            ring_bytes += ring;
+            set_bytes += set;
         }
         f.device += F * 12 + nc * 4; // tab_off + tab_grp, shard order
         if (k > 0) {
@@ -1445,6 +1521,16 @@ Stage::estimate_memory(const ArrayDesc& desc, const StageOptions& opt_in)
     f.pinned += 2 * B * fb0; // pageable -> pinned staging
     if (base.needs_xy_transposition())
         f.device += B * fb0;
+    // the creation-time placement search's transient peak (calibrate_placement):
+    // its random source batch, and one more ring set + the spacers (mode 0)
+    // or every other candidate (mode 1).  An upper bound: the search may
+    // not run (small rings, generic cascade) or stop early.
+    if (opt.placement_tries > 1 && ring_bytes >= (uint64_t(256) << 20)) {
+        const uint64_t extra = opt.placement_tries - 1;
+        f.device += B * fb0;
+        f.device += opt.placement_mode == 1 ? extra * set_bytes
+                                            : set_bytes + extra * opt.placement_spacer;
+    }
     return f;
 }
 
@@ -1999,7 +2085,9 @@ Stage::finalize()
         if (!L.ring.p)
             continue;
         const uint64_t fw = L.frames_written;
-        if (fw % L.F == 0)
+        // (a z-slab stage's frame id may already point past its last slab,
+        // into a layer it never entered: nothing to flush there)
+        if (fw % L.F == 0 || L.slot_layer[(fw / L.F) % L.n_slots] != int64_t(fw / L.F))
             continue;
         const uint64_t end = (fw / L.F + 1) * L.F;
         for (uint64_t fid = fw; fid < end; ++fid) {

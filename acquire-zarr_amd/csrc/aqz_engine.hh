@@ -33,6 +33,7 @@ hipError_t launch_transpose_frames(const void* src, void* dst, uint32_t rows,
                                    hipStream_t stream);
 hipError_t launch_flags_to_bytes(const uint32_t* flags, uint8_t* out, uint32_t n,
                                  uint32_t tag, hipStream_t stream);
+hipError_t launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t stream);
 hipError_t launch_zero_frame_tiles(uint8_t* fb, uint64_t bpc,
                                    uint32_t n_tiles, uint32_t tile_bytes,
                                    hipStream_t stream);
@@ -160,6 +161,27 @@ struct StageOptions
     uint32_t force_levels = 0;
     bool skip_level0_split = false;
     uint64_t first_frame = 0;
+    uint32_t z_slab_begin = 0, z_slab_end = 0; // aqz_stage_options
+    // creation-time placement search (bench-only; 0/1 = off): up to
+    // placement_tries placements of the chunk-layer rings are timed and the
+    // fastest kept.  mode 0: a losing placement is freed and a spacer of
+    // placement_spacer bytes is held until the search ends (peak: two ring
+    // sets + the spacers); mode 1: every candidate is held (peak: tries ring
+    // sets).
+    uint32_t placement_tries = 0;
+    uint32_t placement_mode = 0;
+    uint64_t placement_spacer = uint64_t(128) << 20;
+};
+
+// What the creation-time placement search did (aqz_stage_placement_report).
+struct PlacementReport
+{
+    std::vector<double> ms;       // ms per launch of every candidate
+    size_t kept = 0;              // index of the kept candidate
+    double kept_ms_final = 0;     // the kept placement re-timed alone
+    uint64_t peak_device = 0;     // stage device bytes at the search's peak
+    uint32_t reps = 0;            // timed launches per candidate
+    uint32_t mode = 0;
 };
 
 struct LevelLayout
@@ -304,8 +326,9 @@ class Stage
     int numa_node() const { return numa_node_; }
     size_t numa_cpus() const { return numa_cpus_.size(); }
     // placement calibration: ms per candidate launch and the one kept
-    const std::vector<double>& placement_ms() const { return placement_ms_; }
-    size_t placement_best() const { return placement_best_; }
+    const std::vector<double>& placement_ms() const { return placement_.ms; }
+    size_t placement_best() const { return placement_.kept; }
+    const PlacementReport& placement() const { return placement_; }
 
   private:
     struct Pending
@@ -347,6 +370,10 @@ class Stage
     uint32_t n_fused_ = 0;
     uint32_t rh_log2_ = 4;
     uint64_t max_frames_ = 0; // 0 = unbounded
+    // z-slab schedule: level-0 frames per slab, frames of the current slab
+    // written, and every level's frame-id jump at the end of a slab
+    uint64_t slab_len_ = 0, slab_done_ = 0;
+    std::vector<uint64_t> slab_skip_;
     hipStream_t own_stream_ = nullptr;
     hipStream_t stream_ = nullptr;
     // host-source staging: pinned double buffer -> device double buffer.
@@ -387,6 +414,7 @@ class Stage
     void retire_consumed(bool wait);
     uint32_t nt_mode_ = 7;           // nontemporal policy: input loads (1), level-0 (2) and level-1/2 (4) stores
     uint32_t knobs_ = 0;             // tuning A/B switches
+    uint32_t xcd_rot_ = 0;           // regions each XCD's walk is rotated by, per XCD index
     std::vector<Pending> pend_;
     // kernel timing
     bool timing_ = false;
@@ -396,8 +424,7 @@ class Stage
     uint64_t timed_launches_ = 0;
     hipEvent_t mark_ev_[2] = { nullptr, nullptr };
     hipEvent_t ext_ev_ = nullptr;  // wait_stream
-    std::vector<double> placement_ms_;  // calibration: ms per candidate
-    size_t placement_best_ = 0;
+    PlacementReport placement_;         // creation-time placement search
     bool finalized_ = false;
 };
 

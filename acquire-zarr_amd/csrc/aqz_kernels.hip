@@ -835,7 +835,38 @@ region_of_block(const FusedParams& p)
     if (!p.xcd_order)
         return b;
     const uint32_t per = gridDim.x >> 3;
-    return b < (per << 3) ? (b & 7u) * per + (b >> 3) : b;
+    if (b >= (per << 3))
+        return b;
+    const uint32_t x = b & 7u;
+    uint32_t i = (b >> 3) + p.xrot[x];
+    if (i >= per)
+        i -= per;
+    if (p.xskew) {
+        // step s of the range visits region u of frame (s + u) mod R: the
+        // regions in flight on one XCD write their tiles at different
+        // frame offsets inside the chunks instead of all at the same one
+        const uint32_t nreg = p.nbx_in * p.nby_in;
+        const uint32_t s = fdiv(i, p.d_nreg_in);
+        const uint32_t u = i - s * nreg;
+        i = ((s + u) & p.xskew) * nreg + u;
+    }
+    return x * per + i;
+}
+
+// x * xcd_rot mod (blocks / 8) for the 8 XCDs (region_of_block)
+static FusedParams
+with_xcd_rotation(const FusedParams& p, uint64_t blocks)
+{
+    FusedParams q = p;
+    const uint64_t per = blocks >> 3;
+    for (uint32_t x = 0; x < 8; ++x)
+        q.xrot[x] = per ? uint32_t((uint64_t(x) * p.xcd_rot) % per) : 0u;
+    const uint64_t nreg = uint64_t(p.nbx_in) * p.nby_in;
+    const uint64_t R = nreg ? per / nreg : 0;
+    q.xskew = (p.xskew && p.xcd_order && R >= 2 && per % nreg == 0 && (R & (R - 1)) == 0)
+                ? uint32_t(R - 1)
+                : 0u;
+    return q;
 }
 
 // Region q of a frame -> (row, column) of regions: row-major, or
@@ -1708,7 +1739,34 @@ zero_frame_tiles(uint8_t* fb, uint64_t bpc, uint32_t n_tiles,
         p[i] = 0;
 }
 
+// splitmix64 words (the tests' synthetic_frames stream, seed-offset): the
+// placement calibration times its candidates on random frames, as the
+// stage sees them, not on a constant fill.
+__global__ void
+fill_splitmix(uint64_t* p, uint64_t n, uint64_t seed)
+{
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n;
+         i += uint64_t(gridDim.x) * 256) {
+        uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
 } // namespace
+
+hipError_t
+launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t stream)
+{
+    const uint64_t n = bytes / 8;
+    if (n == 0)
+        return hipSuccess;
+    const uint32_t grid = uint32_t(std::min<uint64_t>((n + 255) / 256, 8192));
+    hipLaunchKernelGGL(fill_splitmix, dim3(grid), dim3(256), 0, stream,
+                       static_cast<uint64_t*>(p), n, seed);
+    return hipGetLastError();
+}
 
 // ---------------------------------------------------------------------------
 // Host launchers: dtype x method dispatch.
@@ -1785,10 +1843,11 @@ launch_fused_pyramid(int dtype, int method, const FusedParams& p,
       uint64_t(p.n_frames) * (uint64_t(p.nbx) * p.nby - uint64_t(p.nbx_in) * p.nby_in);
     if (interior > 0x7fffffffull || edge > 0x7fffffffull)
         return hipErrorInvalidValue;
+    const FusedParams pr = with_xcd_rotation(p, interior);
 #define CALL(T, MM)                                                            \
     do {                                                                       \
         if (interior)                                                          \
-            launch_interior<T, MM>(uint32_t(interior), p, stream);             \
+            launch_interior<T, MM>(uint32_t(interior), pr, stream);            \
         if (edge)                                                              \
             hipLaunchKernelGGL((fused_pyramid_edge<T, MM>),                    \
                                dim3(uint32_t(edge)), dim3(256), 0, stream, p); \
@@ -1811,24 +1870,25 @@ launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
         return hipSuccess;
     // the register-cascade kernel takes 64-row regions down to 4 fused levels
     const bool strip = p.rh_log2 == 6 && p.n_fused <= 4 && !(p.knobs & 256u);
+    const FusedParams pr = with_xcd_rotation(p, blocks);
 #define CALL(T, MM)                                                            \
     do {                                                                       \
         const dim3 gd{ uint32_t(blocks), 1, 1 };                              \
         if (strip && p.nt && (p.knobs & 512u))                                \
             hipLaunchKernelGGL((fused_pyramid_strip3d<T, MM, 7, 0>), gd, dim3(256), 0, \
-                               stream, p);                                    \
+                               stream, pr);                                    \
         else if (strip && p.nt)                                               \
             hipLaunchKernelGGL((fused_pyramid_strip3d<T, MM, 7, 1>), gd, dim3(256), 0, \
-                               stream, p);                                    \
+                               stream, pr);                                    \
         else if (strip)                                                       \
             hipLaunchKernelGGL((fused_pyramid_strip3d<T, MM, 0, 1>), gd, dim3(256), 0, \
-                               stream, p);                                    \
+                               stream, pr);                                    \
         else if (p.nt)                                                        \
             hipLaunchKernelGGL((fused_pyramid_3d<T, MM, 7>), gd, dim3(256), 0,  \
-                               stream, p);                                    \
+                               stream, pr);                                    \
         else                                                                  \
             hipLaunchKernelGGL((fused_pyramid_3d<T, MM, 0>), gd, dim3(256), 0,  \
-                               stream, p);                                    \
+                               stream, pr);                                    \
     } while (0)
     switch (dtype) {
         case 0: AQZ_DISPATCH_M(uint8_t, method, CALL); break;

@@ -88,6 +88,9 @@ struct FusedParams
     uint32_t nt;             // bit0: non-temporal input loads, bit1: nt level-0 stores
     uint32_t knobs;          // tuning A/B switches (0 = shipped defaults)
     uint32_t xcd_order;      // 1: interior regions walk XCD-contiguous ranges
+    uint32_t xcd_rot;        // XCD x starts its range x * xcd_rot regions in
+    uint32_t xrot[8];        // (launcher-filled: x * xcd_rot mod range)
+    uint32_t xskew;          // frames per XCD range - 1 when skewed (power of 2), else 0
     uint32_t G;              // 2x2x2 kernel: level-0 planes per group
     uint32_t zmask;          // 2x2x2 kernel: bit k = level k halves z
     uint32_t tw, th;         // chunk tile (x, y) in pixels

@@ -30,6 +30,14 @@ U8, U16, F32 = 0, 1, 8
 MEAN = 1
 BPP = {U8: 1, U16: 2, F32: 4}
 
+# Creation-time placement search (bench-only option): up to 16
+# placements of the chunk-layer rings timed on random frames, a losing
+# placement freed and a 128 MiB spacer held until the search ends (peak: two
+# ring sets + the spacers, counted by aqz_stage_estimate_memory_bench).
+PLACEMENT = dict(placement_tries=16, placement_mode=0, placement_spacer_bytes=128 << 20)
+
+DTYPE_WORDS = {U8: "uint8", U16: "uint16", F32: "float32"}
+
 CONFIGS = {
     # BASELINE.json configs[1] -- the metric's config.  The reference level
     # rule (downsampler.cpp:512-541) stops at 4 levels for 256-px chunks;
@@ -50,9 +58,10 @@ CONFIGS = {
                dims=[(TIME, 0, 32, 1), (SPACE, 4096, 128, 1), (SPACE, 4096, 128, 1)],
                dtype=U8, method=MEAN, force_levels=0, batch=32, ring=160),
     # BASELINE configs[3]: a 256-plane volume, 2x2x2 pyramid (z 256->128->
-    # 64->64, xy 2048->1024->512->256).  With --gpus N rank r's stream starts
-    # at its z slab (first_frame = r * 256/N, aligned to the 4-plane z
-    # groups) and runs on from there: one independent stream per GPU.
+    # 64->64, xy 2048->1024->512->256).  With --gpus N rank r owns z slab
+    # [lo, hi) of every volume of the stream (aqz_stage_options z_slab_*,
+    # slabs aligned to the 4-plane z groups): its stage receives only those
+    # planes, and frame ids skip the other ranks' planes.
     "c4": dict(workload="uint16 2048x2048x256 light-sheet volume, 4-level 3-D (2x2x2) "
                         "pyramid, 256x256x64 chunks, mean, device-resident",
                dims=[(TIME, 0, 1, 1), (SPACE, 256, 64, 1), (SPACE, 2048, 256, 1),
@@ -516,18 +525,20 @@ def main():
     dt = cfg["dtype"]
     B = args.batch or cfg["batch"]
     bpp = BPP[dt]
-    first = 0
+    slab = None
+    planes = None
     if args.config == "c4" and world > 1:
         from aqz.dist import z_levels, z_slab
         planes = [lv[1][1] for lv in aqz.pyramid_levels(cfg["dims"])]
-        first = z_slab(planes[0], world, rank, 1 << z_levels(planes))[0]
+        slab = z_slab(planes[0], world, rank, 1 << z_levels(planes))
 
     def run(pyramid_only, steps, warmup):
         """Time `steps` launches of B frames (after `warmup`) between
         barrier + device sync on both sides; max over ranks."""
-        st = aqz.Stage(cfg["dims"], dt, cfg["method"], force_levels=cfg["force_levels"],
-                       max_batch_frames=B, layer_slots=2, device=dev.index,
-                       skip_level0_split=pyramid_only, first_frame=first)
+        kw = dict(force_levels=cfg["force_levels"], max_batch_frames=B, layer_slots=2,
+                  skip_level0_split=pyramid_only, **PLACEMENT)
+        est = aqz.estimate_memory(cfg["dims"], dt, cfg["method"], **kw)
+        st = aqz.Stage(cfg["dims"], dt, cfg["method"], device=dev.index, z_slab=slab, **kw)
         # the stage runs on its own HIP stream; the timing marks below are
         # recorded by the library on that same stream
         sizes = level_sizes(st)
@@ -573,10 +584,17 @@ def main():
             kms = elapsed * 1e3
         kernel = st.dominant_kernel()
         placement = st.placement()
+        placement["estimate_device_bytes"] = est["device_bytes"]
+        placement["rings_bytes"] = sum(
+            x["chunk_pitch"] * x["chunks_per_layer"] * x["layer_slots"]
+            for x in (st.layout(l) for l in range(len(sizes))))
         # algorithmic bytes per launch: every input frame read once, plus
         # every frame each level emitted in the timed region written once
         # (a z-halving level emits half as many frames as its parent)
-        emitted = [st.frames_written(l) - fw0[l] for l in range(len(sizes))]
+        if slab:  # frame ids jump over other ranks' planes: count planes
+            emitted = [steps * B * planes[l] // planes[0] for l in range(len(sizes))]
+        else:
+            emitted = [st.frames_written(l) - fw0[l] for l in range(len(sizes))]
         st.close()
         del ring
         out_bytes = sum(n * h * w * bpp for n, (h, w) in zip(emitted[1:], sizes[1:]))
@@ -612,7 +630,8 @@ def main():
     traffic, traffic_src = pmc_traffic(args.config, args.pyramid_only, kernel)
 
     result = {
-        "metric": "input GB/s, device-resident multiscale downsample, uint16 frames @1/2/4/8 GPU",
+        "metric": f"input GB/s, device-resident multiscale downsample, {DTYPE_WORDS[dt]} "
+                  "frames @1/2/4/8 GPU",
         "value": round(value, 2),
         "unit": "GB/s",
         "n_gpus": world,
@@ -628,7 +647,10 @@ def main():
                                                   if args.pyramid_only else ""),
                    "frames_per_step_per_gpu": B, "levels": len(sizes),
                    "level_sizes": [f"{h}x{w}" for (h, w) in sizes],
-                   "parallelism": f"{world} independent per-GPU streams, no collective"},
+                   "parallelism": f"{world} independent per-GPU streams, no collective"
+                                  + (f"; rank r owns z slab [lo, hi) of every "
+                                     f"{planes[0]}-plane volume (rank 0: {list(slab)})"
+                                     if slab else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -638,11 +660,16 @@ def main():
                      "kernel": kernel,
                      "kernel_avg_ms": round(avg_ms, 5),
                      "alg_bytes_per_launch": alg_per_launch,
-                     # creation-time placement calibration of the chunk-layer
-                     # rings (ms per calibration launch of each candidate)
+                     # creation-time placement search of the chunk-layer rings:
+                     # ms per launch of each candidate (random frames), the one
+                     # kept, its re-time alone, the creation peak vs estimate
                      "placement": main_run["placement"]},
         "input_rate_frac_of_peak": round(value / world / HBM_PEAK_GBS, 4),
     }
+    pl = result["roofline"]["placement"]
+    if pl.get("kept_ms_final"):
+        # the steady state against the kept placement's own re-time
+        pl["steady_over_kept_final"] = round(avg_ms / pl["kept_ms_final"], 4)
     if probe:
         # this device's practical HBM rates, measured in this run (SURVEY
         # 8(d)): the dominant kernel against a plain streaming kernel of the

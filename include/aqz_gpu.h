@@ -220,6 +220,25 @@ typedef struct
                                   slab's first plane); level k starts at
                                   first_frame * planes_k / planes_0, which
                                   must be exact.  0 = a whole stream. */
+    uint32_t z_slab_begin;
+    uint32_t z_slab_end;       /* z-slab schedule over a stream of volumes
+                                  (BASELINE configs[3]): the stage
+                                  receives only planes [begin, end) of every
+                                  z stack (the level-0 dim ndims-3; a stack
+                                  is one index of the dims before it), in
+                                  order.  Frame ids skip the other planes:
+                                  after each slab every level's frame id
+                                  jumps by planes_k - (end_k - begin_k), so
+                                  z pairs (Downsampler::add_frame's
+                                  level_frame_count_ % planes,
+                                  downsampler.cpp:358-389) and chunk
+                                  placement (array.dimensions.cpp:264-314)
+                                  stay those of the whole stream.  begin and
+                                  end must scale exactly to every level
+                                  (multiples of 2^(z-halving levels)); the
+                                  first frame is first_frame + begin, with
+                                  first_frame a multiple of the stack size.
+                                  0, 0 = every plane. */
 } aqz_stage_options;
 
 typedef struct

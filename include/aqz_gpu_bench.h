@@ -26,7 +26,39 @@ typedef struct
                                   one above). */
     int32_t skip_level0_split; /* 1 = do not tile-split level 0 (the
                                   pyramid-only side measurement) */
+    uint32_t placement_tries;  /* creation-time placement search: 0/1 = off
+                                  (the drop-in default); n > 1 = time up to n
+                                  placements of the chunk-layer rings on
+                                  random frames and keep the fastest (the
+                                  launch time depends on the physical memory
+                                  the rings land in) */
+    uint32_t placement_mode;   /* 0: a losing placement is freed and a spacer
+                                  allocation held until the search ends
+                                  (peak: 2 ring sets + the spacers);
+                                  1: every candidate is held (peak: n sets) */
+    uint64_t placement_spacer_bytes; /* mode 0 spacer (0 = 128 MiB) */
 } aqz_stage_bench_options;
+
+/* aqz_stage_estimate_memory including the placement search's transient
+ * creation peak (bench may be NULL = aqz_stage_estimate_memory). */
+aqz_status aqz_stage_estimate_memory_bench(const aqz_array_desc* desc,
+                                           const aqz_stage_options* opt,
+                                           const aqz_stage_bench_options* bench,
+                                           aqz_memory_usage* out);
+
+/* What the placement search did. */
+typedef struct
+{
+    uint32_t n;                 /* candidates timed (0 = no search ran) */
+    uint32_t kept;              /* index of the kept one */
+    uint32_t reps;              /* timed launches per candidate (random frames) */
+    uint32_t mode;
+    double ms[32];              /* ms per launch, candidates 0..min(n,32)-1 */
+    double kept_ms_final;       /* the kept placement re-timed alone, after
+                                   the others were freed */
+    uint64_t peak_device_bytes; /* the stage's device bytes at the search's peak */
+} aqz_placement_report;
+aqz_status aqz_stage_placement_report(const aqz_stage* st, aqz_placement_report* out);
 
 /* aqz_stage_create with the bench extensions (bench may be NULL). */
 aqz_status aqz_stage_create_bench(const aqz_array_desc* desc,

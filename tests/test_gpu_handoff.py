@@ -61,6 +61,56 @@ def test_stage_band_handoff_matches_oracle(gpu):
     st.close()
 
 
+def test_stage_band_handoff_ragged_dim1(gpu):
+    """dim 1 not a multiple of its chunk (z 48 in 32-plane chunks): the
+    trailing band holds 16 planes and is complete with its layer
+    (flush_layer_remainder_, array.cpp:863-886), before any frame of the
+    next layer arrives."""
+    dims = [(TIME, 0, 1, 1), (SPACE, 48, 32, 1), (SPACE, 128, 64, 1), (SPACE, 128, 64, 1)]
+    frames = synthetic_frames(U16, 96, 128, 128, 7)  # two timepoints
+    exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
+    st = gpu.Stage(dims, U16, MEAN, max_batch_frames=8, layer_slots=3)
+    L = st.n_levels()
+    geo = [st.band_geometry(l) for l in range(L)]
+    lay = [st.layout(l) for l in range(L)]
+    assert geo[0][:3] == (True, 2, 32)
+    got = {}
+    nxt = [(0, 0)] * L  # (layer, band) to hand off next, per level
+    for b0 in range(0, 96, 8):
+        st.append(np.ascontiguousarray(frames[b0:b0 + 8]))
+        for l in range(L):
+            ok, nb, fpb, cpb = geo[l]
+            F = lay[l]["frames_per_layer"]
+            while True:
+                layer, band = nxt[l]
+                if (layer, 0) not in exp:
+                    break
+                end = layer * F + min((band + 1) * fpb, F)
+                if st.frames_written(l) < end:
+                    with pytest.raises(gpu.AqzError) as e:
+                        st.copy_band_async(l, layer, band, 0, 0)
+                    assert e.value.status == 3
+                    break
+                nbytes = cpb * lay[l]["bytes_per_chunk"]
+                buf, hd = gpu.HostBuffer(nbytes), gpu.HostBuffer(cpb)
+                st.copy_band_async(l, layer, band, buf.ptr, nbytes, hd.ptr, cpb)
+                got[(l, layer, band)] = (buf, hd)
+                nxt[l] = (layer, band + 1) if band + 1 < nb else (layer + 1, 0)
+        # the trailing band of layer 0 leaves with the layer's last frame
+        if b0 + 8 == 48:
+            assert (0, 0, 1) in got
+        st.wait_copies()
+    for (l, layer), (buf, flags) in exp.items():
+        ok, nb, fpb, cpb = geo[l]
+        bpc = lay[l]["bytes_per_chunk"]
+        for b in range(nb):
+            hb, hd = got[(l, layer, b)]
+            assert_same_pixels(hb.array.copy(), buf[b * cpb * bpc:(b + 1) * cpb * bpc],
+                               U16, f"L{l} layer {layer} band {b}")
+            assert np.array_equal(hd.array, flags[b * cpb:(b + 1) * cpb]), (l, layer, b)
+    st.close()
+
+
 def test_stage_band_geometry_without_banding(gpu):
     dims = [(TIME, 0, 4, 1), (SPACE, 64, 16, 1), (SPACE, 64, 16, 1)]
     st = gpu.Stage(dims, U16, MEAN)

@@ -55,10 +55,22 @@ def test_bench_c2_configuration_exact(gpu, cfg):
     c = bench.CONFIGS[cfg]
     dims, B = c["dims"], c["batch"]
     h, w = dims[-2][1], dims[-1][1]
-    st = gpu.Stage(dims, U16, MEAN, force_levels=c["force_levels"],
-                   max_batch_frames=B, layer_slots=2)
+    kw = dict(force_levels=c["force_levels"], max_batch_frames=B, layer_slots=2,
+              **bench.PLACEMENT)
+    est = gpu.estimate_memory(dims, U16, MEAN, **kw)
+    st = gpu.Stage(dims, U16, MEAN, **kw)
     L = st.n_levels()
     assert L == (5 if cfg == "c2" else 4)
+    # the bench's placement search ran; its creation peak is within the
+    # bench estimate, and the stage keeps one ring set afterwards
+    pl = st.placement()
+    assert 1 <= len(pl["candidates_ms"]) <= bench.PLACEMENT["placement_tries"]
+    assert pl["candidates_ms"][pl["kept"]] == min(pl["candidates_ms"])
+    assert 0 < pl["kept_ms_final"]
+    assert pl["peak_device_bytes"] <= est["device_bytes"]
+    assert st.memory_usage()["device_bytes"] <= gpu.estimate_memory(
+        dims, U16, MEAN, force_levels=c["force_levels"], max_batch_frames=B,
+        layer_slots=2)["device_bytes"]
     ldims = [st.level_dims(l) for l in range(L)]
     assert [d[-1][1] for d in ldims] == [2048, 1024, 512, 256, 128][:L]
     assert all(d[-1][2] == 256 and d[-2][2] == 256 for d in ldims)
@@ -126,8 +138,10 @@ def test_c4_volume_exact(gpu, c4_volume):
 
 def test_c4_z_slabs_over_4_stages(gpu, c4_volume):
     """The --gpus 4 decomposition on one device: 4 stages own the z slabs
-    [64r, 64r+64); OR-ing their chunk layers gives exactly the single-stage
-    layers (each slab writes only its own chunk regions; the rest stays 0)."""
+    [64r, 64r+64) of every volume (z_slab schedule) and get two volumes of a
+    stream (the second volume repeats the first's planes); OR-ing their chunk
+    layers gives exactly the single-stream layers of both volumes (each slab
+    writes only its own chunk regions; the rest stays 0)."""
     import aqz
     from aqz.dist import z_levels, z_slab
     c, frames, exp, fw, ldims = c4_volume
@@ -142,21 +156,23 @@ def test_c4_z_slabs_over_4_stages(gpu, c4_volume):
         lo, hi = z_slab(planes[0], 4, r, align)
         assert (lo, hi) == (64 * r, 64 * r + 64)
         st = gpu.Stage(dims, U16, MEAN, max_batch_frames=c["batch"], layer_slots=2,
-                       first_frame=lo)
-        st.append_ptr(ring.data_ptr() + lo * fbytes, hi - lo)
+                       z_slab=(lo, hi))
+        for vol in range(2):
+            st.append_ptr(ring.data_ptr() + lo * fbytes, hi - lo)
         stages.append(st)
     for st in stages:
         st.finalize()
-    for l in range(4):
-        assert stages[-1].frames_written(l) == fw[l]
+    for l in range(4):  # every stage's frame id is at its slab of volume 3
+        assert stages[-1].frames_written(l) == 2 * fw[l] + fw[l] * 3 // 4
     for (l, layer), (buf, flags) in sorted(exp.items()):
-        acc, facc = None, None
-        for st in stages:
-            got, gflags = st.copy_layer(l, layer)
-            acc = got if acc is None else np.bitwise_or(acc, got, out=acc)
-            facc = gflags if facc is None else np.maximum(facc, gflags)
-        assert_same_pixels(acc, buf, U16, f"slabs L{l} layer{layer}")
-        assert np.array_equal(facc, flags), (l, layer)
+        for vol in range(2):
+            acc, facc = None, None
+            for st in stages:
+                got, gflags = st.copy_layer(l, layer + vol)
+                acc = got if acc is None else np.bitwise_or(acc, got, out=acc)
+                facc = gflags if facc is None else np.maximum(facc, gflags)
+            assert_same_pixels(acc, buf, U16, f"slabs L{l} layer{layer + vol}")
+            assert np.array_equal(facc, flags), (l, layer + vol)
     for st in stages:
         st.close()
 

@@ -413,6 +413,61 @@ def test_stage_z_slab_sharding(gpu):
     b.close()
 
 
+@pytest.mark.parametrize("dims,batch", [
+    # fused 2x2x2 strip path (z 64 -> 32 -> 16, xy 256 -> 128 -> 64), G = 4
+    ([(TIME, 0, 1, 1), (SPACE, 64, 16, 1), (SPACE, 256, 64, 1), (SPACE, 256, 64, 1)], 8),
+    # generic cascade (level 2 keeps its xy size), slabs of 8 planes
+    ([(TIME, 0, 1, 1), (SPACE, 32, 8, 1), (SPACE, 128, 64, 1), (SPACE, 128, 64, 1)], 3),
+    # channels: every (t, c) stack is a z stack of its own
+    ([(TIME, 0, 1, 1), (CHANNEL, 2, 1, 1), (SPACE, 32, 8, 1), (SPACE, 128, 64, 1),
+      (SPACE, 128, 64, 1)], 16),
+])
+def test_stage_z_slab_schedule_volume_stream(gpu, dims, batch):
+    """A stream of volumes split into 4 z slabs (aqz_stage_options
+    z_slab_begin / z_slab_end; what --gpus 4 runs for C4): each stage gets
+    only its planes of every stack, its frame ids jump over the other
+    slabs', and the four stages' chunk layers OR together into the oracle's
+    single-stream layers (z pairing, downsampler.cpp:358-389; chunk
+    placement, array.dimensions.cpp:264-314)."""
+    from aqz.dist import z_levels, z_slab
+    Z, h, w = dims[-3][1], dims[-2][1], dims[-1][1]
+    stacks = 2 * (dims[1][1] if dims[1][0] == CHANNEL else 1)  # two timepoints
+    frames = synthetic_frames(U16, stacks * Z, h, w, 23 + Z)
+    exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
+    planes = [lv[-3][1] for lv in gpu.pyramid_levels(dims)]
+    zl = z_levels(planes)
+    stages = []
+    for r in range(4):
+        lo, hi = z_slab(Z, 4, r, 1 << zl)
+        st = gpu.Stage(dims, U16, MEAN, layer_slots=2 * stacks, max_batch_frames=batch,
+                       z_slab=(lo, hi))
+        for s in range(stacks):  # only this slab's planes of every stack
+            st.append(np.ascontiguousarray(frames[s * Z + lo:s * Z + hi]))
+        st.finalize()
+        # after each slab the frame id jumps to the next stack's slab
+        assert st.frames_written(0) == stacks * Z + lo
+        stages.append(st)
+    for (l, layer), (buf, flags) in exp.items():
+        got = [st.copy_layer(l, layer) for st in stages]
+        acc = got[0][0].copy()
+        hd = got[0][1].copy()
+        for g, f in got[1:]:
+            np.bitwise_or(acc, g, out=acc)
+            np.maximum(hd, f, out=hd)
+        assert_same_pixels(acc, buf, U16, f"L{l} layer {layer}")
+        assert np.array_equal(hd, flags), (l, layer)
+    for st in stages:
+        st.close()
+
+
+def test_stage_z_slab_rejects_misaligned(gpu):
+    dims = [(TIME, 0, 1, 1), (SPACE, 64, 16, 1), (SPACE, 256, 64, 1), (SPACE, 256, 64, 1)]
+    with pytest.raises(gpu.AqzError):
+        gpu.Stage(dims, U16, MEAN, z_slab=(2, 18))  # z halves twice: multiples of 4
+    with pytest.raises(gpu.AqzError):
+        gpu.Stage(dims, U16, MEAN, z_slab=(16, 16))
+
+
 @pytest.mark.parametrize("pad", [0, 4224])
 def test_stage_async_handoff_pinned_and_pageable(gpu, pad, monkeypatch):
     """The ingestion / hand-off pipeline: pinned and pageable (multi-threaded
