@@ -658,6 +658,39 @@ aqz_stage_frames_consumed(aqz_stage* st)
 }
 
 aqz_status
+aqz_stage_wait_consumed(aqz_stage* st, uint64_t frames)
+{
+    return guard_sticky(st, [&] { st->st->wait_consumed(frames); });
+}
+
+uint64_t
+aqz_stage_last_ticket(const aqz_stage* st)
+{
+    return st ? st->st->last_ticket() : 0;
+}
+
+uint64_t
+aqz_stage_copies_completed(aqz_stage* st)
+{
+    if (!st || st->sticky != AQZ_STATUS_SUCCESS)
+        return 0;
+    uint64_t n = 0;
+    if (guard_sticky(st, [&] { n = st->st->copies_completed(); }) != AQZ_STATUS_SUCCESS)
+        return 0;
+    return n;
+}
+
+aqz_status
+aqz_stage_wait_ticket(aqz_stage* st, uint64_t ticket)
+{
+    return guard_sticky(st, [&] {
+        if (ticket > st->st->last_ticket())
+            throw Error(AQZ_STATUS_INVALID_ARGUMENT, "ticket not issued");
+        st->st->copies_completed(false, ticket);
+    });
+}
+
+aqz_status
 aqz_stage_copy_layer(aqz_stage* st, uint32_t level, uint64_t layer, void* dst,
                      size_t cap, uint8_t* has_data, size_t has_data_cap,
                      int32_t mem)

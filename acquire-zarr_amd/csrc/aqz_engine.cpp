@@ -663,6 +663,8 @@ Stage::~Stage()
     for (size_t i = inflight_head_; i < inflight_.size(); ++i)
         if (inflight_[i].first)
             free_ev_.push_back(inflight_[i].first);
+    for (hipEvent_t e : tickets_)
+        free_ev_.push_back(e);
     for (hipEvent_t e : free_ev_)
         (void)hipEventDestroy(e);
     for (auto& L : lv_) {
@@ -798,6 +800,64 @@ Stage::frames_consumed()
 {
     retire_consumed(false);
     return consumed_;
+}
+
+// Blocks on the consumption events (no spin) until `frames` level-0 frames
+// of the appended sources have been read.
+void
+Stage::wait_consumed(uint64_t frames)
+{
+    if (frames > appended_)
+        throw Error(1, "wait_consumed beyond the frames appended");
+    while (consumed_ < frames && inflight_head_ < inflight_.size()) {
+        auto& [e, n] = inflight_[inflight_head_];
+        if (e) {
+            hip_check(hipEventSynchronize(e), "hipEventSynchronize");
+            free_ev_.push_back(e);
+        }
+        consumed_ = n;
+        ++inflight_head_;
+    }
+    retire_consumed(false);
+}
+
+// Hand-off tickets: every copy_*_async call records one event on the
+// hand-off stream after its copies; ticket i (1-based, issue order) is
+// complete once that event is.  The D2H stream is in order, so tickets
+// complete in order.
+uint64_t
+Stage::issue_ticket()
+{
+    hipEvent_t e;
+    if (free_ev_.empty()) {
+        hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    } else {
+        e = free_ev_.back();
+        free_ev_.pop_back();
+    }
+    hip_check(hipEventRecord(e, d2h_), "hipEventRecord");
+    tickets_.push_back(e);
+    return ++tickets_issued_;
+}
+
+uint64_t
+Stage::copies_completed(bool wait_all, uint64_t until)
+{
+    while (!tickets_.empty() && tickets_done_ < tickets_issued_) {
+        hipEvent_t e = tickets_.front();
+        if (wait_all || tickets_done_ < until) {
+            hip_check(hipEventSynchronize(e), "hipEventSynchronize");
+        } else {
+            const hipError_t q = hipEventQuery(e);
+            if (q == hipErrorNotReady)
+                break;
+            hip_check(q, "hipEventQuery");
+        }
+        free_ev_.push_back(e);
+        tickets_.pop_front();
+        ++tickets_done_;
+    }
+    return tickets_done_;
 }
 
 void
@@ -1359,6 +1419,7 @@ Stage::copy_layer_async(uint32_t level, uint64_t layer, void* dst, size_t cap,
     }
     hip_check(hipEventRecord(L.copy_ev[slot], d2h_), "hipEventRecord");
     L.copy_pending[slot] = 1;
+    last_ticket_ = issue_ticket();
 }
 
 void
@@ -1427,6 +1488,7 @@ Stage::copy_band_async(uint32_t level, uint64_t layer, uint32_t band, void* dst,
     }
     hip_check(hipEventRecord(L.copy_ev[slot], d2h_), "hipEventRecord");
     L.copy_pending[slot] = 1;
+    last_ticket_ = issue_ticket();
 }
 
 void
@@ -2076,6 +2138,7 @@ Stage::copy_compressed_async(uint32_t level, uint64_t layer, void* dst, size_t c
     hip_check(hipEventRecord(L.cdone_ev[slot], d2h_), "hipEventRecord");
     L.copy_pending[slot] = 1;
     L.cdone_pending[slot] = 1;
+    last_ticket_ = issue_ticket();
 }
 
 void

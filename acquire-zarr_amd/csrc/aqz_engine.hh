@@ -16,6 +16,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <deque>
 #include <memory>
 #include <string>
 #include <vector>
@@ -290,6 +291,10 @@ class Stage
     uint64_t frames_written(uint32_t level) const;
     // level-0 frames whose source bytes the stage has finished reading
     uint64_t frames_consumed();
+    void wait_consumed(uint64_t frames);
+    // hand-off tickets (one per copy_*_async call, 1-based, in issue order)
+    uint64_t last_ticket() const { return last_ticket_; }
+    uint64_t copies_completed(bool wait_all = false, uint64_t until = 0);
     void copy_layer(uint32_t level, uint64_t layer, void* dst, size_t cap,
                     uint8_t* has_data, size_t has_data_cap, int mem);
     void device_layer(uint32_t level, uint64_t layer, void** chunks,
@@ -410,6 +415,9 @@ class Stage
     size_t inflight_head_ = 0;
     std::vector<hipEvent_t> free_ev_;
     uint64_t appended_ = 0, consumed_ = 0;
+    std::deque<hipEvent_t> tickets_;  // hand-off copies not yet retired
+    uint64_t tickets_issued_ = 0, tickets_done_ = 0, last_ticket_ = 0;
+    uint64_t issue_ticket();
     void note_consumed(hipStream_t s, uint64_t frames);
     void retire_consumed(bool wait);
     uint32_t nt_mode_ = 7;           // nontemporal policy: input loads (1), level-0 (2) and level-1/2 (4) stores

@@ -288,6 +288,11 @@ uint64_t aqz_stage_frames_written(const aqz_stage* st, uint32_t level);
 /* Level-0 frames appended so far whose source bytes the stage has finished
  * reading (in append order): their source buffers may be reused. */
 uint64_t aqz_stage_frames_consumed(aqz_stage* st);
+/* Block (on events, no spin) until at least `frames` appended level-0
+ * frames have been read: the reference's frame queue hands its buffer back
+ * when the consumer pops it (frame.queue.cpp:48-73); a caller that appends
+ * pinned batches from a double buffer waits here before refilling one. */
+aqz_status aqz_stage_wait_consumed(aqz_stage* st, uint64_t frames);
 /* Copy chunk layer `layer` of `level` (must still be resident) to dst
  * (bytes_per_chunk*chunks_per_layer bytes) and its has_data flags (one byte
  * per chunk, 1 = some byte of the chunk is nonzero).  Synchronizes.  Frames
@@ -307,6 +312,19 @@ aqz_status aqz_stage_copy_layer_async(aqz_stage* st, uint32_t level,
                                       uint64_t layer, void* dst, size_t cap,
                                       uint8_t* has_data, size_t has_data_cap);
 aqz_status aqz_stage_wait_copies(aqz_stage* st);
+/* Hand-off tickets.  Every aqz_stage_copy_layer_async,
+ * aqz_stage_copy_band_async and aqz_stage_copy_compressed_async call that
+ * succeeds is one ticket, numbered 1, 2, ... in call order;
+ * aqz_stage_last_ticket returns the newest.  aqz_stage_copies_completed
+ * returns (without blocking) how many tickets have completed -- their
+ * destination bytes are in place -- and tickets complete in order.
+ * aqz_stage_wait_ticket blocks until ticket `ticket` has completed.  With
+ * these a caller installs each handed-off unit into its host chunk buffers
+ * (Array::chunks_) when its copy lands, in frame order, and never waits
+ * for copies issued after it (cf. the flush in array.cpp:209-219). */
+uint64_t aqz_stage_last_ticket(const aqz_stage* st);
+uint64_t aqz_stage_copies_completed(aqz_stage* st);
+aqz_status aqz_stage_wait_ticket(aqz_stage* st, uint64_t ticket);
 
 /* ---- dim-1 banding ---------------------------------------------------------
  * Array::flush_completed_bands_ (array.cpp:873-908) flushes the chunks of a

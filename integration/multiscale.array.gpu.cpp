@@ -16,7 +16,8 @@
 //                         appends frames to the aqz stage -- level-0 tile
 //                         split, Downsampler::add_frame and every level's
 //                         tile split on the device -- and hands completed
-//                         layers to the per-level GpuArrays.  Metadata
+//                         layers to the per-level GpuArrays through the
+//                         asynchronous hand-off of aqz_handoff.hh.  Metadata
 //                         (zarr.json, OME multiscales) stays the reference's:
 //                         the base class keeps its Downsampler for level
 //                         geometry and get_metadata(), which aqz reproduces
@@ -31,8 +32,8 @@
 #include "zarr.common.hh"
 
 #include "aqz_gpu.h"
+#include "aqz_handoff.hh"
 
-#include <cstring>
 #include <memory>
 #include <vector>
 
@@ -96,7 +97,9 @@ class GpuArray final : public Array
     bool close_array() { return close_(); }
 };
 
-class GpuMultiscaleArray final : public MultiscaleArray
+class GpuMultiscaleArray final
+  : public MultiscaleArray
+  , private aqz_binding::HandoffSink
 {
   public:
     // settings: the ZarrArraySettings the stream was configured with
@@ -107,9 +110,9 @@ class GpuMultiscaleArray final : public MultiscaleArray
                        std::shared_ptr<S3ConnectionPool> s3_connection_pool,
                        const ZarrArraySettings& settings,
                        int device,
-                       uint32_t batch_frames = 64)
+                       uint32_t batch_frames = 64,
+                       uint32_t host_slots = 2)
       : MultiscaleArray(config, thread_pool, file_handle_pool, s3_connection_pool)
-      , batch_(batch_frames)
     {
         EXPECT(downsampler_ != nullptr, "GpuMultiscaleArray needs a downsampling method");
         // per-level writers that take GPU-filled layers (create_arrays_,
@@ -139,38 +142,22 @@ class GpuMultiscaleArray final : public MultiscaleArray
                              settings.storage_dimension_order,
                              device };
         aqz_stage_options opt{};
-        opt.max_batch_frames = batch_;
+        opt.max_batch_frames = batch_frames;
         opt.layer_slots = 2;
         EXPECT(aqz_stage_create(&desc, &opt, &stage_) == AQZ_STATUS_SUCCESS,
                "aqz_stage_create failed");
-        const uint32_t nl = aqz_stage_n_levels(stage_);
-        EXPECT(nl == arrays_.size(), "level count differs from the Downsampler's");
-        levels_.resize(nl);
-        for (uint32_t l = 0; l < nl; ++l) {
-            Level& L = levels_[l];
-            CHECK(aqz_stage_level_layout(stage_, l, &L.lay) == AQZ_STATUS_SUCCESS);
-            int32_t banded = 0;
-            CHECK(aqz_stage_band_geometry(stage_, l, &banded, &L.n_bands,
-                                          &L.frames_per_band,
-                                          &L.chunks_per_band) == AQZ_STATUS_SUCCESS);
-            L.banded = banded != 0;
-            const size_t nbytes = L.lay.bytes_per_chunk * L.chunks_per_band;
-            CHECK(aqz_host_alloc(nbytes, reinterpret_cast<void**>(&L.chunks)) ==
-                  AQZ_STATUS_SUCCESS);
-            CHECK(aqz_host_alloc(L.chunks_per_band, reinterpret_cast<void**>(&L.has)) ==
-                  AQZ_STATUS_SUCCESS);
-        }
-        CHECK(aqz_host_alloc(size_t(batch_) * bytes_per_frame_,
-                             reinterpret_cast<void**>(&batch_buf_)) == AQZ_STATUS_SUCCESS);
+        EXPECT(aqz_stage_n_levels(stage_) == arrays_.size(),
+               "level count differs from the Downsampler's");
+        aqz_binding::HandoffSink& sink = *this;
+        handoff_ = std::make_unique<aqz_binding::Handoff>(stage_, bytes_per_frame_,
+                                                          batch_frames, host_slots, sink);
+        EXPECT(handoff_->status() == AQZ_STATUS_SUCCESS, "aqz hand-off buffers: ",
+               aqz_status_message(handoff_->status()));
     }
 
     ~GpuMultiscaleArray() override
     {
-        for (Level& L : levels_) {
-            aqz_host_free(L.chunks);
-            aqz_host_free(L.has);
-        }
-        aqz_host_free(batch_buf_);
+        handoff_.reset();
         aqz_stage_destroy(stage_);
     }
 
@@ -178,15 +165,13 @@ class GpuMultiscaleArray final : public MultiscaleArray
     {
         aqz_memory_usage m{};
         (void)aqz_stage_memory_usage(stage_, &m);
-        size_t staging = size_t(batch_) * bytes_per_frame_;
-        for (const Level& L : levels_)
-            staging += L.lay.bytes_per_chunk * L.chunks_per_band + L.chunks_per_band;
-        return MultiscaleArray::memory_usage() + m.pinned_bytes + staging;
+        return MultiscaleArray::memory_usage() + m.pinned_bytes + handoff_->host_bytes();
     }
 
     // MultiscaleArray::write_frame (multiscale.array.cpp:57-74) with the
-    // checks of Array::write_frame (array.cpp:160-189).  Frames are
-    // batched into pinned memory and appended `batch_` at a time.
+    // checks of Array::write_frame (array.cpp:160-189).  The hand-off
+    // batches frames into pinned memory; nothing here waits for the GPU
+    // except to refill a batch buffer the stage has not read yet.
     [[nodiscard]] WriteResult write_frame(std::vector<uint8_t>& frame,
                                           size_t& bytes_written,
                                           uint64_t frame_id) override
@@ -194,20 +179,15 @@ class GpuMultiscaleArray final : public MultiscaleArray
         bytes_written = 0;
         if (frame.size() != bytes_per_frame_)
             return WriteResult::FrameSizeMismatch;
-        if (frame_id != frames_accepted_)
+        if (frame_id != handoff_->frames_accepted())
             return WriteResult::FrameOutOfOrder;
         const uint64_t max = arrays_[0]->max_bytes();
-        if (max > 0 && (frames_accepted_ + 1) * bytes_per_frame_ > max)
+        if (max > 0 && (handoff_->frames_accepted() + 1) * bytes_per_frame_ > max)
             return WriteResult::OutOfBounds;
-        std::memcpy(batch_buf_ + size_t(n_batched_) * bytes_per_frame_, frame.data(),
-                    bytes_per_frame_);
-        ++n_batched_;
-        ++frames_accepted_;
-        if (n_batched_ == batch_) {
-            const WriteResult r = append_batch_();
-            if (r != WriteResult::Ok)
-                return r;
-        }
+        const aqz_status s = handoff_->write_frame(frame.data());
+        if (s == AQZ_STATUS_WRITE_OUT_OF_BOUNDS)
+            return WriteResult::OutOfBounds;
+        EXPECT(s == AQZ_STATUS_SUCCESS, "aqz stage: ", aqz_status_message(s));
         bytes_written = frame.size();
         return WriteResult::Ok;
     }
@@ -216,12 +196,8 @@ class GpuMultiscaleArray final : public MultiscaleArray
     bool close_() override
     {
         try {
-            if (append_batch_() != WriteResult::Ok)
-                return false;
-            // zero-fill the partial last layer of every level (chunk.cpp:
-            // 8-15) and hand it over unflushed; Array::close_ flushes it
-            CHECK(aqz_stage_finalize(stage_) == AQZ_STATUS_SUCCESS);
-            CHECK(hand_off_(true) == WriteResult::Ok);
+            const aqz_status s = handoff_->close();
+            EXPECT(s == AQZ_STATUS_SUCCESS, "aqz stage: ", aqz_status_message(s));
         } catch (const std::exception& exc) {
             LOG_ERROR("Failed to finalize the GPU stage: ", exc.what());
             return false;
@@ -230,75 +206,24 @@ class GpuMultiscaleArray final : public MultiscaleArray
     }
 
   private:
-    struct Level
+    // aqz_binding::HandoffSink: units land in frame order per level
+    void install(uint32_t level, const uint8_t* chunks, const uint8_t* has_data, uint32_t c0,
+                 uint32_t n) override
     {
-        aqz_level_layout lay{};
-        bool banded = false;
-        uint32_t n_bands = 1, chunks_per_band = 0;
-        uint64_t frames_per_band = 0;
-        uint64_t handed = 0; // frames of this level handed to its GpuArray
-        uint8_t* chunks = nullptr;
-        uint8_t* has = nullptr;
-    };
-
-    WriteResult append_batch_()
-    {
-        if (n_batched_ == 0)
-            return WriteResult::Ok;
-        const aqz_status s =
-          aqz_stage_append(stage_, batch_buf_, n_batched_, AQZ_MEM_HOST_PINNED);
-        if (s == AQZ_STATUS_WRITE_OUT_OF_BOUNDS)
-            return WriteResult::OutOfBounds;
-        EXPECT(s == AQZ_STATUS_SUCCESS, "aqz_stage_append: ", aqz_status_message(s));
-        // the pinned batch is read asynchronously: reuse it once consumed
-        while (aqz_stage_frames_consumed(stage_) < frames_accepted_)
-            ;
-        n_batched_ = 0;
-        return hand_off_(false);
+        gpu_arrays_[level]->install_chunks(chunks, has_data, c0, n);
     }
 
-    // Every complete unit (a dim-1 band where Array::flush_completed_bands_
-    // applies, else a chunk layer) of every level goes D2H and into its
-    // GpuArray, in frame order.  final: also the partial last unit.
-    WriteResult hand_off_(bool final)
+    aqz_status commit(uint32_t level, uint64_t frames, bool flush) override
     {
-        for (uint32_t l = 0; l < levels_.size(); ++l) {
-            Level& L = levels_[l];
-            const uint64_t written = aqz_stage_frames_written(stage_, l);
-            const uint64_t unit = L.banded ? L.frames_per_band : L.lay.frames_per_layer;
-            while (L.handed + unit <= written || (final && L.handed < written)) {
-                const uint64_t layer = L.handed / L.lay.frames_per_layer;
-                const uint32_t band =
-                  L.banded ? uint32_t((L.handed % L.lay.frames_per_layer) / unit) : 0;
-                const size_t nbytes = L.lay.bytes_per_chunk * L.chunks_per_band;
-                if (L.banded)
-                    CHECK(aqz_stage_copy_band_async(stage_, l, layer, band, L.chunks, nbytes,
-                                                    L.has, L.chunks_per_band) ==
-                          AQZ_STATUS_SUCCESS);
-                else
-                    CHECK(aqz_stage_copy_layer_async(stage_, l, layer, L.chunks, nbytes, L.has,
-                                                     L.chunks_per_band) == AQZ_STATUS_SUCCESS);
-                CHECK(aqz_stage_wait_copies(stage_) == AQZ_STATUS_SUCCESS);
-                gpu_arrays_[l]->install_chunks(L.chunks, L.has, band * L.chunks_per_band,
-                                               L.chunks_per_band);
-                const uint64_t n = std::min(unit, written - L.handed);
-                const WriteResult r = gpu_arrays_[l]->commit_frames(n, n == unit);
-                if (r != WriteResult::Ok)
-                    return r;
-                L.handed += n;
-            }
-        }
-        return WriteResult::Ok;
+        return gpu_arrays_[level]->commit_frames(frames, flush) == WriteResult::Ok
+                 ? AQZ_STATUS_SUCCESS
+                 : AQZ_STATUS_WRITE_OUT_OF_BOUNDS;
     }
 
     aqz_stage* stage_ = nullptr;
     std::vector<aqz_dimension> dims_;
     std::vector<GpuArray*> gpu_arrays_;
-    std::vector<Level> levels_;
-    const uint32_t batch_;
-    uint8_t* batch_buf_ = nullptr;
-    uint32_t n_batched_ = 0;
-    uint64_t frames_accepted_ = 0;
+    std::unique_ptr<aqz_binding::Handoff> handoff_;
 };
 
 } // namespace zarr

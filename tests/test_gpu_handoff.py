@@ -166,3 +166,78 @@ def test_stage_append_cuda_tensor_from_side_stream(gpu):
         assert np.array_equal(gflags, flags)
     assert not st._held  # released once consumed
     st.close()
+
+
+def _run_replay(tmp_path, dims, dtype, method, frames, batch, slots):
+    """tests/native/handoff_replay: the binding's hand-off
+    (integration/aqz_handoff.hh, what GpuMultiscaleArray runs) over the C
+    ABI with a recording sink.  Returns (commit log, {(level, layer): (bytes,
+    has_data)})."""
+    import json
+    import os
+    import struct
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "handoff_replay")
+    assert os.path.exists(exe), "make -C tests/native (built by __graft_entry__.build)"
+    job, out = tmp_path / "job.bin", tmp_path / "out.bin"
+    fb = frames[0].nbytes
+    with open(job, "wb") as f:
+        f.write(b"AQZJ" + struct.pack("<I", len(dims)))
+        for d in dims:
+            f.write(struct.pack("<iIII", *d))
+        f.write(struct.pack("<iiIIQQ", dtype, method, batch, slots, len(frames), fb))
+        f.write(np.ascontiguousarray(frames).tobytes())
+    r = subprocess.run([exe, str(job), str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    log = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert log[-1]["summary"] and log[-1]["ok"]
+    got = {}
+    b = out.read_bytes()
+    assert b[:4] == b"AQZO"
+    (nl,), o = struct.unpack_from("<I", b, 4), 8
+    for l in range(nl):
+        n, lb, nc = struct.unpack_from("<QQI", b, o)
+        o += 20
+        for _ in range(n):
+            (layer,) = struct.unpack_from("<Q", b, o)
+            o += 8
+            got[(l, layer)] = (np.frombuffer(b, np.uint8, lb, o),
+                               np.frombuffer(b, np.uint8, nc, o + lb))
+            o += lb + nc
+    return log[:-1], got
+
+
+@pytest.mark.parametrize("case", ["banded-3d", "layers-2d-ragged"])
+def test_binding_handoff_replay(gpu, tmp_path, case):
+    """The reference-side binding's consumer path, replayed natively: frames
+    batched into pinned double buffers, asynchronous appends refilled after
+    aqz_stage_wait_consumed, every complete band / layer copied D2H into a
+    2-slot host ring and installed when its ticket completes.  Commits are
+    contiguous and in frame order per level (Array::write_frame's order,
+    array.cpp:196-219), only the partial last unit is unflushed, and every
+    installed layer equals the oracle's (MultiscaleArray::write_frame,
+    multiscale.array.cpp:57-74, 291-325)."""
+    if case == "banded-3d":
+        dims = [(TIME, 0, 1, 1), (SPACE, 64, 16, 1), (SPACE, 256, 64, 1), (SPACE, 256, 64, 1)]
+        frames = synthetic_frames(U16, 2 * 64 + 24, 256, 256, 61)  # 2 volumes + a partial
+        batch = 8
+    else:
+        dims = [(TIME, 0, 4, 1), (SPACE, 300, 64, 1), (SPACE, 260, 64, 1)]
+        frames = synthetic_frames(U16, 4 * 9 + 3, 300, 260, 62)  # ragged last layer
+        batch = 5
+    exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
+    log, got = _run_replay(tmp_path, dims, U16, MEAN, frames, batch, 2)
+    per = {}
+    for e in log:
+        prev = per.setdefault(e["level"], [])
+        assert e["first"] == sum(x["frames"] for x in prev), e  # contiguous, in order
+        prev.append(e)
+    for l, commits in per.items():
+        assert sum(c["frames"] for c in commits) == fw[l]
+        assert all(c["flush"] for c in commits[:-1])
+    if case == "banded-3d":
+        assert len(per[0]) > 2 * 4  # bands, not layers
+    assert set(got) == set(exp)
+    for key, (buf, flags) in exp.items():
+        assert_same_pixels(got[key][0].copy(), buf, U16, f"L{key[0]} layer {key[1]}")
+        assert np.array_equal(got[key][1], flags), key
