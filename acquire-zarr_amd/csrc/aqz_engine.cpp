@@ -1743,6 +1743,10 @@ Compressor::Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compressio
         throw Error(4, "unknown codec");
     if (c.codec != 3 && (c.shuffle < 0 || c.shuffle > 2 || c.clevel < 0 || c.clevel > 9))
         throw Error(1, "invalid compression settings");
+    // stock zstd: levels 0-22, no shuffle (validate_compression_settings,
+    // zarr.stream.cpp:139-153)
+    if (c.codec == 3 && (c.clevel < 0 || c.clevel > 22 || c.shuffle != 0))
+        throw Error(1, "invalid zstd settings: level 0-22 and no shuffle");
     if (chunk_bytes == 0 || chunk_bytes > 0x7fffffefull || typesize == 0 ||
         typesize > 255)
         throw Error(1, "chunk size outside the blosc1 limits");

@@ -133,14 +133,14 @@ unshuffle_block(int sh, uint32_t ts, const uint8_t* src, uint8_t* dst, uint32_t 
     }
 }
 
-// c-blosc 1.x's zstd level for a blosc clevel (zstd_wrap_compress)
+// c-blosc 1.x's zstd level for a blosc clevel (zstd_wrap_compress): it
+// reassigns clevel = clevel < 9 ? 2 * clevel - 1 : ZSTD_maxCLevel() and only
+// then tests `clevel == 8`, which the odd or maximal value never is -- so the
+// effective map is 2c - 1 for c < 9 and the maximum level for 9.
 int
 blosc_zstd_level(const ZstdLib& z, int clevel)
 {
-    int l = clevel < 9 ? clevel * 2 - 1 : z.max_clevel();
-    if (clevel == 8)
-        l = z.max_clevel() - 2;
-    return l;
+    return clevel < 9 ? clevel * 2 - 1 : z.max_clevel();
 }
 
 struct CCtx

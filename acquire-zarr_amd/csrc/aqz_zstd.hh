@@ -99,29 +99,36 @@ struct BitW
 };
 
 // ---- FSE -------------------------------------------------------------------
-constexpr uint32_t kFseMaxLog = 6;
+constexpr uint32_t kFseMaxLog = 6;  // predefined sequence tables, Huffman weights
+constexpr uint32_t kSeqMaxLog = 9;  // custom sequence tables (LL/ML 9, OF 8)
 constexpr uint32_t kFseMaxSym = 53;
 
-struct FseCT
+template<uint32_t LOG>
+struct FseTable
 {
-    uint16_t st[1u << kFseMaxLog]; // next state values, by symbol
-    uint32_t dnb[kFseMaxSym];      // deltaNbBits
-    int32_t dfs[kFseMaxSym];       // deltaFindState
+    uint16_t st[1u << LOG];   // next state values, by symbol
+    uint32_t dnb[kFseMaxSym]; // deltaNbBits
+    int32_t dfs[kFseMaxSym];  // deltaFindState
     uint32_t al;
 };
+using FseCT = FseTable<kFseMaxLog>;
 
 // norm: normalized counts of symbols 0..maxsym (-1 = "less than 1"),
 // summing to 1 << al.  false when the distribution is not valid.
-struct FseBuildWork
+template<uint32_t LOG>
+struct FseBuildWorkT
 {
-    uint8_t sym[1u << kFseMaxLog];
+    uint8_t sym[1u << LOG];
     uint32_t cumul[kFseMaxSym + 1];
 };
+using FseBuildWork = FseBuildWorkT<kFseMaxLog>;
 
+template<uint32_t LOG>
 __host__ __device__ inline bool
-fse_build(FseCT& ct, const int16_t* norm, uint32_t maxsym, uint32_t al, FseBuildWork& bw)
+fse_build(FseTable<LOG>& ct, const int16_t* norm, uint32_t maxsym, uint32_t al,
+          FseBuildWorkT<LOG>& bw)
 {
-    if (al > kFseMaxLog || maxsym >= kFseMaxSym)
+    if (al > LOG || maxsym >= kFseMaxSym)
         return false;
     const uint32_t ts = 1u << al, mask = ts - 1, step = (ts >> 1) + (ts >> 3) + 3;
     uint8_t* sym = bw.sym;
@@ -174,32 +181,36 @@ fse_build(FseCT& ct, const int16_t* norm, uint32_t maxsym, uint32_t al, FseBuild
     return true;
 }
 
+template<uint32_t LOG>
 __host__ __device__ inline bool
-fse_build(FseCT& ct, const int16_t* norm, uint32_t maxsym, uint32_t al)
+fse_build(FseTable<LOG>& ct, const int16_t* norm, uint32_t maxsym, uint32_t al)
 {
-    FseBuildWork bw;
+    FseBuildWorkT<LOG> bw;
     return fse_build(ct, norm, maxsym, al, bw);
 }
 
 // first (= last encoded) symbol: the smallest state, no bits out
+template<uint32_t LOG>
 __host__ __device__ inline uint32_t
-fse_init(const FseCT& ct, uint32_t s)
+fse_init(const FseTable<LOG>& ct, uint32_t s)
 {
     const uint32_t nbo = (ct.dnb[s] + (1u << 15)) >> 16;
     const uint32_t v = (nbo << 16) - ct.dnb[s];
     return ct.st[int32_t(v >> nbo) + ct.dfs[s]];
 }
 
+template<uint32_t LOG>
 __host__ __device__ inline void
-fse_enc(BitW& w, uint32_t& state, const FseCT& ct, uint32_t s)
+fse_enc(BitW& w, uint32_t& state, const FseTable<LOG>& ct, uint32_t s)
 {
     const uint32_t nbo = (state + ct.dnb[s]) >> 16;
     w.add(state, nbo);
     state = ct.st[int32_t(state >> nbo) + ct.dfs[s]];
 }
 
+template<uint32_t LOG>
 __host__ __device__ inline void
-fse_flush(BitW& w, uint32_t state, const FseCT& ct)
+fse_flush(BitW& w, uint32_t state, const FseTable<LOG>& ct)
 {
     w.add(state, ct.al);
 }

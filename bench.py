@@ -273,7 +273,8 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
                 i = handed[l] % 4
                 if codec:
                     st.compress_layer(l, handed[l], codec=codec,
-                                      clevel=3 if codec == 3 else 5, shuffle=args.compress)
+                                      clevel=3 if codec == 3 else 5,
+                                      shuffle=0 if codec == 3 else args.compress)
                     pending.append((l, handed[l]))
                 else:
                     st.copy_layer_async(l, handed[l], dst[l][i].ptr, lbytes[l],
@@ -357,7 +358,8 @@ def run_paced(torch, aqz, dev, cfg, args):
     fbytes = sizes[0][0] * sizes[0][1] * bpp
     lay = [st.layout(l) for l in range(L)]
     lbytes = [x["bytes_per_chunk"] * x["chunks_per_layer"] for x in lay]
-    R = max(4 * b, int(args.fps * 0.25))  # a quarter second of camera buffer
+    # a quarter second of camera buffer (--camera-ring overrides)
+    R = args.camera_ring or max(4 * b, int(args.fps * 0.25))
     ring = aqz.HostBuffer(R * fbytes)
     frame = np.random.default_rng(3).integers(0, 256, size=fbytes, dtype=np.uint8)
     ring.array.reshape(R, fbytes)[:] = frame  # pixel values do not change the cost
@@ -409,6 +411,7 @@ def run_paced(torch, aqz, dev, cfg, args):
         lat.append(time.perf_counter() - t_arr)
         done_frames += n
     el = time.perf_counter() - t0
+    frames_written0 = st.frames_written(0)
     st.close()
     lat_ms = np.array(lat) * 1e3
     return {
@@ -417,6 +420,7 @@ def run_paced(torch, aqz, dev, cfg, args):
         "value": round(done_frames / el, 1), "unit": "frames/s", "n_gpus": 1,
         "higher_is_better": True, "target_fps": args.fps, "frames": n_total,
         "processed": done_frames, "drops": drops, "batch": b, "camera_ring_frames": R,
+        "appended": appended, "stage_frames_written": frames_written0,
         "latency_ms": {"p50": round(float(np.percentile(lat_ms, 50)), 2),
                        "p99": round(float(np.percentile(lat_ms, 99)), 2),
                        "max": round(float(lat_ms.max()), 2)},
@@ -464,6 +468,9 @@ def main():
                          "reports sustained fps, drops and latency")
     ap.add_argument("--seconds", type=float, default=5.0,
                     help="duration of the --fps run")
+    ap.add_argument("--camera-ring", type=int, default=0,
+                    help="--fps run: frames in the simulated camera's pinned ring "
+                         "(default a quarter second)")
     ap.add_argument("--batch", type=int, default=0,
                     help="frames per append (default: the config's batch)")
     ap.add_argument("--compress", type=int, default=0, choices=[0, 1, 2],

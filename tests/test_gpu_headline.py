@@ -219,3 +219,38 @@ def test_hbm_probe_shapes(gpu):
         assert 500 < bus < 8500, (shape, bus)
     with pytest.raises(gpu.AqzError):
         gpu.probe_hbm(7, 1 << 20, 1)
+
+
+def _paced(extra):
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--config", "c3",
+                        "--e2e", "pinned"] + extra, capture_output=True, text=True,
+                       timeout=150)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return lines[0]
+
+
+@pytest.mark.timeout(300)
+def test_paced_camera_accounting():
+    """bench.py's simulated camera (run_paced): u8 4096x4096 frames land in a
+    pinned ring at a fixed rate and are appended in batches of 8 as they
+    arrive.  At a rate the stage sustains nothing is dropped and every frame
+    is processed; with a ring too small for the rate, frames the camera
+    overwrote before the stage read them are counted as drops, and every
+    frame is either processed or dropped -- never both, never lost."""
+    ok = _paced(["--fps", "200", "--seconds", "1", "--batch", "8"])
+    assert ok["frames"] == 200 and ok["drops"] == 0
+    assert ok["processed"] == ok["appended"] == ok["stage_frames_written"] == 200
+    assert ok["value"] > 150  # sustained fps near the target
+    # 10000 fps (160 GB/s of frames) into a 16-frame ring: PCIe cannot keep up
+    over = _paced(["--fps", "10000", "--seconds", "0.3", "--batch", "8",
+                   "--camera-ring", "16"])
+    assert over["drops"] > 0
+    assert over["processed"] + over["drops"] == over["frames"] == 3000
+    assert over["appended"] == over["processed"] == over["stage_frames_written"]
