@@ -202,6 +202,10 @@ def lib():
         "aqz_stage_copy_layer": ([vp, u32, u64, vp, sz, vp, sz, i32], i32),
         "aqz_stage_copy_layer_async": ([vp, u32, u64, vp, sz, vp, sz], i32),
         "aqz_stage_frames_consumed": ([vp], u64),
+        "aqz_stage_wait_consumed": ([vp, u64], i32),
+        "aqz_stage_last_ticket": ([vp], u64),
+        "aqz_stage_copies_completed": ([vp], u64),
+        "aqz_stage_wait_ticket": ([vp, u64], i32),
         "aqz_stage_wait_copies": ([vp], i32),
         "aqz_host_alloc": ([sz, C.POINTER(vp)], i32),
         "aqz_host_free": ([vp], None),
@@ -639,6 +643,19 @@ class Stage:
         _check(lib().aqz_stage_copy_layer_async(self.h, level, layer, dst_ptr, cap,
                                                 has_data_ptr, has_data_cap),
                "copy_layer_async")
+
+    def wait_consumed(self, frames):
+        _check(lib().aqz_stage_wait_consumed(self.h, frames), "wait_consumed")
+        self._release_consumed()
+
+    def last_ticket(self):
+        return lib().aqz_stage_last_ticket(self.h)
+
+    def copies_completed(self):
+        return lib().aqz_stage_copies_completed(self.h)
+
+    def wait_ticket(self, ticket):
+        _check(lib().aqz_stage_wait_ticket(self.h, ticket), "wait_ticket")
 
     def wait_copies(self):
         _check(lib().aqz_stage_wait_copies(self.h), "wait_copies")
