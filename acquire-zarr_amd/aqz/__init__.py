@@ -226,6 +226,7 @@ def lib():
         "aqz_compressor_create": ([u64, u32, C.POINTER(CompressionC), C.POINTER(vp)], i32),
         "aqz_compressor_destroy": ([vp], None),
         "aqz_compressor_max_bytes": ([u64, u32], u64),
+        "aqz_compressor_scratch_bytes": ([C.POINTER(CompressionC), u64, u32, u32], u64),
         "aqz_compressor_run": ([vp, vp, u64, u32, vp, sz, vp, vp], i32),
         "aqz_compressor_blocksize": ([vp], u32),
         "aqz_stage_compressed_entries": ([vp, u32, u64, C.POINTER(ChunkEntryC), sz], i32),

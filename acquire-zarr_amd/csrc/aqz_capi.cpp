@@ -895,6 +895,21 @@ aqz_compressor_max_bytes(uint64_t chunk_bytes, uint32_t n_chunks)
     return Compressor::max_bytes(chunk_bytes, n_chunks);
 }
 
+uint64_t
+aqz_compressor_scratch_bytes(const aqz_compression* comp, uint64_t chunk_bytes,
+                             uint32_t typesize, uint32_t n_chunks)
+{
+    if (!comp)
+        return 0;
+    uint64_t n = 0;
+    const aqz_status s = guard([&] {
+        const Compression c = to_compression(comp);
+        Compressor check(chunk_bytes, typesize, c); // validates the settings
+        n = Compressor::scratch_bytes(c, chunk_bytes, typesize, n_chunks);
+    });
+    return s == AQZ_STATUS_SUCCESS ? n : 0;
+}
+
 uint32_t
 aqz_compressor_blocksize(const aqz_compressor* c)
 {

@@ -103,6 +103,12 @@ namespace aqz {
 // frames (one per chunk), for a whole resident chunk layer.  A segment is
 // what one zstd frame holds (a blosc block, or a chunk); it is cut into
 // zstd blocks of zstd::kBlock bytes, the parallel unit.
+// The Huffman table of a group of kHufGroup zstd blocks (64 KiB): the
+// literal statistics of a shuffled blosc block change at its byte planes,
+// so one table per segment fits neither plane (tools/zstd_lab.cpp: c-blosc's
+// ratio within 1% with group tables, 6% short with segment tables).  The
+// first Huffman block of a group carries the tree, the rest are Treeless.
+constexpr uint32_t kHufGroup = 8;
 struct ZstdSegTable
 {
     uint32_t mode;   // 0 raw literals, 1 one symbol, 2 Huffman
@@ -111,6 +117,20 @@ struct ZstdSegTable
     uint16_t code[256];
     uint8_t len[256];
     uint8_t tree[160];
+};
+
+// The sequence tables of a segment (one zstd frame): FSE_Compressed tables
+// built from the segment's literal-length / offset / match-length code
+// counts, described by the first block with sequences (mode 2) and repeated
+// by the others (mode 3); or the predefined distributions (mode 0) when
+// they cost less.
+struct ZstdSeqSeg
+{
+    uint32_t mode;      // 0 predefined, 2 custom
+    uint32_t desc_n;    // bytes of the three table descriptions (LL, OF, ML)
+    uint32_t pad[2];
+    uint8_t desc[256];
+    zstd::FseTable<zstd::kSeqMaxLog> ll, of, ml;
 };
 
 struct ZstdParams
@@ -126,6 +146,11 @@ struct ZstdParams
     uint32_t bps;           // zstd block slots per segment
     uint32_t store_only;    // blosc clevel 0: every frame memcpyed
     uint32_t match;         // 1: LZ sequences (zstd_parse); 0: literals only
+    uint32_t match_bits;    // a match must save this many literal bits
+    uint32_t phist;         // parse history: bytes before a unit its matches
+                            // may reach (0, kZHist1, kZHist2: the level)
+    uint32_t ngrp;          // Huffman groups per segment
+    uint32_t fit;           // 1: fitted sequence tables allowed (AQZ_ZSTD_FIT=0: predefined)
     const uint32_t* flags;  // has_data words (nullptr: every chunk has data)
     uint32_t tag;
     const zstd::SeqTables* seqt; // predefined sequence tables (device)
@@ -133,9 +158,9 @@ struct ZstdParams
     uint8_t* lits;          // literal bytes, kZSub per unit
     uint64_t* seqs;         // kZSubSeq packed sequences per unit
     uint32_t* snseq, *snlit, *stail;
+    uint32_t* sval;         // the unit's one byte value, 256 when it has several
     // per zstd block ([n_chunks * nseg * bps])
     uint32_t* hist;         // [.. * 256] literal histogram
-    uint32_t* shist;        // per segment [nseg * 256] (segments of > 32 blocks)
     uint8_t* bkind;         // 0 raw, 1 RLE, 2 compressed, 3 none, 4 sequences pending
     uint8_t* bltype;        // compressed: literals 0 raw, 2 Huffman
     uint32_t* bpay;         // compressed: literal payload bytes; RLE: the byte
@@ -143,9 +168,14 @@ struct ZstdParams
     uint32_t* bnlit;        // literals of the block
     uint32_t* bpos;         // block offset after the frame header
     uint8_t* scratch;       // [literal payload][sequences section], zstd::kBlock each
-    // per segment ([n_chunks * nseg])
+    uint32_t* bnseq;        // sequences of the block
+    // per Huffman group ([n_chunks * nseg * ngrp])
     ZstdSegTable* tab;
-    uint32_t* carrier;      // block carrying the tree (~0: none)
+    uint32_t* carrier;      // block of the group carrying its tree (~0: none)
+    // per segment ([n_chunks * nseg])
+    uint32_t* scount;       // [.. * 3 * 64] LL / OF / ML code counts
+    ZstdSeqSeg* sqt;        // sequence tables
+    uint32_t* scarrier;     // block carrying the sequence table descriptions
     uint32_t* ssize;        // record bytes (zstd frame, or the raw block)
     uint8_t* sraw;          // 1: record stored raw (blosc)
     uint32_t* spos;         // record offset inside the chunk frame (blosc)
@@ -162,7 +192,11 @@ struct ZstdParams
 // LZ4 encoder's streams), at most kZSubSeq sequences each
 constexpr uint32_t kZSub = 4096;
 constexpr uint32_t kZSubBlocks = zstd::kBlock / kZSub;
-constexpr uint32_t kZSubSeq = 256;
+constexpr uint32_t kZSubSeq = 1024; // a match is >= 4 bytes
+// parse history of the levels (zstd level >= 3: 12 KiB, >= 7: 28 KiB; blosc
+// clevel c is zstd level 2c - 1)
+constexpr uint32_t kZHist1 = 12 * 1024;
+constexpr uint32_t kZHist2 = 28 * 1024;
 
 hipError_t launch_zstd(const ZstdParams& p, hipStream_t stream);
 

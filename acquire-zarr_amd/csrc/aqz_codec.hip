@@ -744,11 +744,10 @@ constexpr uint32_t kZMinHuf = 64; // fewer literals: raw (as the host model)
 // room for 8 bits per literal (+ end mark and the word a code straddles)
 constexpr uint32_t kZStreamWords = (zstd::kBlock / 4 * 8) / 32 + 4;
 static_assert(4 * kZStreamWords <= 4096, "stream buffers fit the encode kernel's LDS");
-static_assert(kZSubBlocks * kZSubSeq * 8 + 4096 <= 4096 * 4, "staged sequences fit");
 
 struct ZBlock
 {
-    uint32_t c, j, b, seg, len, seglen, nb;
+    uint32_t c, j, b, seg, len, seglen, nb, grp;
 };
 
 __device__ __forceinline__ ZBlock
@@ -764,6 +763,7 @@ zblock(const ZstdParams& p, uint32_t g)
     z.nb = (z.seglen + zstd::kBlock - 1) / zstd::kBlock;
     const uint32_t o = z.b * zstd::kBlock;
     z.len = o < z.seglen ? min(zstd::kBlock, z.seglen - o) : 0;
+    z.grp = z.seg * p.ngrp + z.b / kHufGroup;
     return z;
 }
 
@@ -779,17 +779,23 @@ zchunk_skip(const ZstdParams& p, uint32_t c)
     return p.flags && p.flags[c] != p.tag;
 }
 
+// HIST: bytes of the segment before the unit that its matches may reach
+// (loaded into LDS ahead of the unit and hashed, insert only); HLOG: hash
+// table entries (LDS positions + 1, so 16 bits cover the 32 KiB window).
+template<uint32_t HIST, uint32_t HLOG>
 __global__ __launch_bounds__(64) void
 zstd_parse(const ZstdParams p)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t sw[kZSub / 4 + 4];
-    __shared__ uint16_t table[kHashSize];
+    __shared__ __attribute__((aligned(16))) uint32_t sw[(HIST + kZSub) / 4 + 4];
+    __shared__ uint16_t table[1u << HLOG];
     __shared__ uint32_t lh[256];
-    __shared__ uint64_t sseq[kZSubSeq];
     const uint32_t q = blockIdx.x, g = q / kZSubBlocks, k = q - g * kZSubBlocks;
     const uint32_t lane = threadIdx.x;
     const ZBlock z = zblock(p, g);
     const uint32_t so = k * kZSub;
+    // the unit's sequences go straight to its global slots (lane 0 stores;
+    // LDS is the occupancy limit, kZSubSeq of them would take 8 KiB)
+    uint64_t* sseq = p.seqs + uint64_t(q) * kZSubSeq;
     const uint32_t L = so < z.len ? min(kZSub, z.len - so) : 0;
     if (L == 0 || zchunk_skip(p, z.c)) {
         if (lane == 0) {
@@ -800,11 +806,24 @@ zstd_parse(const ZstdParams p)
         return;
     }
     const uint8_t* src = zblock_src(p, z) + so;
+    // units tile their segment in kZSub steps, so H is a multiple of kZSub
+    const uint32_t H = min(HIST, z.b * zstd::kBlock + so);
     uint8_t* sb = reinterpret_cast<uint8_t*>(sw);
     for (uint32_t b = lane; b < 256; b += 64)
         lh[b] = 0;
-    for (uint32_t i = lane; i < kHashSize / 2; i += 64)
+    for (uint32_t i = lane; i < (1u << HLOG) / 2; i += 64)
         reinterpret_cast<uint32_t*>(table)[i] = 0;
+    if (HIST > 0 && H > 0) {
+        const uint8_t* hs = src - H;
+        if ((reinterpret_cast<uintptr_t>(hs) & 15u) == 0) {
+            const uint4* h16 = reinterpret_cast<const uint4*>(hs);
+            for (uint32_t w = lane; w < H / 16; w += 64)
+                reinterpret_cast<uint4*>(sw)[w] = h16[w];
+        } else {
+            for (uint32_t i = lane; i < H; i += 64)
+                sb[i] = hs[i];
+        }
+    }
     const bool whole = L == kZSub && (reinterpret_cast<uintptr_t>(src) & 15u) == 0;
     if (whole) {
         // lane l holds bytes [64l, 64l + 64): staged to LDS and counted from
@@ -819,7 +838,7 @@ zstd_parse(const ZstdParams p)
         __syncthreads(); // lh zeroed
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            reinterpret_cast<uint4*>(sw)[4 * lane + j] = r[j];
+            reinterpret_cast<uint4*>(sw)[H / 16 + 4 * lane + j] = r[j];
         uint32_t cur = r[0].x & 255u, run = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -839,44 +858,65 @@ zstd_parse(const ZstdParams p)
         }
         atomicAdd(&lh[cur], run);
         if (lane < 2)
-            sw[kZSub / 4 + lane] = 0;
+            sw[(H + kZSub) / 4 + lane] = 0;
     } else {
+        uint8_t* ub = sb + H;
         if ((reinterpret_cast<uintptr_t>(src) & 3u) == 0) {
             const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
             for (uint32_t w = lane; w < L / 4; w += 64)
-                sw[w] = s4[w];
+                sw[H / 4 + w] = s4[w];
             for (uint32_t i = (L & ~3u) + lane; i < L; i += 64)
-                sb[i] = src[i];
+                ub[i] = src[i];
         } else {
             for (uint32_t i = lane; i < L; i += 64)
-                sb[i] = src[i];
+                ub[i] = src[i];
         }
         for (uint32_t i = L + lane; i < L + 8; i += 64)
-            sb[i] = 0;
+            ub[i] = 0;
         __syncthreads();
         for (uint32_t i = lane; i < L; i += 64)
-            atomicAdd(&lh[sb[i]], 1u);
+            atomicAdd(&lh[ub[i]], 1u);
     }
     __syncthreads();
+    if (HIST > 0 && H > 0) {
+        // the history's positions into the table (insert only; concurrent
+        // stores to one slot land in any order: every entry is a valid
+        // earlier position)
+        for (uint32_t i = lane; i < H; i += 64) {
+            const uint32_t v = lds_rd32(sw, i);
+            table[(v * 2654435761u) >> (32 - HLOG)] = uint16_t(i + 1);
+        }
+        __syncthreads();
+    }
     float e = 0.f;
+    uint32_t one = 256; // the unit's only byte value, if it has one
     for (uint32_t b = lane; b < 256; b += 64)
         if (lh[b]) {
             const float pr = float(lh[b]) / float(L);
             e -= pr * __log2f(pr);
+            if (lh[b] == L)
+                one = b;
         }
-    for (int d = 32; d > 0; d >>= 1)
+    for (int d = 32; d > 0; d >>= 1) {
         e += __shfl_xor(e, d);
-    const uint32_t minlen = zstd::min_match(e, kLenCap);
+        one = min(one, uint32_t(__shfl_xor(int(one), d)));
+    }
+    // a block is RLE only when its bytes are one value -- its literals being
+    // one value is not enough once matches copy from the history
+    if (lane == 0)
+        p.sval[q] = one;
+    const uint32_t minlen = zstd::min_match(e, kLenCap, float(p.match_bits));
     // lh keeps the unit's byte histogram: it is the literal histogram
     // when the parse finds no sequence
 
     // greedy parse: probe four 64-position windows, walk the matches
-    uint32_t nseq = 0, anchor = 0, p0 = 0, misses = 0;
+    // (positions are LDS offsets: the unit starts at H)
+    uint32_t nseq = 0, anchor = H, p0 = H, misses = 0;
     bool full = false;
     if (L >= 8) {
-        const uint32_t mflimit = L - 4; // last position a match may start
-        const uint32_t matchlimit = L;  // a match ends at or before here
-        for (uint32_t base = 0; base <= mflimit && !full;) {
+        const uint32_t mflimit = H + L - 4; // last position a match may start
+        const uint32_t matchlimit = H + L;  // a match ends at or before here
+        for (uint32_t base = H; base <= mflimit && !full;) {
             uint32_t cand[kWin], mlen[kWin];
             uint64_t M[kWin];
 #pragma unroll
@@ -886,11 +926,11 @@ zstd_parse(const ZstdParams p)
                 mlen[w] = 0;
                 if (qq <= mflimit) {
                     const uint32_t v = lds_rd32(sw, qq);
-                    const uint32_t h = (v * 2654435761u) >> (32 - kLz4HashLog);
+                    const uint32_t h = (v * 2654435761u) >> (32 - HLOG);
                     const uint32_t en = table[h];
                     table[h] = uint16_t(qq + 1);
                     uint32_t c = ~0u;
-                    if (en != 0 && lds_rd32(sw, en - 1) == v)
+                    if (en != 0 && en - 1 < qq && lds_rd32(sw, en - 1) == v)
                         c = en - 1;
                     else if (qq > 0 && lds_rd32(sw, qq - 1) == v)
                         c = qq - 1;
@@ -960,6 +1000,7 @@ zstd_parse(const ZstdParams p)
             base = max(base + 64 * kWin + skip, p0 & ~63u);
         }
     }
+    __threadfence_block(); // lane 0's sequence stores, read back below
     __syncthreads();
     // literal runs -> the unit's literal slot, and their histogram
     uint8_t* lo = p.lits + uint64_t(q) * kZSub;
@@ -967,10 +1008,10 @@ zstd_parse(const ZstdParams p)
         // every byte is a literal: the unit's histogram is the literal one
         if (whole) {
             for (uint32_t w = lane; w < kZSub / 16; w += 64)
-                reinterpret_cast<uint4*>(lo)[w] = reinterpret_cast<const uint4*>(sw)[w];
+                reinterpret_cast<uint4*>(lo)[w] = reinterpret_cast<const uint4*>(sw)[H / 16 + w];
         } else {
             for (uint32_t i = lane; i < L; i += 64)
-                lo[i] = sb[i];
+                lo[i] = sb[H + i];
         }
         __syncthreads();
         for (uint32_t b = lane; b < 256; b += 64)
@@ -986,27 +1027,31 @@ zstd_parse(const ZstdParams p)
     for (uint32_t b = lane; b < 256; b += 64)
         lh[b] = 0;
     __syncthreads();
-    uint32_t at = 0, pos = 0;
-    for (uint32_t s = 0; s < nseq; ++s) {
-        const zstd::Seq v = zstd::unpack_seq(sseq[s]);
-        for (uint32_t i = lane; i < v.lit; i += 64) {
-            const uint8_t x = sb[pos + i];
-            lo[at + i] = x;
-            atomicAdd(&lh[x], 1u);
+    uint32_t at = 0, pos = H;
+    for (uint32_t s0 = 0; s0 < nseq; s0 += 64) {
+        // 64 sequences per load, one per lane, walked through readlane
+        const uint64_t mine = s0 + lane < nseq ? sseq[s0 + lane] : 0;
+        const uint32_t mlo = uint32_t(mine), mhi = uint32_t(mine >> 32);
+        const uint32_t m = min(64u, nseq - s0);
+        for (uint32_t j = 0; j < m; ++j) {
+            const zstd::Seq v =
+              zstd::unpack_seq(uint64_t(rdlane(mlo, j)) | uint64_t(rdlane(mhi, j)) << 32);
+            for (uint32_t i = lane; i < v.lit; i += 64) {
+                const uint8_t x = sb[pos + i];
+                lo[at + i] = x;
+                atomicAdd(&lh[x], 1u);
+            }
+            at += v.lit;
+            pos += v.lit + v.len;
         }
-        at += v.lit;
-        pos += v.lit + v.len;
     }
-    const uint32_t tail = L - pos;
+    const uint32_t tail = H + L - pos;
     for (uint32_t i = lane; i < tail; i += 64) {
         const uint8_t x = sb[pos + i];
         lo[at + i] = x;
         atomicAdd(&lh[x], 1u);
     }
     at += tail;
-    uint64_t* so_ = p.seqs + uint64_t(q) * kZSubSeq;
-    for (uint32_t s = lane; s < nseq; s += 64)
-        so_[s] = sseq[s];
     __syncthreads();
     for (uint32_t b = lane; b < 256; b += 64)
         if (lh[b])
@@ -1049,26 +1094,6 @@ zstd_hist(const ZstdParams p)
     p.hist[uint64_t(g) * 256 + t] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
 }
 
-// Segments of many blocks (plain zstd: a whole chunk, 1024 blocks of a
-// C2 chunk): their literal histograms summed in parallel, kSegHistBlocks
-// blocks per workgroup, into shist (zeroed by the launcher).
-constexpr uint32_t kSegHistBlocks = 32;
-
-__global__ __launch_bounds__(256) void
-zstd_seghist(const ZstdParams p)
-{
-    const uint32_t s = blockIdx.x, t = threadIdx.x;
-    if (zchunk_skip(p, s / p.nseg))
-        return;
-    const uint32_t b0 = blockIdx.y * kSegHistBlocks;
-    const uint32_t b1 = min(p.bps, b0 + kSegHistBlocks);
-    uint32_t a = 0;
-    for (uint32_t b = b0; b < b1; ++b)
-        a += p.hist[(uint64_t(s) * p.bps + b) * 256 + t];
-    if (a)
-        atomicAdd(&p.shist[uint64_t(s) * 256 + t], a);
-}
-
 __global__ __launch_bounds__(64) void
 zstd_table(const ZstdParams p)
 {
@@ -1079,7 +1104,10 @@ zstd_table(const ZstdParams p)
     __shared__ uint16_t code[256];
     __shared__ uint8_t tree[160];
     __shared__ uint32_t npresent, tree_n, mode;
-    const uint32_t s = blockIdx.x, t = threadIdx.x;
+    // one Huffman group (kHufGroup blocks of a segment)
+    const uint32_t gi = blockIdx.x, t = threadIdx.x;
+    const uint32_t s = gi / p.ngrp, b0 = (gi - s * p.ngrp) * kHufGroup;
+    const uint32_t b1 = min(p.bps, b0 + kHufGroup);
     if (zchunk_skip(p, s / p.nseg))
         return;
     if (t == 0)
@@ -1087,11 +1115,8 @@ zstd_table(const ZstdParams p)
     __syncthreads();
     for (uint32_t k = t; k < 256; k += 64) {
         uint32_t a = 0;
-        if (p.bps > kSegHistBlocks)
-            a = p.shist[uint64_t(s) * 256 + k];
-        else
-            for (uint32_t b = 0; b < p.bps; ++b)
-                a += p.hist[(uint64_t(s) * p.bps + b) * 256 + k];
+        for (uint32_t b = b0; b < b1; ++b)
+            a += p.hist[(uint64_t(s) * p.bps + b) * 256 + k];
         w.cnt[k] = a;
         key[k] = uint64_t(a) << 8 | k;
         len[k] = 0;
@@ -1131,7 +1156,7 @@ zstd_table(const ZstdParams p)
         }
     }
     __syncthreads();
-    ZstdSegTable& T = p.tab[s];
+    ZstdSegTable& T = p.tab[gi];
     for (uint32_t k = t; k < 256; k += 64) {
         T.code[k] = code[k];
         T.len[k] = len[k];
@@ -1156,11 +1181,19 @@ zseq_codes(const zstd::Seq& v)
            uint64_t(v.len - zstd::ml_base(mlc)) << 33 | uint64_t(ofv - (1u << ofc)) << 49;
 }
 
-// zstd::encode_sequences over pre-coded sequences (same bitstream)
+// zstd::encode_sequences over pre-coded sequences (same bitstream), with
+// the predefined tables (LDS) or a segment's fitted ones (global)
+template<class TL, class TO, class TM>
 __device__ uint32_t
-zseq_encode(const zstd::SeqTables& t, const uint64_t* sv, uint32_t n, uint8_t* out,
-            uint32_t cap)
+zseq_encode(const TL& tll, const TO& tof, const TM& tml, const uint64_t* sv, uint32_t n,
+            uint8_t* out, uint32_t cap)
 {
+    struct
+    {
+        const TL& ll;
+        const TO& of;
+        const TM& ml;
+    } t{ tll, tof, tml };
     zstd::BitW w;
     w.init(out, cap);
     uint64_t v = sv[n - 1];
@@ -1249,8 +1282,20 @@ zstd_encode(const ZstdParams p)
     }
     __syncthreads();
     const uint32_t nl = pre[kZSubBlocks], nseq = spre[kZSubBlocks];
-    if (nl > 0 && p.hist[uint64_t(g) * 256 + t] == nl)
-        rle = int32_t(t); // one literal value: every byte of the block is it
+    if (!p.match) {
+        if (nl > 0 && p.hist[uint64_t(g) * 256 + t] == nl)
+            rle = int32_t(t); // one byte value in the whole block
+    } else if (t == 0) {
+        // every unit of the block holds one and the same value
+        uint32_t v = 512;
+        for (uint32_t k = 0; k < kZSubBlocks; ++k)
+            if (k * kZSub < z.len) {
+                const uint32_t u = p.sval[uint64_t(g) * kZSubBlocks + k];
+                v = (v == 512 || v == u) ? u : 256;
+            }
+        if (v < 256)
+            rle = int32_t(v);
+    }
     __syncthreads();
     if (rle >= 0) {
         if (t == 0) {
@@ -1259,7 +1304,7 @@ zstd_encode(const ZstdParams p)
         }
         return;
     }
-    const ZstdSegTable& T = p.tab[z.seg];
+    const ZstdSegTable& T = p.tab[z.grp];
     const ZLits lit{ p.match ? p.lits + uint64_t(g) * kZSubBlocks * kZSub : zblock_src(p, z),
                      p.match ? pre : nullptr };
     const bool try_huf = T.mode == 2 && nl >= kZMinHuf;
@@ -1381,6 +1426,7 @@ zstd_encode(const ZstdParams p)
     if (nseq == 0) {
         if (t == 0) {
             d[lpay] = 0; // sequence section header: no sequences
+            p.bnseq[g] = 0;
             p.bkind[g] = 2;
             p.bltype[g] = uint8_t(ltype);
             p.bpay[g] = lpay;
@@ -1389,12 +1435,21 @@ zstd_encode(const ZstdParams p)
         }
         return;
     }
-    static_assert(kZSubBlocks * kZSubSeq <= 512, "two sequences per thread");
+    // code counts of the block -> the segment's (zstd_seqtab fits its
+    // sequence tables to them); the LDS stream buffers are free by now
+    constexpr uint32_t kPer = kZSubBlocks * kZSubSeq / 256;
+    static_assert(kZSubBlocks * kZSubSeq % 256 == 0, "whole sequences per thread");
+    uint32_t* cnt = zbuf; // [3][64]: LL, OF, ML codes
+    __syncthreads();
+    for (uint32_t i = t; i < 3 * 64; i += 256)
+        cnt[i] = 0;
+    __syncthreads();
     uint64_t* gs = p.seqs + uint64_t(g) * kZSubBlocks * kZSubSeq;
-    uint64_t cw[2] = { 0, 0 };
+    uint64_t cw[kPer];
 #pragma unroll
-    for (uint32_t j = 0; j < 2; ++j) {
+    for (uint32_t j = 0; j < kPer; ++j) {
         const uint32_t i = t + 256 * j;
+        cw[j] = 0;
         if (i < nseq) {
             uint32_t k = 0;
             while (k + 1 < kZSubBlocks && spre[k + 1] <= i)
@@ -1403,19 +1458,152 @@ zstd_encode(const ZstdParams p)
             if (i == spre[k])
                 v.lit += carry[k];
             cw[j] = zseq_codes(v);
+            atomicAdd(&cnt[cw[j] & 63u], 1u);                     // LL
+            atomicAdd(&cnt[64 + ((cw[j] >> 12) & 31u)], 1u);      // OF
+            atomicAdd(&cnt[128 + ((cw[j] >> 6) & 63u)], 1u);      // ML
         }
     }
     __syncthreads(); // every slot read before any is overwritten
 #pragma unroll
-    for (uint32_t j = 0; j < 2; ++j)
+    for (uint32_t j = 0; j < kPer; ++j)
         if (t + 256 * j < nseq)
             gs[t + 256 * j] = cw[j];
+    for (uint32_t i = t; i < 3 * 64; i += 256)
+        if (cnt[i])
+            atomicAdd(&p.scount[uint64_t(z.seg) * 192 + i], cnt[i]);
     if (t == 0) {
         p.bkind[g] = 4; // sequences pending (zstd_seqenc)
         p.bltype[g] = uint8_t(ltype);
         p.bpay[g] = lpay;
         p.bseqb[g] = nseq;
+        p.bnseq[g] = nseq;
         p.bnlit[g] = nl;
+    }
+}
+
+// Sequence tables of a segment, one wave: LL / OF / ML FSE distributions
+// fitted to the segment's code counts (accuracy log 5..9, the one with the
+// fewest bits counted with its description), kept when the three together
+// beat the predefined distributions.  The serial part runs on lane 0.
+__device__ bool
+zfit(const uint32_t* cnt, uint32_t maxlog, int16_t* norm, uint32_t& al_out,
+     uint32_t& maxsym_out, float& bits_out)
+{
+    uint32_t ms = 0, nz = 0;
+    uint64_t total = 0;
+    for (uint32_t s = 0; s < 64; ++s)
+        if (cnt[s]) {
+            ms = s;
+            ++nz;
+            total += cnt[s];
+        }
+    if (nz < 2 || ms >= zstd::kFseMaxSym)
+        return false;
+    float best = 3.0e38f;
+    int16_t nm[zstd::kFseMaxSym];
+    uint8_t tmp[128];
+    for (uint32_t al = 5; al <= maxlog; ++al) {
+        const int ts = 1 << al;
+        int used = 0, big = -1;
+        for (uint32_t s = 0; s <= ms; ++s) {
+            if (!cnt[s]) {
+                nm[s] = 0;
+                continue;
+            }
+            const float pr = float(cnt[s]) * float(ts) / float(total);
+            if (pr < 1.0f) {
+                nm[s] = -1;
+                used += 1;
+            } else {
+                const int v = int(pr + 0.5f);
+                nm[s] = int16_t(v);
+                used += v;
+            }
+            if (big < 0 || cnt[s] > cnt[big])
+                big = int(s);
+        }
+        const int fix = nm[big] + (ts - used);
+        if (nm[big] < 0 || fix < 1)
+            continue;
+        nm[big] = int16_t(fix);
+        const uint32_t d = zstd::fse_write_ncount(tmp, sizeof(tmp), nm, ms, al);
+        if (!d)
+            continue;
+        float b = 8.0f * float(d);
+        for (uint32_t s = 0; s <= ms; ++s)
+            if (cnt[s])
+                b += float(cnt[s]) * (float(al) - (nm[s] < 0 ? 0.0f : __log2f(float(nm[s]))));
+        if (b < best) {
+            best = b;
+            al_out = al;
+            for (uint32_t s = 0; s <= ms; ++s)
+                norm[s] = nm[s];
+        }
+    }
+    maxsym_out = ms;
+    bits_out = best;
+    return best < 3.0e38f;
+}
+
+__device__ float
+zpredef_bits(const uint32_t* cnt, const int16_t* norm, uint32_t maxsym, uint32_t al)
+{
+    float b = 0.0f;
+    for (uint32_t s = 0; s < 64; ++s)
+        if (cnt[s]) {
+            if (s > maxsym)
+                return 3.0e38f;
+            b += float(cnt[s]) * (float(al) - (norm[s] < 0 ? 0.0f : __log2f(float(norm[s]))));
+        }
+    return b;
+}
+
+__global__ __launch_bounds__(64) void
+zstd_seqtab(const ZstdParams p)
+{
+    __shared__ uint32_t cnt[3][64];
+    __shared__ int16_t norm[3][zstd::kFseMaxSym];
+    __shared__ zstd::FseBuildWorkT<zstd::kSeqMaxLog> bw;
+    const uint32_t s = blockIdx.x, t = threadIdx.x;
+    ZstdSeqSeg& Q = p.sqt[s];
+    if (zchunk_skip(p, s / p.nseg)) {
+        if (t == 0)
+            Q.mode = 0;
+        return;
+    }
+    for (uint32_t f = 0; f < 3; ++f)
+        cnt[f][t] = p.scount[uint64_t(s) * 192 + f * 64 + t];
+    __syncthreads();
+    if (t != 0)
+        return;
+    uint32_t al[3] = { 0, 0, 0 }, ms[3] = { 0, 0, 0 };
+    float fb[3];
+    const uint32_t maxlog[3] = { 9, 8, 9 };
+    bool ok = true;
+    for (uint32_t f = 0; f < 3 && ok; ++f)
+        ok = zfit(cnt[f], maxlog[f], norm[f], al[f], ms[f], fb[f]);
+    Q.mode = 0;
+    Q.desc_n = 0;
+    if (!ok || !p.fit)
+        return;
+    const float pre = zpredef_bits(cnt[0], zstd::ll_default_norm(), 35, 6) +
+                      zpredef_bits(cnt[1], zstd::of_default_norm(), 28, 5) +
+                      zpredef_bits(cnt[2], zstd::ml_default_norm(), 52, 6);
+    if (fb[0] + fb[1] + fb[2] >= pre)
+        return;
+    uint32_t n = 0;
+    for (uint32_t f = 0; f < 3 && ok; ++f) {
+        const uint32_t d = zstd::fse_write_ncount(Q.desc + n, sizeof(Q.desc) - n, norm[f],
+                                                  ms[f], al[f]);
+        ok = d != 0;
+        n += d;
+    }
+    ok = ok && zstd::fse_build(Q.ll, norm[0], ms[0], al[0], bw) &&
+         zstd::fse_build(Q.of, norm[1], ms[1], al[1], bw) &&
+         zstd::fse_build(Q.ml, norm[2], ms[2], al[2], bw);
+    if (ok) {
+        Q.desc_n = n;
+        Q.mode = 2;
     }
 }
 
@@ -1440,18 +1628,25 @@ zstd_seqenc(const ZstdParams p)
     const uint32_t nseq = p.bseqb[g], lpay = p.bpay[g], nl = p.bnlit[g];
     uint32_t lsec;
     if (p.bltype[g] == 2) {
-        const uint32_t wt = p.tab[z.seg].tree_n + lpay;
+        const uint32_t wt = p.tab[z.grp].tree_n + lpay;
         lsec = zstd::lit_header_huf_bytes(nl, wt) + wt;
     } else {
         lsec = zstd::lit_header_raw_bytes(nl) + nl;
     }
+    // [count][modes, patched by zstd_write][bitstream]; the table
+    // descriptions of a fitted segment are counted as if this block carried
+    // them (as the tree), so the decision does not depend on which block does
+    const ZstdSeqSeg& Q = p.sqt[z.seg];
+    const bool fitted = Q.mode == 2;
     uint8_t* so = p.scratch + g * zstd::kBlock + lpay;
     const uint32_t cap = zstd::kBlock - lpay;
     uint32_t sq = zstd::write_seq_header(so, nseq);
-    const uint32_t bits = zseq_encode(seqt, p.seqs + g * kZSubBlocks * kZSubSeq, nseq,
-                                      so + sq, cap > sq ? cap - sq : 0);
+    const uint64_t* sv = p.seqs + g * kZSubBlocks * kZSubSeq;
+    const uint32_t bcap = cap > sq ? cap - sq : 0;
+    const uint32_t bits = fitted ? zseq_encode(Q.ll, Q.of, Q.ml, sv, nseq, so + sq, bcap)
+                                 : zseq_encode(seqt.ll, seqt.of, seqt.ml, sv, nseq, so + sq, bcap);
     sq = bits ? sq + bits : 0;
-    if (sq != 0 && lsec + sq < z.len) {
+    if (sq != 0 && lsec + sq + (fitted ? Q.desc_n : 0) < z.len) {
         p.bkind[g] = 2;
         p.bseqb[g] = sq;
     } else {
@@ -1460,12 +1655,15 @@ zstd_seqenc(const ZstdParams p)
 }
 
 
-// One wave per segment: the block carrying the tree (the first Huffman
-// block), each block's bytes, their offsets (a wave scan, 64 blocks per
-// step) and the frame size.
+// One wave per segment: the block carrying each Huffman group's tree (the
+// group's first Huffman block) and the sequence tables' descriptions (the
+// segment's first block with sequences, when its tables are fitted), each
+// block's bytes, their offsets (a wave scan, 64 blocks per step) and the
+// frame size.
 __global__ __launch_bounds__(64) void
 zstd_segment(const ZstdParams p)
 {
+    static_assert(64 % kHufGroup == 0, "a wave step holds whole groups");
     const uint32_t s = blockIdx.x, lane = threadIdx.x;
     if (zchunk_skip(p, s / p.nseg)) {
         if (lane == 0)
@@ -1473,16 +1671,24 @@ zstd_segment(const ZstdParams p)
         return;
     }
     const ZBlock z0 = zblock(p, s * p.bps);
-    const uint32_t tree_n = p.tab[s].tree_n;
-    uint32_t carrier = ~0u;
-    for (uint32_t b0 = 0; b0 < z0.nb && carrier == ~0u; b0 += 64) {
+    const ZstdSeqSeg& Q = p.sqt[s];
+    const uint32_t desc_n = Q.mode == 2 ? Q.desc_n : 0;
+    uint32_t scar = ~0u;
+    for (uint32_t b0 = 0; b0 < z0.nb; b0 += 64) {
         const uint32_t b = b0 + lane;
-        const bool huf = b < z0.nb && p.bkind[s * p.bps + b] == 2 &&
-                         p.bltype[s * p.bps + b] == 2;
-        const uint64_t m = __ballot(huf);
-        if (m)
-            carrier = b0 + uint32_t(__ffsll(static_cast<long long>(m))) - 1;
+        const uint32_t g = s * p.bps + b;
+        const bool cmp = b < z0.nb && p.bkind[g] == 2;
+        const uint64_t huf = __ballot(cmp && p.bltype[g] == 2);
+        const uint64_t sqb = __ballot(cmp && p.bnseq[g] > 0);
+        if (lane < 64 / kHufGroup && b0 + lane * kHufGroup < z0.nb) {
+            const uint32_t m = uint32_t(huf >> (lane * kHufGroup)) & ((1u << kHufGroup) - 1u);
+            p.carrier[s * p.ngrp + (b0 / kHufGroup) + lane] =
+              m ? b0 + lane * kHufGroup + uint32_t(__builtin_ctz(m)) : ~0u;
+        }
+        if (scar == ~0u && sqb)
+            scar = b0 + uint32_t(__ffsll(static_cast<long long>(sqb))) - 1;
     }
+    __syncthreads(); // the carriers above, read below
     uint32_t pos = 0;
     for (uint32_t b0 = 0; b0 < z0.nb; b0 += 64) {
         const uint32_t b = b0 + lane;
@@ -1497,11 +1703,13 @@ zstd_segment(const ZstdParams p)
                 sz = 4;
             } else if (k == 2) {
                 const uint32_t nl = p.bnlit[g];
+                const uint32_t gi = s * p.ngrp + b / kHufGroup;
+                const uint32_t sd = scar == b ? desc_n : 0;
                 if (p.bltype[g] == 2) {
-                    const uint32_t cs = p.bpay[g] + (carrier == b ? tree_n : 0);
-                    sz = 3 + zstd::lit_header_huf_bytes(nl, cs) + cs + p.bseqb[g];
+                    const uint32_t cs = p.bpay[g] + (p.carrier[gi] == b ? p.tab[gi].tree_n : 0);
+                    sz = 3 + zstd::lit_header_huf_bytes(nl, cs) + cs + p.bseqb[g] + sd;
                 } else {
-                    sz = 3 + zstd::lit_header_raw_bytes(nl) + nl + p.bseqb[g];
+                    sz = 3 + zstd::lit_header_raw_bytes(nl) + nl + p.bseqb[g] + sd;
                 }
             }
         }
@@ -1516,7 +1724,7 @@ zstd_segment(const ZstdParams p)
         pos += __shfl(x, 63);
     }
     if (lane == 0) {
-        p.carrier[s] = carrier;
+        p.scarrier[s] = scar;
         const uint32_t frame = zstd::frame_header_bytes(z0.seglen) + pos;
         const bool raw = p.blosc && frame >= z0.seglen;
         p.sraw[s] = raw ? 1 : 0;
@@ -1611,29 +1819,52 @@ zstd_write(const ZstdParams p)
     } else if (k == 2) {
         const uint32_t nl = p.bnlit[g], pay = p.bpay[g], sq = p.bseqb[g];
         const uint8_t* scr = p.scratch + uint64_t(g) * zstd::kBlock;
+        // the sequences section: [count][modes][descriptions, carrier only][bits]
+        const uint32_t ns = p.bnseq[g];
+        const ZstdSeqSeg& Q = p.sqt[z.seg];
+        const bool fitted = ns > 0 && Q.mode == 2;
+        const bool scar = fitted && p.scarrier[z.seg] == z.b;
+        const uint32_t sd = scar ? Q.desc_n : 0;
+        uint8_t* q = d + 3;
+        uint32_t lit_bytes = pay; // literal payload in scratch
         if (p.bltype[g] == 2) {
-            const ZstdSegTable& T = p.tab[z.seg];
-            const bool carry = p.carrier[z.seg] == z.b;
+            const ZstdSegTable& T = p.tab[z.grp];
+            const bool carry = p.carrier[z.grp] == z.b;
             const uint32_t cs = pay + (carry ? T.tree_n : 0);
             const uint32_t lh = zstd::lit_header_huf_bytes(nl, cs);
             if (t == 0) {
-                zstd::write_block_header(d, last, 2, lh + cs + sq);
+                zstd::write_block_header(d, last, 2, lh + cs + sq + sd);
                 zstd::write_lit_header_huf(d + 3, carry ? 2 : 3, nl, cs);
             }
-            uint8_t* q = d + 3 + lh;
+            q += lh;
             if (carry) {
                 for (uint32_t i = t; i < T.tree_n; i += 256)
                     q[i] = T.tree[i];
                 q += T.tree_n;
             }
-            copy_bytes(q, scr, pay + sq);
         } else {
             const uint32_t lh = zstd::lit_header_raw_bytes(nl);
             if (t == 0) {
-                zstd::write_block_header(d, last, 2, lh + nl + sq);
+                zstd::write_block_header(d, last, 2, lh + nl + sq + sd);
                 zstd::write_lit_header_raw(d + 3, 0, nl);
             }
-            copy_bytes(d + 3 + lh, scr, nl + sq);
+            q += lh;
+            lit_bytes = nl;
+        }
+        if (!fitted) {
+            copy_bytes(q, scr, lit_bytes + sq);
+        } else {
+            // count bytes, then the modes byte: LL / OF / ML all
+            // FSE_Compressed (2) in the carrier, Repeat (3) elsewhere
+            const uint32_t kc = ns < 128 ? 1u : ns < 0x7F00 ? 2u : 3u;
+            copy_bytes(q, scr, lit_bytes + kc);
+            if (t == 0)
+                q[lit_bytes + kc] = scar ? uint8_t(2u << 6 | 2u << 4 | 2u << 2)
+                                         : uint8_t(3u << 6 | 3u << 4 | 3u << 2);
+            uint8_t* qd = q + lit_bytes + kc + 1;
+            for (uint32_t i = t; i < sd; i += 256)
+                qd[i] = Q.desc[i];
+            copy_bytes(qd + sd, scr + lit_bytes + kc + 1, sq - kc - 1);
         }
     }
 }
@@ -1682,26 +1913,29 @@ launch_zstd(const ZstdParams& p, hipStream_t stream)
     if (nblk * kZSubBlocks > 0x7fffffffull || p.nseg == 0 || p.bps == 0 ||
         uint64_t(p.bps) * zstd::kBlock < p.seg_bytes)
         return hipErrorInvalidValue;
+    if (p.ngrp != (p.bps + kHufGroup - 1) / kHufGroup)
+        return hipErrorInvalidValue;
     if (!p.store_only) {
+        hipError_t e = hipMemsetAsync(p.scount, 0, nseg * 192 * 4, stream);
+        if (e != hipSuccess)
+            return e;
         if (p.match) {
-            hipError_t e = hipMemsetAsync(p.hist, 0, nblk * 256 * 4, stream);
+            e = hipMemsetAsync(p.hist, 0, nblk * 256 * 4, stream);
             if (e != hipSuccess)
                 return e;
-            hipLaunchKernelGGL(zstd_parse, dim3(uint32_t(nblk * kZSubBlocks)), dim3(64), 0,
-                               stream, p);
+            const dim3 gd(uint32_t(nblk * kZSubBlocks));
+            if (p.phist == 0)
+                hipLaunchKernelGGL((zstd_parse<0, kLz4HashLog>), gd, dim3(64), 0, stream, p);
+            else if (p.phist <= kZHist1)
+                hipLaunchKernelGGL((zstd_parse<kZHist1, 13>), gd, dim3(64), 0, stream, p);
+            else
+                hipLaunchKernelGGL((zstd_parse<kZHist2, 14>), gd, dim3(64), 0, stream, p);
         } else {
             hipLaunchKernelGGL(zstd_hist, dim3(uint32_t(nblk)), dim3(256), 0, stream, p);
         }
-        if (p.bps > kSegHistBlocks) {
-            hipError_t e = hipMemsetAsync(p.shist, 0, nseg * 256 * 4, stream);
-            if (e != hipSuccess)
-                return e;
-            hipLaunchKernelGGL(zstd_seghist,
-                               dim3(uint32_t(nseg), (p.bps + kSegHistBlocks - 1) / kSegHistBlocks),
-                               dim3(256), 0, stream, p);
-        }
-        hipLaunchKernelGGL(zstd_table, dim3(uint32_t(nseg)), dim3(64), 0, stream, p);
+        hipLaunchKernelGGL(zstd_table, dim3(uint32_t(nseg * p.ngrp)), dim3(64), 0, stream, p);
         hipLaunchKernelGGL(zstd_encode, dim3(uint32_t(nblk)), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL(zstd_seqtab, dim3(uint32_t(nseg)), dim3(64), 0, stream, p);
         if (p.match)
             hipLaunchKernelGGL(zstd_seqenc, dim3(uint32_t((nblk + 63) / 64)), dim3(64), 0,
                                stream, p);

@@ -1755,6 +1755,39 @@ Compressor::Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compressio
     store_only_ = c.codec != 3 && c.clevel == 0;
 }
 
+uint64_t
+Compressor::scratch_bytes(const Compression& c, uint64_t chunk_bytes, uint32_t typesize,
+                          uint32_t n_chunks)
+{
+    const uint64_t n = n_chunks;
+    const bool store_only = c.codec != 3 && c.clevel == 0;
+    uint64_t b = n * 4 + n + n * 8; // fsize, mode, cstart
+    if (c.codec == 1) {
+        const BloscGeom g = make_blosc_geom(uint32_t(chunk_bytes), typesize, uint32_t(c.shuffle));
+        const uint64_t ns = n * g.spc;
+        return b + (store_only ? 1 : ns * g.slot) + ns * 8;
+    }
+    uint64_t seg = chunk_bytes, nseg1 = 1;
+    if (c.codec == 2) {
+        const ZstdBloscGeom g = make_zstd_blosc_geom(uint32_t(chunk_bytes), typesize);
+        seg = g.blocksize;
+        nseg1 = g.nblocks;
+    }
+    const uint64_t nseg = n * nseg1, bps = (seg + zstd::kBlock - 1) / zstd::kBlock;
+    const uint64_t nblk = nseg * bps, ngrp = nseg * ((bps + kHufGroup - 1) / kHufGroup);
+    b += nseg * 4; // spos
+    if (c.codec == 2 && !store_only && (c.shuffle == 2 || (c.shuffle == 1 && typesize > 1)))
+        b += n * chunk_bytes; // shuffled input
+    if (store_only)
+        return b;
+    const uint64_t nu = nblk * kZSubBlocks;
+    b += nu * kZSub + nu * kZSubSeq * 8 + 4 * nu * 4;              // parse units
+    b += nblk * (1 + 4 + 4 + 4 + 256 * 4 + 1 + 4 + 4 + zstd::kBlock); // per block
+    b += nseg * (192 * 4 + sizeof(ZstdSeqSeg) + 4 + 1 + 4);         // per segment
+    b += ngrp * (sizeof(ZstdSegTable) + 4) + sizeof(zstd::SeqTables);
+    return b;
+}
+
 void
 Compressor::run(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
                 const uint32_t* flags, uint32_t tag, uint8_t* out, uint64_t* offsets,
@@ -1819,6 +1852,24 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
         p.nseg = 1;
     }
     p.bps = (p.seg_bytes + zstd::kBlock - 1) / zstd::kBlock;
+    p.ngrp = (p.bps + kHufGroup - 1) / kHufGroup;
+    // the level: the parse history of plain zstd (level >= 3: 12 KiB, >= 7:
+    // 28 KiB; level 0 is libzstd's default, 3).  Shuffled blosc planes gain
+    // nothing from a history (tools/zstd_lab.cpp: camera 1.891 -> 1.890, dim
+    // 4.09 -> 3.88: the extra short matches cost more than their literals),
+    // so blosc-zstd clevels >= 1 share the unit-local parse.
+    {
+        const int zl = c_.clevel == 0 ? 3 : c_.clevel;
+        p.phist = blosc ? 0 : zl >= 7 ? kZHist2 : zl >= 3 ? kZHist1 : 0;
+        if (const char* e = std::getenv("AQZ_ZSTD_HIST")) // tuning knob
+            p.phist = uint32_t(std::atoi(e));
+    }
+    // a match must save the bits of a sequence: ~12 with the fitted tables
+    // of unshuffled data, 16 on shuffled planes (tools/zstd_lab.cpp sweep)
+    p.match_bits = uint32_t(blosc ? zstd::kMatchBits : zstd::kMatchBitsFitted);
+    p.fit = 1;
+    if (const char* e = std::getenv("AQZ_ZSTD_FIT")) // tuning knob
+        p.fit = uint32_t(std::atoi(e));
     p.src = chunks;
     p.src_pitch = pitch;
     const bool shuffle = blosc && !store_only_ &&
@@ -1851,18 +1902,23 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
             snseq_.alloc(nu * 4);
             snlit_.alloc(nu * 4);
             stail_.alloc(nu * 4);
+            sval_.alloc(nu * 4);
         }
+        const uint64_t ngrp = nseg * p.ngrp;
         bltype_.alloc(nblk);
         bseqb_.alloc(nblk * 4);
         bnlit_.alloc(nblk * 4);
+        bnseq_.alloc(nblk * 4);
         hist_.alloc(nblk * 256 * 4);
-        shist_.alloc(nseg * 256 * 4);
+        scount_.alloc(nseg * 192 * 4);
+        sqt_.alloc(nseg * sizeof(ZstdSeqSeg));
+        scarrier_.alloc(nseg * 4);
         bkind_.alloc(nblk);
         bpay_.alloc(nblk * 4);
         bpos_.alloc(nblk * 4);
         scratch_.alloc(nblk * zstd::kBlock);
-        tab_.alloc(nseg * sizeof(ZstdSegTable));
-        carrier_.alloc(nseg * 4);
+        tab_.alloc(ngrp * sizeof(ZstdSegTable));
+        carrier_.alloc(ngrp * 4);
         sraw_.alloc(nseg);
         ssize_.alloc(nseg * 4);
     }
@@ -1876,11 +1932,15 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
     p.snseq = reinterpret_cast<uint32_t*>(snseq_.p);
     p.snlit = reinterpret_cast<uint32_t*>(snlit_.p);
     p.stail = reinterpret_cast<uint32_t*>(stail_.p);
+    p.sval = reinterpret_cast<uint32_t*>(sval_.p);
     p.bltype = bltype_.p;
     p.bseqb = reinterpret_cast<uint32_t*>(bseqb_.p);
     p.bnlit = reinterpret_cast<uint32_t*>(bnlit_.p);
     p.hist = reinterpret_cast<uint32_t*>(hist_.p);
-    p.shist = reinterpret_cast<uint32_t*>(shist_.p);
+    p.bnseq = reinterpret_cast<uint32_t*>(bnseq_.p);
+    p.scount = reinterpret_cast<uint32_t*>(scount_.p);
+    p.sqt = reinterpret_cast<ZstdSeqSeg*>(sqt_.p);
+    p.scarrier = reinterpret_cast<uint32_t*>(scarrier_.p);
     p.bkind = bkind_.p;
     p.bpay = reinterpret_cast<uint32_t*>(bpay_.p);
     p.bpos = reinterpret_cast<uint32_t*>(bpos_.p);

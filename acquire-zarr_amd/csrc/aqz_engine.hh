@@ -119,12 +119,17 @@ class Compressor
             return make_zstd_blosc_geom(uint32_t(nbytes_), typesize_).blocksize;
         return 0;
     }
+    // device bytes of the scratch buffers run() allocates for n_chunks
+    // chunks of chunk_bytes (an upper bound: aqz_compressor_scratch_bytes)
+    static uint64_t scratch_bytes(const Compression& c, uint64_t chunk_bytes,
+                                  uint32_t typesize, uint32_t n_chunks);
     // device bytes of the scratch buffers allocated so far
     uint64_t device_bytes() const
     {
         uint64_t n = scratch_.n + ssize_.n + spos_.n + fsize_.n + mode_.n + cstart_.n;
-        for (const DevBuf* b : { &zin_, &hist_, &shist_, &bkind_, &bpay_, &bpos_, &tab_, &carrier_,
+        for (const DevBuf* b : { &zin_, &hist_, &scount_, &bkind_, &bpay_, &bpos_, &tab_, &carrier_,
                                  &sraw_, &lits_, &seqs_, &snseq_, &snlit_, &stail_, &bltype_,
+                                 &bnseq_, &sqt_, &scarrier_, &sval_,
                                  &bseqb_, &bnlit_, &seqt_ })
             n += b->n;
         return n;
@@ -140,7 +145,8 @@ class Compressor
     BloscGeom g_{};
     bool store_only_;
     DevBuf scratch_, ssize_, spos_, fsize_, mode_, cstart_;
-    DevBuf zin_, hist_, shist_, bkind_, bpay_, bpos_, tab_, carrier_, sraw_; // zstd
+    DevBuf zin_, hist_, scount_, bkind_, bpay_, bpos_, tab_, carrier_, sraw_; // zstd
+    DevBuf bnseq_, sqt_, scarrier_, sval_;
     DevBuf lits_, seqs_, snseq_, snlit_, stail_, bltype_, bseqb_, bnlit_, seqt_;
 };
 

@@ -804,14 +804,17 @@ unpack_seq(uint64_t v)
 }
 
 // Minimum match length for a block whose bytes have entropy H bits: a match
-// pays when its literal cost beats a sequence's ~16 bits (CPU model sweep,
-// tests/zstd/zstd_host.cpp MATCH_BITS).
+// pays when its literal cost beats a sequence's cost.  With the predefined
+// sequence tables a sequence is ~16 bits (CPU model sweep,
+// tests/zstd/zstd_host.cpp MATCH_BITS); with tables fitted to the segment
+// ~12 (tools/zstd_lab.cpp sweep: dim sCMOS plain zstd 2.86 -> 3.11).
 constexpr float kMatchBits = 16.0f;
+constexpr float kMatchBitsFitted = 12.0f;
 __host__ __device__ inline uint32_t
-min_match(float H, uint32_t cap)
+min_match(float H, uint32_t cap, float bits = kMatchBits)
 {
     const float h = H > 0.25f ? H : 0.25f;
-    uint32_t m = uint32_t(kMatchBits / h + 0.999f);
+    uint32_t m = uint32_t(bits / h + 0.999f);
     return m < 4 ? 4 : (m > cap ? cap : m);
 }
 

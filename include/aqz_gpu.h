@@ -362,8 +362,8 @@ typedef struct
 /* Bytes currently allocated by the stage. */
 aqz_status aqz_stage_memory_usage(const aqz_stage* st, aqz_memory_usage* out);
 /* Upper bound of what a stage created with (desc, opt) allocates, compressed
- * hand-off excluded (add aqz_compressor_max_bytes per compressed slot).  No
- * GPU needed. */
+ * hand-off excluded (add aqz_compressor_max_bytes per compressed slot and
+ * aqz_compressor_scratch_bytes per compressed level).  No GPU needed. */
 aqz_status aqz_stage_estimate_memory(const aqz_array_desc* desc,
                                      const aqz_stage_options* opt,
                                      aqz_memory_usage* out);
@@ -475,6 +475,12 @@ aqz_status aqz_compressor_create(uint64_t chunk_bytes, uint32_t typesize,
                                  const aqz_compression* comp, aqz_compressor** out);
 void aqz_compressor_destroy(aqz_compressor* c);
 uint64_t aqz_compressor_max_bytes(uint64_t chunk_bytes, uint32_t n_chunks);
+/* Device scratch one compressor (or one level of a stage compressing its
+ * layers) allocates to compress n_chunks chunks of chunk_bytes with `comp`
+ * (an upper bound; the zstd codecs keep parse units, sequences and per-block
+ * state at about 4x the layer).  0 on invalid settings.  No GPU needed. */
+uint64_t aqz_compressor_scratch_bytes(const aqz_compression* comp, uint64_t chunk_bytes,
+                                      uint32_t typesize, uint32_t n_chunks);
 aqz_status aqz_compressor_run(aqz_compressor* c, const void* chunks, uint64_t pitch,
                               uint32_t n_chunks, void* dst, size_t dst_cap,
                               uint64_t* offsets, void* stream);

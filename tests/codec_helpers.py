@@ -104,10 +104,11 @@ def shuffle(kind: str, ts: int, data: bytes) -> bytes:
     return out.raw[:len(data)]
 
 
-def camera_like(rng, n_px: int, dtype, level=1000.0, noise=30.0) -> np.ndarray:
-    """Smooth background + shot-noise-like jitter, the shape of sCMOS frames."""
+def camera_like(rng, n_px: int, dtype, level=1000.0, noise=30.0, amp=200.0) -> np.ndarray:
+    """Smooth background + shot-noise-like jitter, the shape of sCMOS frames
+    (level 100, noise 3, amp 0: a dim low-light sCMOS frame)."""
     x = np.arange(n_px, dtype=np.float64)
-    base = level + 200.0 * np.sin(x / 977.0)
+    base = level + amp * np.sin(x / 977.0)
     v = base + rng.normal(0.0, noise, n_px)
     info = np.iinfo(dtype) if np.issubdtype(dtype, np.integer) else None
     if info is not None:

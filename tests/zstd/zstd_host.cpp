@@ -78,6 +78,7 @@ huf_streams(const Table& t, const uint8_t* lit, uint32_t n, uint8_t* out, uint32
 }
 
 constexpr uint32_t kMinHuf = 64; // fewer literals: stored raw
+constexpr uint32_t kGroup = 8;   // blocks per Huffman table (the device's kHufGroup)
 
 // how often each format path was taken (the run must take every one)
 struct Paths
@@ -149,10 +150,12 @@ encode_frame(const uint8_t* src, uint64_t n, bool lz, const SeqTables& st)
     std::vector<uint8_t> out(frame_header_bytes(n) + n + 3 * (n / kBlock + 1) + 64);
     uint32_t at = write_frame_header(out.data(), n);
     const uint32_t nb = uint32_t((n + kBlock - 1) / kBlock);
-    // parse every block; the literal histogram of the frame
+    // parse every block; the literal histogram of each group of kGroup
+    // blocks (the device's Huffman groups, aqz_codec.hh kHufGroup)
     std::vector<std::vector<Seq>> bseq(nb);
     std::vector<std::vector<uint8_t>> blit(nb);
-    uint32_t hist[256] = { 0 };
+    const uint32_t ng = (nb + kGroup - 1) / kGroup;
+    std::vector<std::vector<uint32_t>> ghist(ng, std::vector<uint32_t>(256, 0));
     for (uint32_t j = 0; j < nb; ++j) {
         const uint8_t* b = src + uint64_t(j) * kBlock;
         const uint32_t bn = uint32_t(std::min<uint64_t>(kBlock, n - uint64_t(j) * kBlock));
@@ -161,10 +164,12 @@ encode_frame(const uint8_t* src, uint64_t n, bool lz, const SeqTables& st)
         else
             blit[j].assign(b, b + bn);
         for (uint8_t x : blit[j])
-            hist[x]++;
+            ghist[j / kGroup][x]++;
     }
-    const Table t = make_table(hist);
-    bool tree_sent = false;
+    std::vector<Table> gt(ng);
+    for (uint32_t k = 0; k < ng; ++k)
+        gt[k] = make_table(ghist[k].data());
+    std::vector<bool> gsent(ng, false);
     std::vector<uint8_t> tmp(2 * kBlock + 1024);
     for (uint32_t j = 0; j < nb; ++j) {
         const uint8_t* b = src + uint64_t(j) * kBlock;
@@ -182,6 +187,8 @@ encode_frame(const uint8_t* src, uint64_t n, bool lz, const SeqTables& st)
         }
         const std::vector<uint8_t>& L = blit[j];
         const uint32_t nl = uint32_t(L.size());
+        const Table& t = gt[j / kGroup];
+        const bool tree_sent = gsent[j / kGroup];
         // literals section into tmp
         uint32_t lsz = 0, tree_extra = 0; // tree bytes a later block would not carry
         bool used_tree = false;
@@ -235,7 +242,8 @@ encode_frame(const uint8_t* src, uint64_t n, bool lz, const SeqTables& st)
             at += 3 + bn;
             continue;
         }
-        tree_sent |= used_tree;
+        if (used_tree)
+            gsent[j / kGroup] = true;
         g_paths.cmp_block++;
         if (used_tree)
             (t.tree[0] < 128 ? g_paths.tree_fse : g_paths.tree_direct)++;
