@@ -103,12 +103,27 @@ namespace aqz {
 // frames (one per chunk), for a whole resident chunk layer.  A segment is
 // what one zstd frame holds (a blosc block, or a chunk); it is cut into
 // zstd blocks of zstd::kBlock bytes, the parallel unit.
-// The Huffman table of a group of kHufGroup zstd blocks (64 KiB): the
-// literal statistics of a shuffled blosc block change at its byte planes,
-// so one table per segment fits neither plane (tools/zstd_lab.cpp: c-blosc's
-// ratio within 1% with group tables, 6% short with segment tables).  The
-// first Huffman block of a group carries the tree, the rest are Treeless.
+// The Huffman table of a group of zstd blocks (at most kHufGroup, 64 KiB):
+// the literal statistics of a shuffled blosc block change at its byte or bit
+// planes, so one table per segment fits no plane (tools/zstd_lab.cpp: c-blosc's
+// ratio within 1% with group tables, 6% short with segment tables).  A group
+// is one plane where planes are shorter than kHufGroup blocks (bitshuffle:
+// a u16 plane of a 256 KiB block is 16 KiB, 2 blocks; dim sCMOS 3.19 -> 3.40).
+// The first Huffman block of a group carries the tree, the rest are Treeless.
 constexpr uint32_t kHufGroup = 8;
+
+// log2 of the blocks per Huffman group for a segment of seg_bytes
+inline uint32_t
+zstd_huf_group_log2(uint32_t shuffle, uint32_t typesize, uint32_t seg_bytes)
+{
+    uint32_t lg = 3; // kHufGroup
+    if (shuffle == 2 && typesize > 0) {
+        const uint32_t plane = seg_bytes / (8u * typesize);
+        while (lg > 0 && (zstd::kBlock << lg) > plane)
+            --lg;
+    }
+    return lg;
+}
 struct ZstdSegTable
 {
     uint32_t mode;   // 0 raw literals, 1 one symbol, 2 Huffman
@@ -150,6 +165,7 @@ struct ZstdParams
     uint32_t phist;         // parse history: bytes before a unit its matches
                             // may reach (0, kZHist1, kZHist2: the level)
     uint32_t ngrp;          // Huffman groups per segment
+    uint32_t hgrp_log2;     // log2 of the zstd blocks per Huffman group (<= 3)
     uint32_t fit;           // 1: fitted sequence tables allowed (AQZ_ZSTD_FIT=0: predefined)
     const uint32_t* flags;  // has_data words (nullptr: every chunk has data)
     uint32_t tag;

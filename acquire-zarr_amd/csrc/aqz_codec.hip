@@ -763,7 +763,7 @@ zblock(const ZstdParams& p, uint32_t g)
     z.nb = (z.seglen + zstd::kBlock - 1) / zstd::kBlock;
     const uint32_t o = z.b * zstd::kBlock;
     z.len = o < z.seglen ? min(zstd::kBlock, z.seglen - o) : 0;
-    z.grp = z.seg * p.ngrp + z.b / kHufGroup;
+    z.grp = z.seg * p.ngrp + (z.b >> p.hgrp_log2);
     return z;
 }
 
@@ -1104,10 +1104,10 @@ zstd_table(const ZstdParams p)
     __shared__ uint16_t code[256];
     __shared__ uint8_t tree[160];
     __shared__ uint32_t npresent, tree_n, mode;
-    // one Huffman group (kHufGroup blocks of a segment)
+    // one Huffman group (2^hgrp_log2 blocks of a segment)
     const uint32_t gi = blockIdx.x, t = threadIdx.x;
-    const uint32_t s = gi / p.ngrp, b0 = (gi - s * p.ngrp) * kHufGroup;
-    const uint32_t b1 = min(p.bps, b0 + kHufGroup);
+    const uint32_t s = gi / p.ngrp, b0 = (gi - s * p.ngrp) << p.hgrp_log2;
+    const uint32_t b1 = min(p.bps, b0 + (1u << p.hgrp_log2));
     if (zchunk_skip(p, s / p.nseg))
         return;
     if (t == 0)
@@ -1664,6 +1664,7 @@ __global__ __launch_bounds__(64) void
 zstd_segment(const ZstdParams p)
 {
     static_assert(64 % kHufGroup == 0, "a wave step holds whole groups");
+    const uint32_t gl = p.hgrp_log2, gn = 1u << gl;
     const uint32_t s = blockIdx.x, lane = threadIdx.x;
     if (zchunk_skip(p, s / p.nseg)) {
         if (lane == 0)
@@ -1680,10 +1681,10 @@ zstd_segment(const ZstdParams p)
         const bool cmp = b < z0.nb && p.bkind[g] == 2;
         const uint64_t huf = __ballot(cmp && p.bltype[g] == 2);
         const uint64_t sqb = __ballot(cmp && p.bnseq[g] > 0);
-        if (lane < 64 / kHufGroup && b0 + lane * kHufGroup < z0.nb) {
-            const uint32_t m = uint32_t(huf >> (lane * kHufGroup)) & ((1u << kHufGroup) - 1u);
-            p.carrier[s * p.ngrp + (b0 / kHufGroup) + lane] =
-              m ? b0 + lane * kHufGroup + uint32_t(__builtin_ctz(m)) : ~0u;
+        if (lane < (64u >> gl) && b0 + (lane << gl) < z0.nb) {
+            const uint32_t m = uint32_t(huf >> (lane << gl)) & ((1u << gn) - 1u);
+            p.carrier[s * p.ngrp + (b0 >> gl) + lane] =
+              m ? b0 + (lane << gl) + uint32_t(__builtin_ctz(m)) : ~0u;
         }
         if (scar == ~0u && sqb)
             scar = b0 + uint32_t(__ffsll(static_cast<long long>(sqb))) - 1;
@@ -1703,7 +1704,7 @@ zstd_segment(const ZstdParams p)
                 sz = 4;
             } else if (k == 2) {
                 const uint32_t nl = p.bnlit[g];
-                const uint32_t gi = s * p.ngrp + b / kHufGroup;
+                const uint32_t gi = s * p.ngrp + (b >> gl);
                 const uint32_t sd = scar == b ? desc_n : 0;
                 if (p.bltype[g] == 2) {
                     const uint32_t cs = p.bpay[g] + (p.carrier[gi] == b ? p.tab[gi].tree_n : 0);
@@ -1913,7 +1914,7 @@ launch_zstd(const ZstdParams& p, hipStream_t stream)
     if (nblk * kZSubBlocks > 0x7fffffffull || p.nseg == 0 || p.bps == 0 ||
         uint64_t(p.bps) * zstd::kBlock < p.seg_bytes)
         return hipErrorInvalidValue;
-    if (p.ngrp != (p.bps + kHufGroup - 1) / kHufGroup)
+    if (p.hgrp_log2 > 3 || p.ngrp != ((p.bps + (1u << p.hgrp_log2) - 1) >> p.hgrp_log2))
         return hipErrorInvalidValue;
     if (!p.store_only) {
         hipError_t e = hipMemsetAsync(p.scount, 0, nseg * 192 * 4, stream);

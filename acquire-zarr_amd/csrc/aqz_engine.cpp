@@ -351,6 +351,16 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         if (v >= std::max<uint32_t>(4, n_fused_) && (1u << v) <= uint32_t(kMaxRegionRows))
             rh_log2_ = v;
     }
+    // XY-transposed storage order: the strip kernel reads the acquisition-
+    // order frames itself (load_region_xy) when it takes the interior
+    // regions (launch_interior's condition); otherwise transpose_frames
+    // writes the storage-order frames first.  Knob 4096: always transpose.
+    if (xy_ && fused_2d_) {
+        const bool tail = n_levels() - 1 > n_fused_;
+        xy_direct_ = bpp_ <= 4 && rh_log2_ == 6 && n_fused_ >= 3 && !(knobs_ & 128u) &&
+                     (!tail || n_fused_ >= 5) && !(knobs_ & 4096u) &&
+                     (uint64_t(acq_cols_) * bpp_) % 16 == 0;
+    }
 
     const Dim& d0 = lv_[0].dims[0];
     if (d0.array_size_px > 0) {
@@ -944,12 +954,15 @@ Stage::append(const void* frames, uint64_t n_frames, int mem)
 void
 Stage::run_batch(const uint8_t* dsrc, uint32_t n)
 {
-    if (xy_) {
+    if (xy_ && !(xy_direct_ && reinterpret_cast<uintptr_t>(dsrc) % 16 == 0)) {
         xbuf_.alloc(size_t(opt_.max_batch_frames) * acq_rows_ * acq_cols_ * bpp_);
         hip_check(launch_transpose_frames(dsrc, xbuf_.p, acq_rows_, acq_cols_, n,
                                           uint32_t(bpp_), stream_),
                   "transpose launch");
         dsrc = xbuf_.p;
+        xy_src_ = false;
+    } else {
+        xy_src_ = xy_;
     }
     std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
     if (timing_) {
@@ -1075,13 +1088,15 @@ Stage::fused_params(const uint8_t* dsrc, uint32_t n, uint32_t n_fused,
     FusedParams p{};
     p.src = dsrc;
     p.src_stride = uint64_t(L0.W) * L0.H * bpp_;
+    p.xy = xy_src_ ? 1u : 0u;
     p.n_frames = n;
     p.n_fused = n_fused;
     p.rh_log2 = rh_log2;
     const uint32_t RW = uint32_t(512 / bpp_);
     p.nbx = parts_along(L0.W, RW);
     p.nby = parts_along(L0.H, 1u << rh_log2);
-    p.vec_rows = ((uint64_t(L0.W) * bpp_) % 16 == 0 &&
+    // (xy: the acquisition rows, H[0] pixels, are the ones loaded as vectors)
+    p.vec_rows = ((uint64_t(p.xy ? L0.H : L0.W) * bpp_) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(dsrc) % 16 == 0)
                    ? 1
                    : 0;
@@ -1774,7 +1789,9 @@ Compressor::scratch_bytes(const Compression& c, uint64_t chunk_bytes, uint32_t t
         nseg1 = g.nblocks;
     }
     const uint64_t nseg = n * nseg1, bps = (seg + zstd::kBlock - 1) / zstd::kBlock;
-    const uint64_t nblk = nseg * bps, ngrp = nseg * ((bps + kHufGroup - 1) / kHufGroup);
+    const uint32_t gl =
+      zstd_huf_group_log2(c.codec == 2 ? uint32_t(c.shuffle) : 0u, typesize, uint32_t(seg));
+    const uint64_t nblk = nseg * bps, ngrp = nseg * ((bps + (1u << gl) - 1) >> gl);
     b += nseg * 4; // spos
     if (c.codec == 2 && !store_only && (c.shuffle == 2 || (c.shuffle == 1 && typesize > 1)))
         b += n * chunk_bytes; // shuffled input
@@ -1852,15 +1869,21 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
         p.nseg = 1;
     }
     p.bps = (p.seg_bytes + zstd::kBlock - 1) / zstd::kBlock;
-    p.ngrp = (p.bps + kHufGroup - 1) / kHufGroup;
-    // the level: the parse history of plain zstd (level >= 3: 12 KiB, >= 7:
-    // 28 KiB; level 0 is libzstd's default, 3).  Shuffled blosc planes gain
-    // nothing from a history (tools/zstd_lab.cpp: camera 1.891 -> 1.890, dim
-    // 4.09 -> 3.88: the extra short matches cost more than their literals),
-    // so blosc-zstd clevels >= 1 share the unit-local parse.
+    p.hgrp_log2 = zstd_huf_group_log2(p.shuffle, typesize_, p.seg_bytes);
+    p.ngrp = (p.bps + (1u << p.hgrp_log2) - 1) >> p.hgrp_log2;
+    // the level: the parse history (zstd level >= 3: 12 KiB, >= 7: 28 KiB;
+    // plain zstd level 0 is libzstd's default, 3; blosc clevel c is zstd
+    // level 2c - 1, zarr.common.cpp:117-126 -> c-blosc's zstd wrapper).
+    // Byte-shuffled planes gain nothing from a history (tools/zstd_lab.cpp:
+    // camera 1.891 -> 1.890, dim 4.09 -> 3.88: the extra short matches cost
+    // more than their literals), so those blosc-zstd clevels >= 1 share the
+    // unit-local parse.  Bit planes do: a 28 KiB history reaches the previous
+    // plane of a u16 block (camera 1.914 -> 1.977, c-blosc clevel 5 1.974).
     {
-        const int zl = c_.clevel == 0 ? 3 : c_.clevel;
-        p.phist = blosc ? 0 : zl >= 7 ? kZHist2 : zl >= 3 ? kZHist1 : 0;
+        const int zl = blosc ? (c_.clevel == 0 ? 0 : 2 * c_.clevel - 1)
+                             : (c_.clevel == 0 ? 3 : c_.clevel);
+        const bool hist_pays = !blosc || p.shuffle == 2;
+        p.phist = !hist_pays ? 0 : zl >= 7 ? kZHist2 : zl >= 3 ? kZHist1 : 0;
         if (const char* e = std::getenv("AQZ_ZSTD_HIST")) // tuning knob
             p.phist = uint32_t(std::atoi(e));
     }
@@ -2292,6 +2315,10 @@ Stage::dominant_kernel() const
         const bool tail = n_levels() - 1 > n_fused_;
         const bool strip = bpp_ <= 4 && rh_log2_ == 6 && n_fused_ >= 3 &&
                            !(knobs_ & 128u) && (!tail || n_fused_ >= 5);
+        if (xy_)
+            return xy_direct_ ? "fused_pyramid_strip (XY load)"
+                              : (strip ? "transpose_frames + fused_pyramid_strip"
+                                       : "transpose_frames + fused_pyramid");
         return strip ? "fused_pyramid_strip" : "fused_pyramid";
     }
     if (fused_3d_) // launch_fused_pyramid_3d's choice

@@ -414,6 +414,8 @@ class Stage
     // XY-transposed storage order: level-0 frames are transposed into xbuf_
     // (acquisition rows x cols -> storage rows x cols) before the pipeline
     bool xy_ = false;
+    bool xy_direct_ = false; // XY transpose fused into the strip kernel's loads
+    bool xy_src_ = false;    // the batch being launched is in acquisition order
     uint32_t acq_rows_ = 0, acq_cols_ = 0;
     DevBuf xbuf_;
     // source consumption: (event, appended frames when it fires)

@@ -20,6 +20,8 @@
 //   shrink.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "aqz_params.hh"
 #include "aqz_reduce.hh"
 
@@ -576,7 +578,15 @@ generic_region(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0,
             const uint32_t ya = min(y + 1, H0 - 1); // bottom edge replicate
             T r0[VEC], r1[VEC];
             const int nv0 = int(min(uint32_t(VEC), W0 - x));
-            if (p.vec_rows && nv0 == VEC) {
+            if (p.xy) {
+                // acquisition-order source: storage (y, x) is src[x * H0 + y]
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) {
+                    const uint32_t xi = min(x + uint32_t(i), W0 - 1);
+                    r0[i] = src[uint64_t(xi) * H0 + y];
+                    r1[i] = src[uint64_t(xi) * H0 + ya];
+                }
+            } else if (p.vec_rows && nv0 == VEC) {
                 const uint4 a = *reinterpret_cast<const uint4*>(
                   src + uint64_t(y) * W0 + x);
                 const uint4 b = *reinterpret_cast<const uint4*>(
@@ -941,6 +951,69 @@ fused_pyramid(const FusedParams p)
         lean_levels<T, M, RW>(p, f, y0, x0, lds_a, lds_b);
 }
 
+// XY-transposed storage order fused into the strip kernel's region load
+// (transpose_frame, array.cpp:488-534, applied before the split and the
+// downsampler, :525-533).  The region's storage rows [y0, y0+64) x columns
+// [x0, x0+RW) are acquisition columns [y0, y0+64) of acquisition rows
+// [x0, x0+RW): the workgroup reads those rows as coalesced 64-pixel segments
+// (8 x 16 B per lane), stores them in LDS as column pairs (c, c+1), and each
+// thread gathers its storage row vectors: ra[i] = storage row ry + 4i, rb[i]
+// = the row below, both from one LDS read per pixel pair.  Pair index pc of
+// row r sits at (pc + r + r / VEC) mod 32, so the 32 lanes of a gather
+// (rows cv * VEC + k) hit distinct banks.
+template<typename T, int NTM>
+__device__ __forceinline__ void
+load_region_xy(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0, uint32_t ry,
+               uint32_t cv, uint4 (&ra)[4], uint4 (&rb)[4])
+{
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+    typedef typename std::conditional<
+      sizeof(T) == 1, uint16_t,
+      typename std::conditional<sizeof(T) == 2, uint32_t, uint64_t>::type>::type PT;
+    constexpr uint32_t VEC = 16 / sizeof(T);
+    constexpr uint32_t RW = 32 * VEC;      // acquisition rows of the region
+    constexpr uint32_t VR = 4 * sizeof(T); // 16-B vectors per 64-pixel row segment
+    constexpr uint32_t PV = 8 / sizeof(T); // column pairs per 16-B vector
+    __shared__ PT xt[RW * 32];             // 32 KiB
+    const uint64_t pitch = uint64_t(p.H[0]) * sizeof(T); // acquisition row bytes
+    const uint8_t* s =
+      p.src + uint64_t(f) * p.src_stride + uint64_t(x0) * pitch + uint64_t(y0) * sizeof(T);
+    u32x4v v[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        const uint32_t idx = threadIdx.x + 256u * j;
+        const uint32_t r = idx / VR, c16 = idx % VR;
+        v[j] = gload<(NTM & 1) != 0, u32x4v>(s + uint64_t(r) * pitch + c16 * 16u);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        const uint32_t idx = threadIdx.x + 256u * j;
+        const uint32_t r = idx / VR, c16 = idx % VR;
+        PT e[PV];
+        __builtin_memcpy(e, &v[j], 16);
+#pragma unroll
+        for (uint32_t q = 0; q < PV; ++q)
+            xt[r * 32u + ((c16 * PV + q + r + r / VEC) & 31u)] = e[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t pc = (ry + 4u * i) >> 1; // ry is even
+        T a[VEC], b[VEC];
+#pragma unroll
+        for (uint32_t k = 0; k < VEC; ++k) {
+            const uint32_t r = cv * VEC + k;
+            const PT e = xt[r * 32u + ((pc + r + cv) & 31u)];
+            T two[2];
+            __builtin_memcpy(two, &e, sizeof(PT));
+            a[k] = two[0];
+            b[k] = two[1];
+        }
+        __builtin_memcpy(&ra[i], a, 16);
+        __builtin_memcpy(&rb[i], b, 16);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Interior regions of 64 rows with pixels of <= 4 bytes ("strip" kernel).
 // Wave w owns the region's rows [16w, 16w+16): level 1 is a 2x2 in
@@ -953,7 +1026,8 @@ fused_pyramid(const FusedParams p)
 // NTM: compile-time nontemporal policy -- bit 1 input loads, bit 2 level-0
 // tile stores, bit 4 level-1/2 stores (the launcher maps p.nt onto one of the
 // instantiated policies).
-template<typename T, int M, int NTM>
+// XY: the source is in acquisition order (load_region_xy).
+template<typename T, int M, int NTM, bool XY = false>
 __global__ __launch_bounds__(256) void
 fused_pyramid_strip(const FusedParams p)
 {
@@ -988,7 +1062,9 @@ fused_pyramid_strip(const FusedParams p)
     // this half-wave's rows: y0 + ry + 4i + {0, 1}, i = 0..3
     const uint32_t ry = 16 * w + 2 * hw;
     uint4 ra[4], rb[4];
-    {
+    if constexpr (XY) {
+        load_region_xy<T, NTM>(p, f, y0, x0, ry, cv, ra, rb);
+    } else {
         const uint64_t row = uint64_t(p.W[0]) * sizeof(T);
         const uint8_t* s = p.src + uint64_t(f) * p.src_stride + uint64_t(y0 + ry) * row +
                            uint64_t(x0 + cv * VEC) * sizeof(T);
@@ -1802,6 +1878,15 @@ void
 launch_interior(uint32_t blocks, const FusedParams& p, hipStream_t stream)
 {
     if constexpr (sizeof(T) <= 4) {
+        if (p.xy) { // launch_fused_pyramid checked the strip kernel applies
+            if (p.nt)
+                hipLaunchKernelGGL((fused_pyramid_strip<T, M, 7, true>), dim3(blocks),
+                                   dim3(256), 0, stream, p);
+            else
+                hipLaunchKernelGGL((fused_pyramid_strip<T, M, 0, true>), dim3(blocks),
+                                   dim3(256), 0, stream, p);
+            return;
+        }
         if (p.rh_log2 == 6 && p.n_fused >= 3 && !(p.knobs & 128u) &&
             (p.scratch_level == 0 || p.scratch_level >= 5)) {
             switch (p.nt) {
@@ -1842,6 +1927,13 @@ launch_fused_pyramid(int dtype, int method, const FusedParams& p,
     const uint64_t edge =
       uint64_t(p.n_frames) * (uint64_t(p.nbx) * p.nby - uint64_t(p.nbx_in) * p.nby_in);
     if (interior > 0x7fffffffull || edge > 0x7fffffffull)
+        return hipErrorInvalidValue;
+    // acquisition-order source: interior regions only through the strip kernel
+    if (p.xy && interior &&
+        !((dtype == 0 || dtype == 1 || dtype == 2 || dtype == 4 || dtype == 5 ||
+           dtype == 6 || dtype == 8) &&
+          p.rh_log2 == 6 && p.n_fused >= 3 &&
+          !(p.knobs & 128u) && (p.scratch_level == 0 || p.scratch_level >= 5)))
         return hipErrorInvalidValue;
     const FusedParams pr = with_xcd_rotation(p, interior);
 #define CALL(T, MM)                                                            \

@@ -73,8 +73,11 @@ struct LevelRefs
 // the level extents vary per level.
 struct FusedParams
 {
-    const uint8_t* src;      // level-0 frames, row-major
+    const uint8_t* src;      // level-0 frames, row-major (xy: acquisition order)
     uint64_t src_stride;     // bytes between frames
+    uint32_t xy;             // 1: src holds acquisition-order frames (XY-transposed storage
+                             // order): storage pixel (y, x) is src[x * H[0] + y]
+                             // (transpose_frame, array.cpp:488-534, fused into the loads)
     LevelRefs lr[kMaxFused + 1];
     uint8_t* scratch;        // row-major frames of level scratch_level
     uint32_t scratch_level;  // 0: no scratch output

@@ -572,6 +572,40 @@ def test_stage_storage_dimension_order(gpu, perm):
     st.close()
 
 
+# XY-transposed storage order with the transpose fused into the strip
+# kernel's loads (load_region_xy): storage rows = acquisition X (chunk 128,
+# so 64-row regions), 4 levels, interior and edge regions; knob 4096 forces
+# the separate transpose_frames pass, whose output must be the same.
+XY_KERNELS = {"fused": ("0", "fused_pyramid_strip (XY load)"),
+              "pass": ("4096", "transpose_frames + fused_pyramid_strip")}
+
+
+@pytest.mark.parametrize("path", sorted(XY_KERNELS))
+@pytest.mark.parametrize("dtype", [U8, U16, I16, U32, F32], ids=lambda d: DTYPE_NAMES[d])
+def test_stage_xy_fused_strip(gpu, monkeypatch, dtype, path):
+    knobs, name = XY_KERNELS[path]
+    monkeypatch.setenv("AQZ_KNOBS", knobs)
+    # acquisition Y x X = 1000 x 1088 -> storage 1088 rows x 1000 columns
+    acq = [(TIME, 0, 4, 1), (SPACE, 1000, 128, 1), (SPACE, 1088, 128, 1)]
+    methods = [MEAN, MIN] if path == "fused" else [MEAN]
+    for m in methods:
+        frames = _frames(dtype, 6, 1000, 1088, 61 + dtype + 5 * m)
+        stored = np.ascontiguousarray(frames.transpose(0, 2, 1))
+        exp, fw, ldims = expected_stage_layers([acq[0], acq[2], acq[1]], dtype, m, stored)
+        st = gpu.Stage(acq, dtype, m, storage_order=[0, 2, 1], max_batch_frames=4,
+                       layer_slots=4)
+        assert st.dominant_kernel() == name
+        assert st.n_levels() >= 4
+        st.append(frames[:4])
+        st.append(frames[4:])
+        st.finalize()
+        for (l, layer), (buf, flags) in sorted(exp.items()):
+            got, gflags = st.copy_layer(l, layer)
+            assert_same_pixels(got, buf, dtype, f"{path} m{m} L{l} layer{layer}")
+            assert (gflags == flags).all(), (l, layer)
+        st.close()
+
+
 @pytest.mark.parametrize("dtype", [U8, U16, F32, F64], ids=lambda d: DTYPE_NAMES[d])
 def test_stage_xy_transpose_sizes(gpu, dtype):
     # frames larger than one 64x64 transpose tile, ragged on both axes

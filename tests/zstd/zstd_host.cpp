@@ -78,7 +78,7 @@ huf_streams(const Table& t, const uint8_t* lit, uint32_t n, uint8_t* out, uint32
 }
 
 constexpr uint32_t kMinHuf = 64; // fewer literals: stored raw
-constexpr uint32_t kGroup = 8;   // blocks per Huffman table (the device's kHufGroup)
+constexpr uint32_t kGroupLog2 = 3; // blocks per Huffman table: 8 (the device's kHufGroup)
 
 // how often each format path was taken (the run must take every one)
 struct Paths
@@ -145,16 +145,17 @@ parse(const uint8_t* b, uint32_t n, std::vector<Seq>& seqs, std::vector<uint8_t>
 // the device encoder: a block is compressed iff its content, counted with
 // the tree description, is smaller than the block.
 std::vector<uint8_t>
-encode_frame(const uint8_t* src, uint64_t n, bool lz, const SeqTables& st)
+encode_frame(const uint8_t* src, uint64_t n, bool lz, const SeqTables& st,
+             uint32_t glog2 = kGroupLog2)
 {
     std::vector<uint8_t> out(frame_header_bytes(n) + n + 3 * (n / kBlock + 1) + 64);
     uint32_t at = write_frame_header(out.data(), n);
     const uint32_t nb = uint32_t((n + kBlock - 1) / kBlock);
-    // parse every block; the literal histogram of each group of kGroup
-    // blocks (the device's Huffman groups, aqz_codec.hh kHufGroup)
+    // parse every block; the literal histogram of each group of 2^glog2
+    // blocks (the device's Huffman groups, aqz_codec.hh zstd_huf_group_log2)
     std::vector<std::vector<Seq>> bseq(nb);
     std::vector<std::vector<uint8_t>> blit(nb);
-    const uint32_t ng = (nb + kGroup - 1) / kGroup;
+    const uint32_t ng = (nb + (1u << glog2) - 1) >> glog2;
     std::vector<std::vector<uint32_t>> ghist(ng, std::vector<uint32_t>(256, 0));
     for (uint32_t j = 0; j < nb; ++j) {
         const uint8_t* b = src + uint64_t(j) * kBlock;
@@ -164,7 +165,7 @@ encode_frame(const uint8_t* src, uint64_t n, bool lz, const SeqTables& st)
         else
             blit[j].assign(b, b + bn);
         for (uint8_t x : blit[j])
-            ghist[j / kGroup][x]++;
+            ghist[j >> glog2][x]++;
     }
     std::vector<Table> gt(ng);
     for (uint32_t k = 0; k < ng; ++k)
@@ -187,8 +188,8 @@ encode_frame(const uint8_t* src, uint64_t n, bool lz, const SeqTables& st)
         }
         const std::vector<uint8_t>& L = blit[j];
         const uint32_t nl = uint32_t(L.size());
-        const Table& t = gt[j / kGroup];
-        const bool tree_sent = gsent[j / kGroup];
+        const Table& t = gt[j >> glog2];
+        const bool tree_sent = gsent[j >> glog2];
         // literals section into tmp
         uint32_t lsz = 0, tree_extra = 0; // tree bytes a later block would not carry
         bool used_tree = false;
@@ -243,7 +244,7 @@ encode_frame(const uint8_t* src, uint64_t n, bool lz, const SeqTables& st)
             continue;
         }
         if (used_tree)
-            gsent[j / kGroup] = true;
+            gsent[j >> glog2] = true;
         g_paths.cmp_block++;
         if (used_tree)
             (t.tree[0] < 128 ? g_paths.tree_fse : g_paths.tree_direct)++;
@@ -272,17 +273,25 @@ encode_frame(const uint8_t* src, uint64_t n, bool lz, const SeqTables& st)
 // ctypes entry (tests/test_gpu_zstd.py): the frame of src[0..n) into out;
 // bytes, 0 when cap is too small.
 extern "C" uint64_t
-zh_encode_frame(const uint8_t* src, uint64_t n, int lz, uint8_t* out, uint64_t cap)
+zh_encode_frame_g(const uint8_t* src, uint64_t n, int lz, uint32_t glog2, uint8_t* out,
+                  uint64_t cap)
 {
     static SeqTables st;
     static const bool ok = build_seq_tables(st);
-    if (!ok)
+    if (!ok || glog2 > 3)
         return 0;
-    const std::vector<uint8_t> f = encode_frame(src, n, lz != 0, st);
+    const std::vector<uint8_t> f = encode_frame(src, n, lz != 0, st, glog2);
     if (f.size() > cap)
         return 0;
     std::memcpy(out, f.data(), f.size());
     return f.size();
+}
+
+// the same with the default group of 8 blocks
+extern "C" uint64_t
+zh_encode_frame(const uint8_t* src, uint64_t n, int lz, uint8_t* out, uint64_t cap)
+{
+    return zh_encode_frame_g(src, n, lz, kGroupLog2, out, cap);
 }
 
 namespace {

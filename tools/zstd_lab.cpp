@@ -811,7 +811,17 @@ payload(const std::string& kind, uint64_t n, uint32_t seed)
         const double base = dim ? 100.0 : 1000 + 200 * std::sin(double(i) / 977.0);
         px[i] = uint16_t(std::clamp(base + nd(rng), 0.0, 65535.0));
     }
-    if (kind.find("shuf") == std::string::npos) {
+    if (kind.find("bit") != std::string::npos) { // bitshuffle in 256 KiB blosc blocks
+        for (uint64_t b0 = 0; b0 < np; b0 += 131072) {
+            const uint64_t m = std::min<uint64_t>(131072, np - b0);
+            uint8_t* o = v.data() + 2 * b0;
+            std::memset(o, 0, 2 * m);
+            for (uint64_t i = 0; i < m; ++i)
+                for (int bit = 0; bit < 16; ++bit)
+                    if ((px[b0 + i] >> bit) & 1)
+                        o[bit * (m / 8) + i / 8] |= uint8_t(1u << (i % 8));
+        }
+    } else if (kind.find("shuf") == std::string::npos) {
         std::memcpy(v.data(), px.data(), 2 * np);
     } else { // byte shuffle in 256 KiB blosc blocks
         for (uint64_t b0 = 0; b0 < np; b0 += 131072) {
@@ -877,7 +887,7 @@ main(int argc, char** argv)
             p1 = kinds.size();
         const std::string kind = kinds.substr(p0, p1 - p0);
         p0 = p1 + 1;
-        const bool shuf = kind.find("shuf") != std::string::npos;
+        const bool shuf = kind.find("shuf") != std::string::npos || kind.find("bit") != std::string::npos;
         const std::vector<uint8_t> src = payload(kind, chunk, 7);
         const uint64_t seg = shuf ? (256u << 10) : chunk; // one frame per segment
         uint64_t ours = 0;
