@@ -485,6 +485,9 @@ def main():
                     help="end-to-end mode: frames start in host memory (pinned or "
                          "pageable), every completed chunk layer is handed back to "
                          "pinned host buffers (DESIGN.md 'End to end')")
+    ap.add_argument("--xy", action="store_true",
+                    help="XY-transposed storage order (storage_dimension_order swaps the "
+                         "last two dims; the frames stay in acquisition order)")
     ap.add_argument("--no-hbm-probe", action="store_true",
                     help="skip the live streaming probe of this device's HBM rates")
     ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
@@ -544,6 +547,9 @@ def main():
         barrier + device sync on both sides; max over ranks."""
         kw = dict(force_levels=cfg["force_levels"], max_batch_frames=B, layer_slots=2,
                   skip_level0_split=pyramid_only, **PLACEMENT)
+        if args.xy:
+            nd = len(cfg["dims"])
+            kw["storage_order"] = list(range(nd - 2)) + [nd - 1, nd - 2]
         est = aqz.estimate_memory(cfg["dims"], dt, cfg["method"], **kw)
         st = aqz.Stage(cfg["dims"], dt, cfg["method"], device=dev.index, z_slab=slab, **kw)
         # the stage runs on its own HIP stream; the timing marks below are
@@ -651,7 +657,8 @@ def main():
         "dtype": {U8: "u8", U16: "u16", F32: "f32"}[dt],
         "data": "synthetic (device-resident random frames, per-rank seed)",
         "config": {"workload": cfg["workload"] + (" [pyramid only: no level-0 split]"
-                                                  if args.pyramid_only else ""),
+                                                  if args.pyramid_only else "")
+                               + (" [XY-transposed storage order]" if args.xy else ""),
                    "frames_per_step_per_gpu": B, "levels": len(sizes),
                    "level_sizes": [f"{h}x{w}" for (h, w) in sizes],
                    "parallelism": f"{world} independent per-GPU streams, no collective"
