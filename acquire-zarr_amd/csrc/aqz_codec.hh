@@ -167,6 +167,12 @@ struct ZstdParams
     uint32_t ngrp;          // Huffman groups per segment
     uint32_t hgrp_log2;     // log2 of the zstd blocks per Huffman group (<= 3)
     uint32_t fit;           // 1: fitted sequence tables allowed (AQZ_ZSTD_FIT=0: predefined)
+    // far candidates (zstd_far; plain zstd at level >= 5): per segment
+    // position the most recent earlier position with the same 5-byte key,
+    // + 1 (0: none), [n_chunks * nseg * seg_bytes]; nullptr: no far pass
+    uint32_t* far;
+    uint32_t far_tb;        // tag bits of a far table entry (32 - position bits)
+    uint32_t far_slices;    // hash slices (workgroups) per segment: 1, 2, 4 or 8
     const uint32_t* flags;  // has_data words (nullptr: every chunk has data)
     uint32_t tag;
     const zstd::SeqTables* seqt; // predefined sequence tables (device)
@@ -213,6 +219,28 @@ constexpr uint32_t kZSubSeq = 1024; // a match is >= 4 bytes
 // clevel c is zstd level 2c - 1)
 constexpr uint32_t kZHist1 = 12 * 1024;
 constexpr uint32_t kZHist2 = 28 * 1024;
+// far candidates (zstd_far): hash slices of 2^15 entries (128 KiB of LDS
+// each, one workgroup per slice walking the whole segment); a far match is
+// >= 5 bytes.  tools/zstd_lab.cpp, 8 MiB chunks, no LDS history: 4 slices
+// (2^17 entries) camera-like 1.458 -> 1.596, dim sCMOS 3.070 -> 3.260; 8
+// slices camera 1.624 (libzstd level 5: 1.699 / 3.377)
+constexpr uint32_t kFarLog = 15;
+constexpr uint32_t kFarMin = 5;
+constexpr uint32_t kZOffMax = (1u << 24) - 4; // largest match distance (aqz_codec.hip zseq_codes)
+// tag bits for a segment of seg_bytes split into `slices` hash slices (0:
+// segments too large for the pass)
+inline uint32_t
+zstd_far_tag_bits(uint32_t seg_bytes, uint32_t slices)
+{
+    uint32_t pb = 0, sb = 0;
+    while (pb < 32 && (uint64_t(1) << pb) <= seg_bytes) // positions + 1 <= seg_bytes
+        ++pb;
+    while ((1u << sb) < slices)
+        ++sb;
+    const uint32_t room = 32 - sb - kFarLog; // hash bits left for the tag
+    const uint32_t tb = 32 - pb < room ? 32 - pb : room;
+    return tb >= 6 ? tb : 0;
+}
 
 hipError_t launch_zstd(const ZstdParams& p, hipStream_t stream);
 

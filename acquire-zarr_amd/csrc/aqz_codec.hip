@@ -779,17 +779,132 @@ zchunk_skip(const ZstdParams& p, uint32_t c)
     return p.flags && p.flags[c] != p.tag;
 }
 
-// HIST: bytes of the segment before the unit that its matches may reach
-// (loaded into LDS ahead of the unit and hashed, insert only); HLOG: hash
-// table entries (LDS positions + 1, so 16 bits cover the 32 KiB window).
-template<uint32_t HIST, uint32_t HLOG>
+// Far candidates for the parse: libzstd's levels >= 3 find most of their
+// matches on noisy camera data 8 KiB - 2 MiB back -- 5-byte coincidences no
+// unit-local window sees (tools/zstd_lab.cpp).  A segment's positions are
+// split by a 32-bit hash of their 5-byte key into p.far_slices slices; one
+// workgroup per (segment, slice) walks the whole segment in order, one parse
+// unit (kZSub bytes) per step, and keeps for its slice a table of 2^kFarLog
+// entries in LDS: (position + 1) << far_tb | tag, the most recent position
+// per bucket.  Each step first probes (a tag-equal entry is the candidate:
+// far[i] = its position + 1, else 0), then inserts the step's positions (LDS
+// atomic max: the latest wins), so a position sees every earlier unit; the
+// parse's own table covers its unit.  The next step's bytes are loaded while
+// the current one is probed.  The slices of one segment run on one XCD
+// (their far[] stores interleave in the same lines).  The parse verifies
+// every candidate.
+constexpr uint32_t kFarThreads = 1024;
+static_assert(kZSub == 4 * kFarThreads, "one parse unit per far step, 4 positions a thread");
+
+__device__ __forceinline__ uint32_t
+far_hash(uint32_t lo, uint32_t hi)
+{
+    uint32_t h = lo * 0x9E3779B1u + hi * 0x7FEB352Du;
+    h ^= h >> 15;
+    h *= 0x846CA68Bu;
+    h ^= h >> 16;
+    return h;
+}
+
+__global__ __launch_bounds__(kFarThreads) void
+zstd_far(const ZstdParams p)
+{
+    __shared__ uint32_t T[1u << kFarLog];
+    const uint32_t S = p.far_slices, nb = gridDim.x, b = blockIdx.x;
+    const uint32_t grp = 8u * S, full = nb - nb % grp;
+    uint32_t seg, slice;
+    if (b < full) { // groups of 8 segments x S slices, a segment's on XCD b % 8
+        seg = (b / grp) * 8 + (b & 7u);
+        slice = (b % grp) >> 3;
+    } else {
+        seg = b / S;
+        slice = b % S;
+    }
+    const uint32_t c = seg / p.nseg, j = seg - c * p.nseg;
+    if (zchunk_skip(p, c))
+        return;
+    const uint64_t s0 = uint64_t(j) * p.seg_bytes;
+    const uint32_t len = uint32_t(min(uint64_t(p.seg_bytes), uint64_t(p.nbytes) - s0));
+    const uint8_t* src = p.src + c * p.src_pitch + s0;
+    uint32_t* far = p.far + uint64_t(seg) * p.seg_bytes;
+    const uint32_t t = threadIdx.x, TB = p.far_tb, tmask = (1u << TB) - 1u;
+    const uint32_t sbits = 31u - uint32_t(__builtin_clz(S)); // log2 of the slices
+    const uint32_t bshift = 32u - sbits - kFarLog;
+    for (uint32_t i = t; i < (1u << kFarLog); i += kFarThreads)
+        T[i] = 0;
+    // positions with fewer than 5 bytes after them have no key
+    const uint32_t nkey = len >= 5 ? len - 4 : 0;
+    if (slice == 0)
+        for (uint32_t i = nkey + t; i < len; i += kFarThreads)
+            far[i] = 0;
+    // bytes [i0, i0 + 8) of this thread's step (zero past the segment)
+    auto load = [&](uint32_t i0, uint32_t& a, uint32_t& d) {
+        if (i0 + 8 <= len) {
+            a = *reinterpret_cast<const uint32_t*>(src + i0);
+            d = *reinterpret_cast<const uint32_t*>(src + i0 + 4);
+        } else {
+            a = d = 0;
+            for (uint32_t k = 0; k < 8 && i0 + k < len; ++k)
+                (k < 4 ? a : d) |= uint32_t(src[i0 + k]) << (8 * (k & 3u));
+        }
+    };
+    uint32_t a = 0, d = 0;
+    if (4 * t < nkey)
+        load(4 * t, a, d);
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < nkey; b0 += kZSub) {
+        const uint32_t i0 = b0 + 4 * t;
+        uint32_t na = 0, nd = 0;
+        if (i0 + kZSub < nkey)
+            load(i0 + kZSub, na, nd);
+        uint32_t h[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            h[k] = far_hash(__builtin_amdgcn_alignbyte(d, a, k), (d >> (8 * k)) & 255u);
+        // probe
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t i = i0 + k;
+            if (i < nkey && (sbits == 0 || (h[k] >> (32u - sbits)) == slice)) {
+                const uint32_t e = T[(h[k] >> bshift) & ((1u << kFarLog) - 1u)];
+                far[i] = (e != 0 && (e & tmask) == (h[k] & tmask)) ? (e >> TB) : 0u;
+            }
+        }
+        __syncthreads();
+        // insert
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t i = i0 + k;
+            if (i < nkey && (sbits == 0 || (h[k] >> (32u - sbits)) == slice))
+                atomicMax(&T[(h[k] >> bshift) & ((1u << kFarLog) - 1u)],
+                          ((i + 1) << TB) | (h[k] & tmask));
+        }
+        __syncthreads();
+        a = na;
+        d = nd;
+    }
+}
+
+// FAR: p.far holds zstd_far's candidates; a lane keeps the longer of its
+// local match and the verified far one (>= kFarMin bytes, measured up to 16).
+template<uint32_t HIST, uint32_t HLOG, bool FAR = false>
 __global__ __launch_bounds__(64) void
 zstd_parse(const ZstdParams p)
 {
     __shared__ __attribute__((aligned(16))) uint32_t sw[(HIST + kZSub) / 4 + 4];
     __shared__ uint16_t table[1u << HLOG];
     __shared__ uint32_t lh[256];
-    const uint32_t q = blockIdx.x, g = q / kZSubBlocks, k = q - g * kZSubBlocks;
+    // FAR: the units are dealt to the 8 XCDs in contiguous ranges (block b
+    // runs on XCD b mod 8), so an XCD walks its chunks in order and the far
+    // candidates its units verify -- mostly within the last MiB of the same
+    // chunk -- were just read through the same L2
+    uint32_t q = blockIdx.x;
+    if constexpr (FAR) {
+        const uint32_t per = gridDim.x >> 3;
+        if (q < (per << 3))
+            q = (q & 7u) * per + (q >> 3);
+    }
+    const uint32_t g = q / kZSubBlocks, k = q - g * kZSubBlocks;
     const uint32_t lane = threadIdx.x;
     const ZBlock z = zblock(p, g);
     const uint32_t so = k * kZSub;
@@ -916,6 +1031,10 @@ zstd_parse(const ZstdParams p)
     if (L >= 8) {
         const uint32_t mflimit = H + L - 4; // last position a match may start
         const uint32_t matchlimit = H + L;  // a match ends at or before here
+        // FAR: the segment, its far candidates, the unit's segment offset
+        const uint8_t* seg = p.src + z.c * p.src_pitch + uint64_t(z.j) * p.seg_bytes;
+        const uint32_t* farp = FAR ? p.far + uint64_t(z.seg) * p.seg_bytes : nullptr;
+        const uint32_t ubase = z.b * zstd::kBlock + so;
         for (uint32_t base = H; base <= mflimit && !full;) {
             uint32_t cand[kWin], mlen[kWin];
             uint64_t M[kWin];
@@ -951,8 +1070,47 @@ zstd_parse(const ZstdParams p)
                             while (len < lim && sb[qq + len] == sb[c + len])
                                 ++len;
                         if (len >= minlen) {
-                            cand[w] = c;
+                            cand[w] = qq - c; // distance
                             mlen[w] = len;
+                        }
+                    }
+                    if constexpr (FAR) {
+                        const uint32_t sp = ubase + (qq - H);
+                        const uint32_t fv = farp[sp];
+                        if (fv != 0 && fv - 1 < sp) {
+                            // bytes of the candidate from global memory: one
+                            // 8-B load holds its first 8 - (fp & 3) >= 5;
+                            // the next 8 only when those all match
+                            typedef uint32_t u32x2 __attribute__((ext_vector_type(2), aligned(4)));
+                            const uint32_t fp = fv - 1, wi = fp >> 2, sh = 8u * (fp & 3u);
+                            const uint32_t nw = (z.seglen + 3u) >> 2; // words of the segment
+                            const uint32_t* a4 = reinterpret_cast<const uint32_t*>(seg) + wi;
+                            const u32x2 v = wi + 2 <= nw ? *reinterpret_cast<const u32x2*>(a4)
+                                                   : u32x2{ a4[0], 0u };
+                            const uint64_t cw = (uint64_t(v.y) << 32 | v.x) >> sh;
+                            const uint64_t mine =
+                              uint64_t(lds_rd32(sw, qq + 4)) << 32 | lds_rd32(sw, qq);
+                            const uint32_t avail = 8u - (fp & 3u);
+                            const uint64_t x = (cw ^ mine) & (~0ull >> (64u - 8u * avail));
+                            uint32_t flen = x ? uint32_t(__builtin_ctzll(x)) >> 3 : avail;
+                            if (flen == avail) {
+                                // candidate bytes [avail, avail + 8) are words
+                                // wi + 2, wi + 3
+                                const uint32_t w2 = wi + 2;
+                                const u32x2 u = w2 + 2 <= nw
+                                                  ? *reinterpret_cast<const u32x2*>(a4 + 2)
+                                                  : u32x2{ w2 < nw ? a4[2] : 0u, 0u };
+                                const uint64_t x2 =
+                                  (uint64_t(u.y) << 32 | u.x) ^
+                                  (uint64_t(lds_rd32(sw, qq + avail + 4)) << 32 |
+                                   lds_rd32(sw, qq + avail));
+                                flen += x2 ? uint32_t(__builtin_ctzll(x2)) >> 3 : 8u;
+                            }
+                            flen = min(flen, min(matchlimit - qq, 16u));
+                            if (flen >= kFarMin && flen > mlen[w] && sp - fp <= kZOffMax) {
+                                cand[w] = sp - fp;
+                                mlen[w] = flen;
+                            }
                         }
                     }
                 }
@@ -971,9 +1129,10 @@ zstd_parse(const ZstdParams p)
                         break;
                     const uint32_t i = uint32_t(__ffsll(static_cast<long long>(mm))) - 1;
                     const uint32_t qq = wb + i;
-                    const uint32_t cc = rdlane(cand[w], i);
+                    const uint32_t dist = rdlane(cand[w], i);
                     uint32_t len = rdlane(mlen[w], i);
-                    if (len == kLenCap) {
+                    if (len == kLenCap) { // a local match (far ones are <= 16 bytes)
+                        const uint32_t cc = qq - dist;
                         for (;;) {
                             const uint32_t a = qq + len + lane;
                             const bool eq = a < matchlimit && sb[a] == sb[cc + len + lane];
@@ -987,7 +1146,7 @@ zstd_parse(const ZstdParams p)
                         }
                     }
                     if (lane == 0)
-                        sseq[nseq] = zstd::pack_seq(qq - anchor, len, qq - cc);
+                        sseq[nseq] = zstd::pack_seq(qq - anchor, len, dist);
                     ++nseq;
                     full = nseq == kZSubSeq;
                     p0 = qq + len;
@@ -1170,7 +1329,11 @@ zstd_table(const ZstdParams p)
 }
 
 // A sequence's codes and extra bits in one word: llc (6) | mlc (6) | ofc (5)
-// | ll extra (16) | ml extra (16) | offset extra (15).
+// | ll extra (13) | ml extra (11) | offset extra (23).  A block's sequence
+// has < 2 * kZSub literals (its unit's and the previous unit's tail: LL
+// extra <= 13 bits) and a match ends inside its unit (length <= kZSub: ML
+// extra <= 11 bits); far matches reach < 2^24 - 3 back (OF extra <= 23 bits).
+static_assert(2 * kZSub <= 8192 && kZSub <= 4096, "sequence word field widths");
 __device__ __forceinline__ uint64_t
 zseq_codes(const zstd::Seq& v)
 {
@@ -1178,7 +1341,7 @@ zseq_codes(const zstd::Seq& v)
     const uint32_t ofv = v.off + 3, ofc = zstd::highbit(ofv);
     return uint64_t(llc) | uint64_t(mlc) << 6 | uint64_t(ofc) << 12 |
            uint64_t(v.lit - zstd::ll_base(llc)) << 17 |
-           uint64_t(v.len - zstd::ml_base(mlc)) << 33 | uint64_t(ofv - (1u << ofc)) << 49;
+           uint64_t(v.len - zstd::ml_base(mlc)) << 30 | uint64_t(ofv - (1u << ofc)) << 41;
 }
 
 // zstd::encode_sequences over pre-coded sequences (same bitstream), with
@@ -1200,9 +1363,9 @@ zseq_encode(const TL& tll, const TO& tof, const TM& tml, const uint64_t* sv, uin
     uint32_t llc = uint32_t(v & 63u), mlc = uint32_t((v >> 6) & 63u), ofc = uint32_t((v >> 12) & 31u);
     uint32_t sml = zstd::fse_init(t.ml, mlc), sof = zstd::fse_init(t.of, ofc),
              sll = zstd::fse_init(t.ll, llc);
-    w.add((v >> 17) & 0xFFFFu, zstd::ll_bits(llc));
-    w.add((v >> 33) & 0xFFFFu, zstd::ml_bits(mlc));
-    w.add(v >> 49, ofc);
+    w.add((v >> 17) & 0x1FFFu, zstd::ll_bits(llc));
+    w.add((v >> 30) & 0x7FFu, zstd::ml_bits(mlc));
+    w.add(v >> 41, ofc);
     uint64_t nx = n >= 2 ? sv[n - 2] : 0;
     for (int i = int(n) - 2; i >= 0; --i) {
         v = nx;
@@ -1214,9 +1377,9 @@ zseq_encode(const TL& tll, const TO& tof, const TM& tml, const uint64_t* sv, uin
         zstd::fse_enc(w, sof, t.of, ofc);
         zstd::fse_enc(w, sml, t.ml, mlc);
         zstd::fse_enc(w, sll, t.ll, llc);
-        w.add((v >> 17) & 0xFFFFu, zstd::ll_bits(llc));
-        w.add((v >> 33) & 0xFFFFu, zstd::ml_bits(mlc));
-        w.add(v >> 49, ofc);
+        w.add((v >> 17) & 0x1FFFu, zstd::ll_bits(llc));
+        w.add((v >> 30) & 0x7FFu, zstd::ml_bits(mlc));
+        w.add(v >> 41, ofc);
     }
     zstd::fse_flush(w, sml, t.ml);
     zstd::fse_flush(w, sof, t.of);
@@ -1617,12 +1780,29 @@ zstd_seqtab(const ZstdParams p)
 __global__ __launch_bounds__(64) void
 zstd_seqenc(const ZstdParams p)
 {
+    // one wave per (segment, 64 of its blocks): the segment's tables -- the
+    // predefined ones or its fitted ones -- in LDS, so the FSE state chains
+    // look them up at LDS latency
     __shared__ zstd::SeqTables seqt;
-    for (uint32_t i = threadIdx.x; i < sizeof(zstd::SeqTables) / 4; i += 64)
-        reinterpret_cast<uint32_t*>(&seqt)[i] = reinterpret_cast<const uint32_t*>(p.seqt)[i];
+    __shared__ zstd::FseTable<zstd::kSeqMaxLog> fll, fof, fml;
+    const uint32_t gpseg = (p.bps + 63) / 64;
+    const uint32_t s = blockIdx.x / gpseg, k0 = (blockIdx.x - s * gpseg) * 64;
+    const ZstdSeqSeg& Q = p.sqt[s];
+    const bool fitted = !zchunk_skip(p, s / p.nseg) && Q.mode == 2;
+    if (fitted) {
+        for (uint32_t i = threadIdx.x; i < sizeof(fll) / 4; i += 64) {
+            reinterpret_cast<uint32_t*>(&fll)[i] = reinterpret_cast<const uint32_t*>(&Q.ll)[i];
+            reinterpret_cast<uint32_t*>(&fof)[i] = reinterpret_cast<const uint32_t*>(&Q.of)[i];
+            reinterpret_cast<uint32_t*>(&fml)[i] = reinterpret_cast<const uint32_t*>(&Q.ml)[i];
+        }
+    } else {
+        for (uint32_t i = threadIdx.x; i < sizeof(zstd::SeqTables) / 4; i += 64)
+            reinterpret_cast<uint32_t*>(&seqt)[i] = reinterpret_cast<const uint32_t*>(p.seqt)[i];
+    }
     __syncthreads();
-    const uint64_t g = uint64_t(blockIdx.x) * 64 + threadIdx.x;
-    if (g >= uint64_t(p.n_chunks) * p.nseg * p.bps || p.bkind[g] != 4)
+    const uint32_t b = k0 + threadIdx.x;
+    const uint64_t g = uint64_t(s) * p.bps + b;
+    if (b >= p.bps || p.bkind[g] != 4)
         return;
     const ZBlock z = zblock(p, uint32_t(g));
     const uint32_t nseq = p.bseqb[g], lpay = p.bpay[g], nl = p.bnlit[g];
@@ -1636,14 +1816,12 @@ zstd_seqenc(const ZstdParams p)
     // [count][modes, patched by zstd_write][bitstream]; the table
     // descriptions of a fitted segment are counted as if this block carried
     // them (as the tree), so the decision does not depend on which block does
-    const ZstdSeqSeg& Q = p.sqt[z.seg];
-    const bool fitted = Q.mode == 2;
     uint8_t* so = p.scratch + g * zstd::kBlock + lpay;
     const uint32_t cap = zstd::kBlock - lpay;
     uint32_t sq = zstd::write_seq_header(so, nseq);
     const uint64_t* sv = p.seqs + g * kZSubBlocks * kZSubSeq;
     const uint32_t bcap = cap > sq ? cap - sq : 0;
-    const uint32_t bits = fitted ? zseq_encode(Q.ll, Q.of, Q.ml, sv, nseq, so + sq, bcap)
+    const uint32_t bits = fitted ? zseq_encode(fll, fof, fml, sv, nseq, so + sq, bcap)
                                  : zseq_encode(seqt.ll, seqt.of, seqt.ml, sv, nseq, so + sq, bcap);
     sq = bits ? sq + bits : 0;
     if (sq != 0 && lsec + sq + (fitted ? Q.desc_n : 0) < z.len) {
@@ -1925,12 +2103,28 @@ launch_zstd(const ZstdParams& p, hipStream_t stream)
             if (e != hipSuccess)
                 return e;
             const dim3 gd(uint32_t(nblk * kZSubBlocks));
-            if (p.phist == 0)
+            if (p.far) {
+                const uint32_t S = p.far_slices;
+                if (!(S == 1 || S == 2 || S == 4 || S == 8) || p.far_tb < 6 ||
+                    p.far_tb + kFarLog + (S == 8 ? 3 : S == 4 ? 2 : S == 2 ? 1 : 0) > 32 ||
+                    (reinterpret_cast<uintptr_t>(p.src) & 3u) || (p.src_pitch & 3u) ||
+                    (p.seg_bytes & 3u))
+                    return hipErrorInvalidValue;
+                hipLaunchKernelGGL(zstd_far, dim3(uint32_t(nseg * p.far_slices)),
+                                   dim3(kFarThreads), 0, stream, p);
+            }
+            if (p.phist == 0 && !p.far)
                 hipLaunchKernelGGL((zstd_parse<0, kLz4HashLog>), gd, dim3(64), 0, stream, p);
-            else if (p.phist <= kZHist1)
+            else if (p.phist <= kZHist1 && !p.far)
                 hipLaunchKernelGGL((zstd_parse<kZHist1, 13>), gd, dim3(64), 0, stream, p);
-            else
+            else if (!p.far)
                 hipLaunchKernelGGL((zstd_parse<kZHist2, 14>), gd, dim3(64), 0, stream, p);
+            else if (p.phist == 0)
+                hipLaunchKernelGGL((zstd_parse<0, kLz4HashLog, true>), gd, dim3(64), 0, stream, p);
+            else if (p.phist <= kZHist1)
+                hipLaunchKernelGGL((zstd_parse<kZHist1, 13, true>), gd, dim3(64), 0, stream, p);
+            else
+                hipLaunchKernelGGL((zstd_parse<kZHist2, 14, true>), gd, dim3(64), 0, stream, p);
         } else {
             hipLaunchKernelGGL(zstd_hist, dim3(uint32_t(nblk)), dim3(256), 0, stream, p);
         }
@@ -1938,7 +2132,7 @@ launch_zstd(const ZstdParams& p, hipStream_t stream)
         hipLaunchKernelGGL(zstd_encode, dim3(uint32_t(nblk)), dim3(256), 0, stream, p);
         hipLaunchKernelGGL(zstd_seqtab, dim3(uint32_t(nseg)), dim3(64), 0, stream, p);
         if (p.match)
-            hipLaunchKernelGGL(zstd_seqenc, dim3(uint32_t((nblk + 63) / 64)), dim3(64), 0,
+            hipLaunchKernelGGL(zstd_seqenc, dim3(uint32_t(nseg * ((p.bps + 63) / 64))), dim3(64), 0,
                                stream, p);
         hipLaunchKernelGGL(zstd_segment, dim3(uint32_t(nseg)), dim3(64), 0, stream, p);
     }

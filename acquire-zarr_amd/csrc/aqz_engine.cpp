@@ -1770,6 +1770,30 @@ Compressor::Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compressio
     store_only_ = c.codec != 3 && c.clevel == 0;
 }
 
+// Hash slices of the far-candidate pass for a compression setting (0: no
+// far pass).  zstd level L (blosc clevel c is zstd level 2c - 1,
+// zarr.common.cpp:117-126 -> c-blosc's zstd wrapper; plain zstd level 0 is
+// libzstd's default, 3):
+//   plain zstd   L 1-2: none (unit-local parse); 3-6: 4 slices (2^17
+//                entries); >= 7: 8 slices (2^18)
+//   blosc-zstd   bitshuffle, L >= 3: 1 slice (a bit plane of a u16 block
+//                matches the previous plane 16 KiB back: camera 1.914 ->
+//                1.983, c-blosc clevel 5 1.974); byte shuffle: none (its
+//                planes lose from longer matches: camera 1.891 -> 1.845)
+// (tools/zstd_lab.cpp far=..., farbatch=4096)
+uint32_t
+zstd_far_slices(const Compression& c, uint32_t typesize)
+{
+    (void)typesize;
+    if (c.codec == 3) {
+        const int zl = c.clevel == 0 ? 3 : c.clevel;
+        return zl >= 7 ? 8u : zl >= 3 ? 4u : 0u;
+    }
+    if (c.codec == 2 && c.shuffle == 2 && c.clevel >= 2)
+        return 1u;
+    return 0u;
+}
+
 uint64_t
 Compressor::scratch_bytes(const Compression& c, uint64_t chunk_bytes, uint32_t typesize,
                           uint32_t n_chunks)
@@ -1797,6 +1821,8 @@ Compressor::scratch_bytes(const Compression& c, uint64_t chunk_bytes, uint32_t t
         b += n * chunk_bytes; // shuffled input
     if (store_only)
         return b;
+    if (zstd_far_slices(c, typesize))
+        b += nseg * seg * 4; // far candidates
     const uint64_t nu = nblk * kZSubBlocks;
     b += nu * kZSub + nu * kZSubSeq * 8 + 4 * nu * 4;              // parse units
     b += nblk * (1 + 4 + 4 + 4 + 256 * 4 + 1 + 4 + 4 + zstd::kBlock); // per block
@@ -1871,22 +1897,14 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
     p.bps = (p.seg_bytes + zstd::kBlock - 1) / zstd::kBlock;
     p.hgrp_log2 = zstd_huf_group_log2(p.shuffle, typesize_, p.seg_bytes);
     p.ngrp = (p.bps + (1u << p.hgrp_log2) - 1) >> p.hgrp_log2;
-    // the level: the parse history (zstd level >= 3: 12 KiB, >= 7: 28 KiB;
-    // plain zstd level 0 is libzstd's default, 3; blosc clevel c is zstd
-    // level 2c - 1, zarr.common.cpp:117-126 -> c-blosc's zstd wrapper).
-    // Byte-shuffled planes gain nothing from a history (tools/zstd_lab.cpp:
-    // camera 1.891 -> 1.890, dim 4.09 -> 3.88: the extra short matches cost
-    // more than their literals), so those blosc-zstd clevels >= 1 share the
-    // unit-local parse.  Bit planes do: a 28 KiB history reaches the previous
-    // plane of a u16 block (camera 1.914 -> 1.977, c-blosc clevel 5 1.974).
-    {
-        const int zl = blosc ? (c_.clevel == 0 ? 0 : 2 * c_.clevel - 1)
-                             : (c_.clevel == 0 ? 3 : c_.clevel);
-        const bool hist_pays = !blosc || p.shuffle == 2;
-        p.phist = !hist_pays ? 0 : zl >= 7 ? kZHist2 : zl >= 3 ? kZHist1 : 0;
-        if (const char* e = std::getenv("AQZ_ZSTD_HIST")) // tuning knob
-            p.phist = uint32_t(std::atoi(e));
-    }
+    // The level chooses how far back matches reach (zstd_far_slices): the
+    // unit-local parse at the fast levels, the far candidates above them.
+    // A parse history (matches into the 12 / 28 KiB before a unit, loaded and
+    // hashed per unit) is kept only as a tuning knob: the far candidates
+    // reach every earlier unit at a fraction of its cost.
+    p.phist = 0;
+    if (const char* e = std::getenv("AQZ_ZSTD_HIST")) // tuning knob
+        p.phist = uint32_t(std::atoi(e));
     // a match must save the bits of a sequence: ~12 with the fitted tables
     // of unshuffled data, 16 on shuffled planes (tools/zstd_lab.cpp sweep)
     p.match_bits = uint32_t(blosc ? zstd::kMatchBits : zstd::kMatchBitsFitted);
@@ -1917,6 +1935,20 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
                 throw Error(10, "zstd sequence tables");
             seqt_.alloc(sizeof(t));
             hip_check(hipMemcpy(seqt_.p, &t, sizeof(t), hipMemcpyHostToDevice), "hipMemcpy");
+        }
+        // far candidates (zstd_far) in place of a parse history, where a
+        // history pays: zstd_far_slices (the level), 4-byte aligned segments;
+        // AQZ_ZSTD_FAR=0 off
+        p.far_slices = zstd_far_slices(c_, typesize_);
+        p.far_tb = p.far_slices ? zstd_far_tag_bits(p.seg_bytes, p.far_slices) : 0;
+        bool far = p.match && p.far_tb != 0 && (reinterpret_cast<uintptr_t>(p.src) & 3u) == 0 &&
+                   (p.src_pitch & 3u) == 0 && (p.seg_bytes & 3u) == 0;
+        if (const char* e = std::getenv("AQZ_ZSTD_FAR")) // tuning knob
+            far = far && std::atoi(e) != 0;
+        if (far) {
+            far_.alloc(nseg * p.seg_bytes * 4);
+            p.far = reinterpret_cast<uint32_t*>(far_.p);
+            p.phist = 0; // the far candidates cover every earlier unit
         }
         if (p.match) {
             const uint64_t nu = nblk * kZSubBlocks;

@@ -81,12 +81,15 @@ struct Compression
 {
     int32_t codec = 0;   // 0 none, 1 blosc-lz4, 2 blosc-zstd, 3 zstd
     int32_t clevel = 1;  // blosc clevel (0 stores every chunk uncompressed);
-                         // zstd level (the device encoder has one setting)
+                         // zstd level (the device encoder: zstd_far_slices)
     int32_t shuffle = 1; // 0 none, 1 byte, 2 bit
 };
 
 // Device frames of arrays of equally sized device chunks (aqz_codec.hip):
 // blosc1-lz4, blosc1-zstd or plain zstd.
+// hash slices of the device zstd far-candidate pass (0: none); aqz_engine.cpp
+uint32_t zstd_far_slices(const Compression& c, uint32_t typesize);
+
 class Compressor
 {
   public:
@@ -130,7 +133,7 @@ class Compressor
         for (const DevBuf* b : { &zin_, &hist_, &scount_, &bkind_, &bpay_, &bpos_, &tab_, &carrier_,
                                  &sraw_, &lits_, &seqs_, &snseq_, &snlit_, &stail_, &bltype_,
                                  &bnseq_, &sqt_, &scarrier_, &sval_,
-                                 &bseqb_, &bnlit_, &seqt_ })
+                                 &bseqb_, &bnlit_, &seqt_, &far_ })
             n += b->n;
         return n;
     }
@@ -147,7 +150,7 @@ class Compressor
     DevBuf scratch_, ssize_, spos_, fsize_, mode_, cstart_;
     DevBuf zin_, hist_, scount_, bkind_, bpay_, bpos_, tab_, carrier_, sraw_; // zstd
     DevBuf bnseq_, sqt_, scarrier_, sval_;
-    DevBuf lits_, seqs_, snseq_, snlit_, stail_, bltype_, bseqb_, bnlit_, seqt_;
+    DevBuf lits_, seqs_, snseq_, snlit_, stail_, bltype_, bseqb_, bnlit_, seqt_, far_;
 };
 
 struct ArrayDesc

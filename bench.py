@@ -264,6 +264,10 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
             d2h[0] += lbytes[l] if codec != 1 and host_zstd else int(off[-1])
             out_bytes[0] += int(off[-1])
 
+    # zstd level 1 (the reference's examples and tests compress at level 1),
+    # blosc clevel 5; --clevel overrides
+    clevel = args.clevel if args.clevel >= 0 else (1 if codec == 3 else 5)
+
     def hand_off():
         if codec:
             drain_compressed()  # last step's layers: their kernels are done by now
@@ -272,8 +276,7 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
             while handed[l] < done:
                 i = handed[l] % 4
                 if codec:
-                    st.compress_layer(l, handed[l], codec=codec,
-                                      clevel=3 if codec == 3 else 5,
+                    st.compress_layer(l, handed[l], codec=codec, clevel=clevel,
                                       shuffle=0 if codec == 3 else args.compress)
                     pending.append((l, handed[l]))
                 else:
@@ -318,7 +321,7 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
                       2: ("device shuffle (%d) -> D2H -> host blosc-zstd of every chunk "
                           "layer" if host_zstd else "device blosc-zstd compression "
                           "(shuffle %d) -> D2H of every compressed chunk layer") % args.compress,
-                      3: ("D2H -> host zstd (level 3) of every chunk layer" if host_zstd
+                      3: ("D2H -> host zstd of every chunk layer" if host_zstd
                           else "device zstd compression -> D2H of every compressed chunk "
                           "layer")}[codec]
                      if codec else "D2H of every chunk layer"),
@@ -330,7 +333,7 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
         "data": f"synthetic{' camera-like' if codec else ' random'}, host {args.e2e} source ring of {src_frames} frames",
         "config": {"workload": cfg["workload"].replace("device-resident", "host-resident") +
                    f" [e2e, {args.e2e} source]", "frames_per_step_per_gpu": B,
-                   "levels": L},
+                   "levels": L, "clevel": clevel if codec else None},
         "h2d_gbs_per_gpu": round(in_bytes / el / 1e9, 3),
         "d2h_gbs_per_gpu": round(d2h[0] / el / 1e9, 3),
         "frames_per_s_per_gpu": round(args.steps * B / el, 1),
@@ -485,6 +488,8 @@ def main():
                     help="end-to-end mode: frames start in host memory (pinned or "
                          "pageable), every completed chunk layer is handed back to "
                          "pinned host buffers (DESIGN.md 'End to end')")
+    ap.add_argument("--clevel", type=int, default=-1,
+                    help="e2e compression level (default: zstd 1, blosc 5)")
     ap.add_argument("--xy", action="store_true",
                     help="XY-transposed storage order (storage_dimension_order swaps the "
                          "last two dims; the frames stay in acquisition order)")

@@ -389,10 +389,15 @@ aqz_status aqz_stage_device_layer(aqz_stage* st, uint32_t level,
  *    106-140 with "zstd"); blosc clevel 0 stores memcpyed frames.
  *  - AQZ_CODEC_ZSTD: one zstd frame per chunk (ZSTD_compress,
  *    zarr.common.cpp:142-166), made on the device.
- *  The device zstd encoder has one operating point for every level: Huffman
- *  literals (one table per frame), a greedy LZ parse in 4 KiB units and
- *  the predefined sequence tables; ratios on camera-like u16 data are within
- *  ~8% (blosc-zstd) and ~16% (plain zstd) of libzstd at level 5.  With
+ *  The device zstd encoder: Huffman literals (one table per 64 KiB group of
+ *  blocks, or per bit plane under bitshuffle), sequence tables fitted per
+ *  frame, a greedy LZ parse in 4 KiB units; the level sets how far back
+ *  matches reach (zstd level L; blosc clevel c is L = 2c - 1): plain zstd
+ *  L 1-2 unit-local, L 3-6 + far candidates from a 2^17-entry table over
+ *  the whole chunk, L >= 7 a 2^18-entry table; blosc-zstd with bitshuffle
+ *  L >= 3 a 2^15-entry table per block.  Ratios on camera-like and dim u16
+ *  data are within ~1% (blosc-zstd) and ~7% (plain zstd L 5) of libzstd
+ *  (c-blosc clevel 5 / ZSTD_compress level 5).  With
  *  AQZ_ZSTD_HOST=1 in the environment the zstd codecs run on a host pool
  *  instead (device shuffle, D2H, the system's libzstd.so.1 at the clevel ->
  *  zstd level map of c-blosc; absent library ->

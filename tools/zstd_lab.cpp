@@ -46,7 +46,22 @@ struct Opt
     int seqtab = 0;           // 0 predefined, 1 custom per frame, 2 per block (repeat allowed)
     int hashlog = 12;
     uint32_t hufgroup = 8;    // huf=4: blocks per Huffman table group
+    // far candidates (the device's zstd_far model): a table of 2^far entries
+    // over the whole segment, most recent position per bucket with a tag,
+    // probed and then filled in batches of farbatch positions; a far match
+    // needs farmin bytes
+    int far = 0;
+    uint32_t farmin = 5;
+    uint32_t farbatch = 256;
+    uint32_t fartag = 9;
+    int farcost = 0;          // 1: the device's cost rule for far matches
+    uint32_t farcap = 1u << 30; // far match bytes measured
 };
+double g_H = 8.0; // the block's byte entropy (parse_block)
+
+// far[i] = candidate position for segment position i (-1: none), keyed on
+// the 5 bytes at i
+std::vector<int64_t> g_far;
 
 std::map<std::string, double> g_stats;
 
@@ -150,6 +165,7 @@ parse_block(const uint8_t* src, uint64_t b0, uint64_t b1, const Opt& o, const ui
         minlen = std::max<uint32_t>(o.minmatch,
                                     uint32_t(std::ceil(o.match_bits / std::max(H, 0.25))));
         minlen = std::min<uint32_t>(minlen, 64);
+        g_H = std::max(H, 0.25);
     }
     // insert history positions
     const uint64_t base = b0 >= o.hist ? b0 - o.hist : 0;
@@ -206,6 +222,12 @@ parse_block(const uint8_t* src, uint64_t b0, uint64_t b1, const Opt& o, const ui
                 }
             }
         }
+        if (o.far && !g_far.empty() && g_far[q] >= 0 && !o.farcost) {
+            const uint64_t c = uint64_t(g_far[q]);
+            const uint32_t l = std::min<uint32_t>(match_len(c, q, end), o.farcap);
+            if (l >= o.farmin && l > b.len + (b.isrep ? 1 : 0))
+                b = Best{ l, uint32_t(q - c), false };
+        }
         int64_t c = head[hsh(q)];
         for (uint32_t d = 0; d < o.chain && c >= 0; ++d) {
             if (uint64_t(c) >= lo && uint64_t(c) < q) {
@@ -219,9 +241,21 @@ parse_block(const uint8_t* src, uint64_t b0, uint64_t b1, const Opt& o, const ui
             }
             c = prev[pidx(uint64_t(c))];
         }
-        const uint32_t need = b.isrep ? 3u : minlen;
+        const uint32_t need = b.isrep ? 3u : (o.far && b.off > q - lo_of(q)) ? o.farmin : minlen;
         if (b.len < need)
             b.len = 0;
+        if (o.far && o.farcost && !g_far.empty() && g_far[q] >= 0) {
+            // the device rule: a far match pays its extra offset bits
+            const uint64_t c = uint64_t(g_far[q]);
+            const uint32_t l = std::min<uint32_t>(match_len(c, q, end), 16);
+            const uint32_t d = uint32_t(q - c);
+            const double fob = std::floor(std::log2(double(d) + 3));
+            bool take = l >= o.farmin && l * g_H >= o.match_bits + fob - 10.0;
+            if (take && b.len)
+                take = (double(l) - b.len) * g_H > fob - std::floor(std::log2(double(b.off) + 3));
+            if (take)
+                b = Best{ l, d, false };
+        }
         return b;
     };
     (void)unit0;
@@ -423,6 +457,31 @@ encode_frame(const uint8_t* src, uint64_t n, const Opt& o, FrameStats& fs)
     const uint32_t nb = uint32_t((n + o.block - 1) / o.block);
     uint32_t rep_parse[3] = { 1, 4, 8 };
     std::vector<Parsed> P(nb);
+    g_far.clear();
+    if (o.far) {
+        g_far.assign(n, -1);
+        const uint32_t FL = uint32_t(o.far), TB = o.fartag;
+        std::vector<uint32_t> tab(size_t(1) << FL, 0); // (pos + 1) << TB | tag
+        auto key = [&](uint64_t i) {
+            uint64_t k = 0;
+            std::memcpy(&k, src + i, 5);
+            return (k * 0x9E3779B97F4A7C15ull) >> (64 - FL - TB);
+        };
+        const uint64_t last = n >= 5 ? n - 5 : 0;
+        for (uint64_t b = 0; b + 5 <= n; b += o.farbatch) {
+            const uint64_t e = std::min<uint64_t>(last + 1, b + o.farbatch);
+            for (uint64_t i = b; i < e; ++i) { // probe
+                const uint64_t h = key(i);
+                const uint32_t v = tab[h >> TB];
+                if (v && (v & ((1u << TB) - 1)) == (h & ((1u << TB) - 1)))
+                    g_far[i] = int64_t(v >> TB) - 1;
+            }
+            for (uint64_t i = b; i < e; ++i) { // insert (the latest wins)
+                const uint64_t h = key(i);
+                tab[h >> TB] = uint32_t(((i + 1) << TB) | (h & ((1u << TB) - 1)));
+            }
+        }
+    }
     uint32_t fhist[256] = { 0 };
     for (uint32_t j = 0; j < nb; ++j) {
         const uint64_t b0 = uint64_t(j) * o.block, b1 = std::min<uint64_t>(n, b0 + o.block);
@@ -872,6 +931,12 @@ main(int argc, char** argv)
         else if (k == "seqtab") o.seqtab = int(x);
         else if (k == "hashlog") o.hashlog = int(x);
         else if (k == "hufgroup") o.hufgroup = uint32_t(x);
+        else if (k == "far") o.far = int(x);
+        else if (k == "farmin") o.farmin = uint32_t(x);
+        else if (k == "farbatch") o.farbatch = uint32_t(x);
+        else if (k == "fartag") o.fartag = uint32_t(x);
+        else if (k == "farcost") o.farcost = int(x);
+        else if (k == "farcap") o.farcap = uint32_t(x);
         else if (k == "kinds") kinds = v;
         else if (k == "ref") ref = int(x);
         else if (k == "chunk") chunk = uint64_t(x);
