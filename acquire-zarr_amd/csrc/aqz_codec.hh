@@ -107,17 +107,20 @@ namespace aqz {
 // the literal statistics of a shuffled blosc block change at its byte or bit
 // planes, so one table per segment fits no plane (tools/zstd_lab.cpp: c-blosc's
 // ratio within 1% with group tables, 6% short with segment tables).  A group
-// is one plane where planes are shorter than kHufGroup blocks (bitshuffle:
-// a u16 plane of a 256 KiB block is 16 KiB, 2 blocks; dim sCMOS 3.19 -> 3.40).
+// is one plane where planes are shorter than kHufGroup blocks at blosc
+// clevel >= 7 (bitshuffle: a u16 plane of a 256 KiB block is 16 KiB, 2
+// blocks; tools/zstd_lab.cpp with far candidates: dim sCMOS 3.20 -> 3.37,
+// camera 1.972 -> 1.983, c-blosc clevel 5 3.14 / 1.974) -- four times the
+// tables to build (zstd_table 0.5 -> 2.5 ms per 512 MiB layer).
 // The first Huffman block of a group carries the tree, the rest are Treeless.
 constexpr uint32_t kHufGroup = 8;
 
 // log2 of the blocks per Huffman group for a segment of seg_bytes
 inline uint32_t
-zstd_huf_group_log2(uint32_t shuffle, uint32_t typesize, uint32_t seg_bytes)
+zstd_huf_group_log2(uint32_t shuffle, uint32_t typesize, uint32_t seg_bytes, int32_t clevel)
 {
     uint32_t lg = 3; // kHufGroup
-    if (shuffle == 2 && typesize > 0) {
+    if (shuffle == 2 && typesize > 0 && clevel >= 7) {
         const uint32_t plane = seg_bytes / (8u * typesize);
         while (lg > 0 && (zstd::kBlock << lg) > plane)
             --lg;

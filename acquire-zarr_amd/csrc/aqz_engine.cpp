@@ -444,6 +444,12 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
                                                       mode == 2 ? least : greatest),
                           "hipStreamCreate");
         }
+        // the smallest levels' layers (a few chunks: their codec kernels are
+        // a handful of workgroups, pure latency) on a stream of the least
+        // priority, whose hardware queue pool is not the normal one's, so
+        // they run beside levels 0-2 instead of queueing behind them
+        hip_check(hipStreamCreateWithPriority(&comp_lo2_, hipStreamNonBlocking, least),
+                  "hipStreamCreate");
     }
     for (auto& L : lv_) {
         hip_check(hipEventCreateWithFlags(&L.ops_ev, hipEventDisableTiming),
@@ -661,7 +667,7 @@ Stage::~Stage()
     zpool_.reset();
     if (stream_)
         (void)hipStreamSynchronize(stream_);
-    for (hipStream_t s : { h2d_, comp_, comp_lo_, d2h_ })
+    for (hipStream_t s : { h2d_, comp_, comp_lo_, comp_lo2_, d2h_ })
         if (s) {
             (void)hipStreamSynchronize(s);
             (void)hipStreamDestroy(s);
@@ -752,6 +758,7 @@ Stage::synchronize()
     hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(comp_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(comp_lo_), "hipStreamSynchronize");
+    hip_check(hipStreamSynchronize(comp_lo2_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(d2h_), "hipStreamSynchronize");
     retire_consumed(true);
 }
@@ -875,6 +882,7 @@ Stage::wait_copies()
 {
     hip_check(hipStreamSynchronize(comp_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(comp_lo_), "hipStreamSynchronize");
+    hip_check(hipStreamSynchronize(comp_lo2_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(d2h_), "hipStreamSynchronize");
 }
 
@@ -1814,7 +1822,8 @@ Compressor::scratch_bytes(const Compression& c, uint64_t chunk_bytes, uint32_t t
     }
     const uint64_t nseg = n * nseg1, bps = (seg + zstd::kBlock - 1) / zstd::kBlock;
     const uint32_t gl =
-      zstd_huf_group_log2(c.codec == 2 ? uint32_t(c.shuffle) : 0u, typesize, uint32_t(seg));
+      zstd_huf_group_log2(c.codec == 2 ? uint32_t(c.shuffle) : 0u, typesize, uint32_t(seg),
+                          c.clevel);
     const uint64_t nblk = nseg * bps, ngrp = nseg * ((bps + (1u << gl) - 1) >> gl);
     b += nseg * 4; // spos
     if (c.codec == 2 && !store_only && (c.shuffle == 2 || (c.shuffle == 1 && typesize > 1)))
@@ -1895,7 +1904,7 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
         p.nseg = 1;
     }
     p.bps = (p.seg_bytes + zstd::kBlock - 1) / zstd::kBlock;
-    p.hgrp_log2 = zstd_huf_group_log2(p.shuffle, typesize_, p.seg_bytes);
+    p.hgrp_log2 = zstd_huf_group_log2(p.shuffle, typesize_, p.seg_bytes, c_.clevel);
     p.ngrp = (p.bps + (1u << p.hgrp_log2) - 1) >> p.hgrp_log2;
     // The level chooses how far back matches reach (zstd_far_slices): the
     // unit-local parse at the fast levels, the far candidates above them.
@@ -2069,7 +2078,7 @@ Stage::compress_layer_host(StageLevel& L, uint32_t slot, uint64_t layer,
                            const Compression& c)
 {
     // level 0's layers compress on comp_; the small layers of the other
-    // levels on comp_lo_, overlapping level 0's (their kernels are few
+    // levels on comp_lo_ / comp_lo2_, overlapping level 0's (their kernels are few
     // workgroups and latency-bound)
     const hipStream_t cs = comp_stream(L);
     const ZstdLib& z = ZstdLib::get();
@@ -2151,7 +2160,7 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
         throw Error(3, "level out of range");
     StageLevel& L = lv_[level];
     // level 0's layers compress on comp_; the small layers of the other
-    // levels on comp_lo_, overlapping level 0's (their kernels are few
+    // levels on comp_lo_ / comp_lo2_, overlapping level 0's (their kernels are few
     // workgroups and latency-bound)
     const hipStream_t cs = comp_stream(L);
     if (!L.ring.p)

@@ -403,10 +403,12 @@ class Stage
     // device compression of handed-off layers runs on comp_, so layer i+1
     // compresses while layer i's frames go D2H on d2h_
     hipStream_t comp_ = nullptr;
-    hipStream_t comp_lo_ = nullptr; // compression of levels >= 1
+    hipStream_t comp_lo_ = nullptr;  // compression of levels 1-2
+    hipStream_t comp_lo2_ = nullptr; // levels >= 3 (least priority: a queue pool of its own)
     hipStream_t comp_stream(const StageLevel& L) const
     {
-        return &L == &lv_[0] ? comp_ : comp_lo_;
+        const size_t k = size_t(&L - &lv_[0]);
+        return k == 0 ? comp_ : k <= 2 ? comp_lo_ : comp_lo2_;
     }
     std::unique_ptr<CopyPool> pool_;
     std::unique_ptr<TaskPool> zpool_; // host zstd workers

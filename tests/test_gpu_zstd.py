@@ -268,8 +268,8 @@ def test_device_blosc_zstd_bitshuffle_levels_differ(gpu, monkeypatch):
 
 @needs_zstd
 @pytest.mark.skipif(not os.path.exists(MODEL), reason="tests/zstd not built")
-@pytest.mark.parametrize("codec,shuffle", [(3, 0), (2, 1), (2, 2)])
-def test_device_frames_equal_serial_model(gpu, monkeypatch, codec, shuffle):
+@pytest.mark.parametrize("codec,shuffle,clevel", [(3, 0, 5), (2, 1, 5), (2, 2, 5), (2, 2, 7)])
+def test_device_frames_equal_serial_model(gpu, monkeypatch, codec, shuffle, clevel):
     """Literal-only frames: the device encoder's bytes equal the serial
     model's (same Huffman construction, same block decisions), frame by
     frame -- plain zstd per chunk, blosc-zstd per record of a shuffled
@@ -282,7 +282,7 @@ def test_device_frames_equal_serial_model(gpu, monkeypatch, codec, shuffle):
     st.append(frames)
     layer, flags = st.copy_layer(0, 0)
     bpc = st.layout(0)["bytes_per_chunk"]
-    st.compress_layer(0, 0, codec=codec, clevel=5, shuffle=shuffle)
+    st.compress_layer(0, 0, codec=codec, clevel=clevel, shuffle=shuffle)
     data, _ = st.copy_compressed(0, 0)
     ent = st.compressed_entries(0, 0)
     st.close()
@@ -310,9 +310,10 @@ def test_device_frames_equal_serial_model(gpu, monkeypatch, codec, shuffle):
             if cs == len(blk):
                 assert rec == sh, (c, j)
             else:
-                # bitshuffle: a Huffman group is one bit plane of the block
+                # bitshuffle at clevel >= 7: a Huffman group is one bit plane
                 glog2 = 3
-                while shuffle == 2 and glog2 > 0 and (8192 << glog2) > len(blk) // 16:
+                while (shuffle == 2 and clevel >= 7 and glog2 > 0
+                       and (8192 << glog2) > len(blk) // 16):
                     glog2 -= 1
                 assert rec == model_frame(sh, glog2=glog2), (c, j)
             checked += 1
