@@ -1076,8 +1076,8 @@ zstd_parse(const ZstdParams p)
                     }
                     if constexpr (FAR) {
                         const uint32_t sp = ubase + (qq - H);
-                        const uint32_t fv = farp[sp];
-                        if (fv != 0 && fv - 1 < sp) {
+                        const uint32_t fv = (p.dbg & 2u) ? 0u : farp[sp];
+                        if (fv != 0 && fv - 1 < sp && !(p.dbg & 1u)) {
                             // bytes of the candidate from global memory: one
                             // 8-B load holds its first 8 - (fp & 3) >= 5;
                             // the next 8 only when those all match

@@ -1922,6 +1922,8 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
         p.fit = uint32_t(std::atoi(e));
     p.src = chunks;
     p.src_pitch = pitch;
+    if (const char* e = std::getenv("AQZ_ZSTD_DBG")) // tuning knob (A/B)
+        p.dbg = uint32_t(std::atoi(e));
     const bool shuffle = blosc && !store_only_ &&
                          (c_.shuffle == 2 || (c_.shuffle == 1 && typesize_ > 1));
     if (shuffle) {

@@ -1122,9 +1122,11 @@ fused_pyramid_strip(const FusedParams p)
             t2.nz |= any_nonzero<T, QV>(q2[i]);
         }
     }
-    flush_tile_flag(t0);
-    flush_tile_flag(t1);
-    flush_tile_flag(t2);
+    if (!(p.knobs & 32u)) { // tuning knob 32: no has_data stores (A/B only)
+        flush_tile_flag(t0);
+        flush_tile_flag(t1);
+        flush_tile_flag(t2);
+    }
     if (nf < 3 || (p.knobs & 8u))
         return;
 
