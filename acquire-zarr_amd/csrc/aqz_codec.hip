@@ -1107,7 +1107,8 @@ zstd_parse(const ZstdParams p)
                                 flen += x2 ? uint32_t(__builtin_ctzll(x2)) >> 3 : 8u;
                             }
                             flen = min(flen, min(matchlimit - qq, 16u));
-                            if (flen >= kFarMin && flen > mlen[w] && sp - fp <= kZOffMax) {
+                            if (flen >= kFarMin && flen > mlen[w] && sp - fp <= kZOffMax &&
+                                !(p.dbg & 4u)) {
                                 cand[w] = sp - fp;
                                 mlen[w] = flen;
                             }
