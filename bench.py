@@ -47,7 +47,7 @@ CONFIGS = {
                         "256x256 chunks (t-chunk 64), mean, level-0 split + pyramid + "
                         "tile split of all levels, device-resident",
                dims=[(TIME, 0, 64, 1), (SPACE, 2048, 256, 1), (SPACE, 2048, 256, 1)],
-               dtype=U16, method=MEAN, force_levels=5, batch=128, ring=256),
+               dtype=U16, method=MEAN, force_levels=5, batch=256, ring=256),
     # same, reference level rule (4 levels)
     "c2-ref4": dict(workload="uint16 2048x2048 frames, 4-level pyramid (reference rule "
                              "at 256-px chunks), t-chunk 64, mean, device-resident",
@@ -72,6 +72,15 @@ CONFIGS = {
                dims=[(TIME, 0, 4, 1), (SPACE, 8192, 128, 1), (SPACE, 8192, 128, 1)],
                dtype=F32, method=MEAN, force_levels=0, batch=4, ring=12),
 }
+
+
+def layer_slots_for(cfg, B):
+    """Chunk-layer ring slots of the device-resident run: a 2-D launch of B
+    frames spans B / t-chunk layers of every level, which the ring must hold
+    (at least 2)."""
+    if len(cfg["dims"]) != 3:
+        return 2
+    return max(2, -(-B // cfg["dims"][0][2]))
 
 
 def hbm_probe(aqz, device):
@@ -115,7 +124,7 @@ def fill_ring(torch, ring, dtype, seed):
         ring.view(torch.float32).uniform_(0.0, 65535.0, generator=g)
 
 
-def pmc_traffic(config, pyramid_only, kernel):
+def pmc_traffic(config, pyramid_only, kernel, frames):
     """Per-launch HBM bytes of the dominant kernel from the newest committed
     rocprofv3 PMC summary for this configuration (tools/profile.sh ->
     tools/pmc_summary.py -> profiles/<round>_<config>_pmc.json: FETCH_SIZE x2
@@ -128,7 +137,13 @@ def pmc_traffic(config, pyramid_only, kernel):
     for f in reversed(files):
         d = json.load(open(f))
         if d.get("config") == name and kernel and kernel in d.get("kernel", ""):
-            return d["traffic_bytes_per_launch"], os.path.relpath(f, REPO)
+            # (traffic is linear in the frames of a launch: a profile of
+            # another launch size is scaled to this one)
+            t = d["traffic_bytes_per_launch"]
+            fpl = d.get("frames_per_launch")
+            if fpl and fpl != frames:
+                t = int(round(t * frames / fpl))
+            return t, os.path.relpath(f, REPO)
     return None, None
 
 
@@ -217,7 +232,10 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
     2-batch ring of host frames; layers land in a per-level ring of pinned
     buffers (no consumer: the sink is out of scope).  Timed from the first
     append to the last hand-off copy."""
-    dt, B, bpp = cfg["dtype"], cfg["batch"], BPP[cfg["dtype"]]
+    # (the device-resident launch size of C2 is 256 frames; the host path
+    # keeps 128-frame batches: a 2-batch pinned source ring of 2 GiB)
+    dt, bpp = cfg["dtype"], BPP[cfg["dtype"]]
+    B = args.batch or min(cfg["batch"], 128)
     st = aqz.Stage(cfg["dims"], dt, cfg["method"], force_levels=cfg["force_levels"],
                    max_batch_frames=B, layer_slots=2, device=dev.index)
     L = st.n_levels()
@@ -550,7 +568,8 @@ def main():
     def run(pyramid_only, steps, warmup):
         """Time `steps` launches of B frames (after `warmup`) between
         barrier + device sync on both sides; max over ranks."""
-        kw = dict(force_levels=cfg["force_levels"], max_batch_frames=B, layer_slots=2,
+        kw = dict(force_levels=cfg["force_levels"], max_batch_frames=B,
+                  layer_slots=layer_slots_for(cfg, B),
                   skip_level0_split=pyramid_only, **PLACEMENT)
         if args.xy:
             nd = len(cfg["dims"])
@@ -645,7 +664,7 @@ def main():
     sizes, elapsed, value = main_run["sizes"], main_run["elapsed"], main_run["value"]
     kernel, avg_ms, achieved = main_run["kernel"], main_run["avg_ms"], main_run["achieved"]
     alg_per_launch = main_run["alg"]
-    traffic, traffic_src = pmc_traffic(args.config, args.pyramid_only, kernel)
+    traffic, traffic_src = pmc_traffic(args.config, args.pyramid_only, kernel, B)
 
     result = {
         "metric": f"input GB/s, device-resident multiscale downsample, {DTYPE_WORDS[dt]} "

@@ -55,7 +55,8 @@ def test_bench_c2_configuration_exact(gpu, cfg):
     c = bench.CONFIGS[cfg]
     dims, B = c["dims"], c["batch"]
     h, w = dims[-2][1], dims[-1][1]
-    kw = dict(force_levels=c["force_levels"], max_batch_frames=B, layer_slots=2,
+    slots = bench.layer_slots_for(c, B)
+    kw = dict(force_levels=c["force_levels"], max_batch_frames=B, layer_slots=slots,
               **bench.PLACEMENT)
     est = gpu.estimate_memory(dims, U16, MEAN, **kw)
     st = gpu.Stage(dims, U16, MEAN, **kw)
@@ -70,7 +71,7 @@ def test_bench_c2_configuration_exact(gpu, cfg):
     assert pl["peak_device_bytes"] <= est["device_bytes"]
     assert st.memory_usage()["device_bytes"] <= gpu.estimate_memory(
         dims, U16, MEAN, force_levels=c["force_levels"], max_batch_frames=B,
-        layer_slots=2)["device_bytes"]
+        layer_slots=slots)["device_bytes"]
     ldims = [st.level_dims(l) for l in range(L)]
     assert [d[-1][1] for d in ldims] == [2048, 1024, 512, 256, 128][:L]
     assert all(d[-1][2] == 256 and d[-2][2] == 256 for d in ldims)

@@ -30,6 +30,7 @@ def per_kernel(path):
 
 def main():
     d, cfg, tag = sys.argv[1], sys.argv[2], sys.argv[3]
+    fpl = int(sys.argv[4]) if len(sys.argv) > 4 else None # frames per launch
     stats = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))))
     ours = [s for s in stats if "aqz::" in s["Name"]]
     dom = max(ours, key=lambda s: float(s["TotalDurationNs"]))
@@ -51,6 +52,19 @@ def main():
         "correction": "FETCH_SIZE x2 (gfx950 reports half of a 16-B/lane streaming read); "
                       "KiB -> bytes",
     }
+    if fpl:
+        res["frames_per_launch"] = fpl
+    # the timed launches alone: the stats average also holds the stage's
+    # creation-time placement calibration (up to 10 launches per candidate)
+    tr = os.path.join(d, "trace", "run_kernel_trace.csv")
+    if os.path.exists(tr):
+        steps = int(os.environ.get("STEPS", "200"))
+        rows = sorted((r for r in csv.DictReader(open(tr)) if r["Kernel_Name"] == name),
+                      key=lambda r: int(r["Start_Timestamp"]))
+        dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows][-steps:]
+        if dur:
+            res["steady_avg_duration_ns"] = statistics.mean(dur)
+            res["steady_launches"] = len(dur)
     sq = os.path.join(d, "pmc_sq", "run_counter_collection.csv")
     if os.path.exists(sq):
         s = per_kernel(sq).get(name, {})
