@@ -176,6 +176,7 @@ struct ZstdParams
     uint32_t* far;
     uint32_t far_tb;        // tag bits of a far table entry (32 - position bits)
     uint32_t far_slices;    // hash slices (workgroups) per segment: 1, 2, 4 or 8
+    uint32_t far_log;       // log2 of a slice's table entries (<= kFarLog)
     uint32_t dbg;           // A/B switches (AQZ_ZSTD_DBG; 0 = shipped)
     const uint32_t* flags;  // has_data words (nullptr: every chunk has data)
     uint32_t tag;
@@ -231,17 +232,17 @@ constexpr uint32_t kZHist2 = 28 * 1024;
 constexpr uint32_t kFarLog = 15;
 constexpr uint32_t kFarMin = 5;
 constexpr uint32_t kZOffMax = (1u << 24) - 4; // largest match distance (aqz_codec.hip zseq_codes)
-// tag bits for a segment of seg_bytes split into `slices` hash slices (0:
-// segments too large for the pass)
+// tag bits for a segment of seg_bytes split into `slices` hash slices of
+// 2^far_log entries (0: segments too large for the pass)
 inline uint32_t
-zstd_far_tag_bits(uint32_t seg_bytes, uint32_t slices)
+zstd_far_tag_bits(uint32_t seg_bytes, uint32_t slices, uint32_t far_log = kFarLog)
 {
     uint32_t pb = 0, sb = 0;
     while (pb < 32 && (uint64_t(1) << pb) <= seg_bytes) // positions + 1 <= seg_bytes
         ++pb;
     while ((1u << sb) < slices)
         ++sb;
-    const uint32_t room = 32 - sb - kFarLog; // hash bits left for the tag
+    const uint32_t room = 32 - sb - far_log; // hash bits left for the tag
     const uint32_t tb = 32 - pb < room ? 32 - pb : room;
     return tb >= 6 ? tb : 0;
 }

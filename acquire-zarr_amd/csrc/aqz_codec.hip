@@ -809,7 +809,7 @@ far_hash(uint32_t lo, uint32_t hi)
 __global__ __launch_bounds__(kFarThreads) void
 zstd_far(const ZstdParams p)
 {
-    __shared__ uint32_t T[1u << kFarLog];
+    extern __shared__ __attribute__((aligned(16))) uint32_t T[]; // 2^far_log entries
     const uint32_t S = p.far_slices, nb = gridDim.x, b = blockIdx.x;
     const uint32_t grp = 8u * S, full = nb - nb % grp;
     uint32_t seg, slice;
@@ -827,10 +827,10 @@ zstd_far(const ZstdParams p)
     const uint32_t len = uint32_t(min(uint64_t(p.seg_bytes), uint64_t(p.nbytes) - s0));
     const uint8_t* src = p.src + c * p.src_pitch + s0;
     uint32_t* far = p.far + uint64_t(seg) * p.seg_bytes;
-    const uint32_t t = threadIdx.x, TB = p.far_tb, tmask = (1u << TB) - 1u;
+    const uint32_t t = threadIdx.x, TB = p.far_tb, tmask = (1u << TB) - 1u, FL = p.far_log;
     const uint32_t sbits = 31u - uint32_t(__builtin_clz(S)); // log2 of the slices
-    const uint32_t bshift = 32u - sbits - kFarLog;
-    for (uint32_t i = t; i < (1u << kFarLog); i += kFarThreads)
+    const uint32_t bshift = 32u - sbits - FL;
+    for (uint32_t i = t; i < (1u << FL); i += kFarThreads)
         T[i] = 0;
     // positions with fewer than 5 bytes after them have no key
     const uint32_t nkey = len >= 5 ? len - 4 : 0;
@@ -866,7 +866,7 @@ zstd_far(const ZstdParams p)
         for (uint32_t k = 0; k < 4; ++k) {
             const uint32_t i = i0 + k;
             if (i < nkey && (sbits == 0 || (h[k] >> (32u - sbits)) == slice)) {
-                const uint32_t e = T[(h[k] >> bshift) & ((1u << kFarLog) - 1u)];
+                const uint32_t e = T[(h[k] >> bshift) & ((1u << FL) - 1u)];
                 far[i] = (e != 0 && (e & tmask) == (h[k] & tmask)) ? (e >> TB) : 0u;
             }
         }
@@ -876,7 +876,7 @@ zstd_far(const ZstdParams p)
         for (uint32_t k = 0; k < 4; ++k) {
             const uint32_t i = i0 + k;
             if (i < nkey && (sbits == 0 || (h[k] >> (32u - sbits)) == slice))
-                atomicMax(&T[(h[k] >> bshift) & ((1u << kFarLog) - 1u)],
+                atomicMax(&T[(h[k] >> bshift) & ((1u << FL) - 1u)],
                           ((i + 1) << TB) | (h[k] & tmask));
         }
         __syncthreads();
@@ -2107,12 +2107,18 @@ launch_zstd(const ZstdParams& p, hipStream_t stream)
             if (p.far) {
                 const uint32_t S = p.far_slices;
                 if (!(S == 1 || S == 2 || S == 4 || S == 8) || p.far_tb < 6 ||
-                    p.far_tb + kFarLog + (S == 8 ? 3 : S == 4 ? 2 : S == 2 ? 1 : 0) > 32 ||
+                    p.far_log < 10 || p.far_log > kFarLog ||
+                    p.far_tb + p.far_log + (S == 8 ? 3 : S == 4 ? 2 : S == 2 ? 1 : 0) > 32 ||
                     (reinterpret_cast<uintptr_t>(p.src) & 3u) || (p.src_pitch & 3u) ||
                     (p.seg_bytes & 3u))
                     return hipErrorInvalidValue;
+                static const hipError_t attr = hipFuncSetAttribute(
+                  reinterpret_cast<const void*>(zstd_far),
+                  hipFuncAttributeMaxDynamicSharedMemorySize, int(4u << kFarLog));
+                if (attr != hipSuccess)
+                    return attr;
                 hipLaunchKernelGGL(zstd_far, dim3(uint32_t(nseg * p.far_slices)),
-                                   dim3(kFarThreads), 0, stream, p);
+                                   dim3(kFarThreads), size_t(4) << p.far_log, stream, p);
             }
             if (p.phist == 0 && !p.far)
                 hipLaunchKernelGGL((zstd_parse<0, kLz4HashLog>), gd, dim3(64), 0, stream, p);

@@ -1951,7 +1951,11 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
         // history pays: zstd_far_slices (the level), 4-byte aligned segments;
         // AQZ_ZSTD_FAR=0 off
         p.far_slices = zstd_far_slices(c_, typesize_);
-        p.far_tb = p.far_slices ? zstd_far_tag_bits(p.seg_bytes, p.far_slices) : 0;
+        // a blosc block (256 KiB) needs no more than 2^13 entries (bitshuffle
+        // camera 1.972 -> 1.969, tools/zstd_lab.cpp far=13), a quarter of the
+        // LDS: twice the workgroups per CU
+        p.far_log = blosc ? 13u : kFarLog;
+        p.far_tb = p.far_slices ? zstd_far_tag_bits(p.seg_bytes, p.far_slices, p.far_log) : 0;
         bool far = p.match && p.far_tb != 0 && (reinterpret_cast<uintptr_t>(p.src) & 3u) == 0 &&
                    (p.src_pitch & 3u) == 0 && (p.seg_bytes & 3u) == 0;
         if (const char* e = std::getenv("AQZ_ZSTD_FAR")) // tuning knob
