@@ -52,11 +52,11 @@ CONFIGS = {
     "c2-ref4": dict(workload="uint16 2048x2048 frames, 4-level pyramid (reference rule "
                              "at 256-px chunks), t-chunk 64, mean, device-resident",
                     dims=[(TIME, 0, 64, 1), (SPACE, 2048, 256, 1), (SPACE, 2048, 256, 1)],
-                    dtype=U16, method=MEAN, force_levels=0, batch=64, ring=256),
+                    dtype=U16, method=MEAN, force_levels=0, batch=128, ring=256),
     "c3": dict(workload="uint8 4096x4096 frames, 6-level pyramid, 128x128 chunks, mean, "
                         "device-resident",
                dims=[(TIME, 0, 32, 1), (SPACE, 4096, 128, 1), (SPACE, 4096, 128, 1)],
-               dtype=U8, method=MEAN, force_levels=0, batch=32, ring=160),
+               dtype=U8, method=MEAN, force_levels=0, batch=64, ring=160),
     # BASELINE configs[3]: a 256-plane volume, 2x2x2 pyramid (z 256->128->
     # 64->64, xy 2048->1024->512->256).  With --gpus N rank r owns z slab
     # [lo, hi) of every volume of the stream (aqz_stage_options z_slab_*,
@@ -70,7 +70,7 @@ CONFIGS = {
     "c5": dict(workload="float32 8192x8192 frames, 7-level pyramid, 128x128 chunks, mean, "
                         "device-resident (one camera stream per GPU)",
                dims=[(TIME, 0, 4, 1), (SPACE, 8192, 128, 1), (SPACE, 8192, 128, 1)],
-               dtype=F32, method=MEAN, force_levels=0, batch=4, ring=12),
+               dtype=F32, method=MEAN, force_levels=0, batch=8, ring=12),
 }
 
 
