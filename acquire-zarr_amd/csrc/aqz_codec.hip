@@ -1123,7 +1123,21 @@ zstd_parse(const ZstdParams p)
 #pragma unroll
             for (uint32_t w = 0; w < kWin; ++w) {
                 const uint32_t wb = base + 64 * w;
-                while (p0 < wb + 64 && !full) {
+                // FAR (matches at most positions): the greedy walk's next
+                // step from each lane's match, the first match at or after
+                // its end (64: none in this window; 65: the match reached
+                // kLenCap and may run longer)
+                const uint32_t ml = mlen[w];
+                uint32_t jmp = 64u;
+                if (ml == kLenCap) {
+                    jmp = 65u;
+                } else if (ml != 0 && lane + ml < 64u) {
+                    const uint64_t nx = M[w] & (~0ull << (lane + ml));
+                    jmp = nx ? uint32_t(__ffsll(static_cast<long long>(nx))) - 1 : 64u;
+                }
+                const uint32_t end = wb + lane + ml; // this lane's match end
+                while (!FAR && p0 < wb + 64 && !full) {
+                    // few matches (no far candidates): one step per match
                     const uint32_t sh = p0 > wb ? p0 - wb : 0;
                     const uint64_t mm = M[w] & (~0ull << sh);
                     if (mm == 0)
@@ -1132,7 +1146,7 @@ zstd_parse(const ZstdParams p)
                     const uint32_t qq = wb + i;
                     const uint32_t dist = rdlane(cand[w], i);
                     uint32_t len = rdlane(mlen[w], i);
-                    if (len == kLenCap) { // a local match (far ones are <= 16 bytes)
+                    if (len == kLenCap) {
                         const uint32_t cc = qq - dist;
                         for (;;) {
                             const uint32_t a = qq + len + lane;
@@ -1154,9 +1168,74 @@ zstd_parse(const ZstdParams p)
                     anchor = p0;
                     any = true;
                 }
+                while (FAR && p0 < wb + 64 && !full) {
+                    const uint32_t sh = p0 > wb ? p0 - wb : 0;
+                    const uint64_t mm = M[w] & (~0ull << sh);
+                    if (mm == 0)
+                        break;
+                    // the chain of greedy matches from the first: one
+                    // readlane per match; the sequences are then packed and
+                    // stored by their own lanes at once
+                    uint32_t s = uint32_t(__ffsll(static_cast<long long>(mm))) - 1;
+                    const uint32_t room = kZSubSeq - nseq;
+                    uint64_t sel = 0;
+                    uint32_t cnt = 0;
+                    bool cap = false;
+                    for (;;) {
+                        const uint32_t j = rdlane(jmp, s);
+                        if (j == 65u) {
+                            cap = true;
+                            break;
+                        }
+                        sel |= 1ull << s;
+                        if (++cnt == room || j >= 64u)
+                            break;
+                        s = j;
+                    }
+                    if (sel) {
+                        const uint64_t below = sel & ((1ull << lane) - 1ull);
+                        const int prev = below ? 63 - __clzll(static_cast<long long>(below)) : -1;
+                        const uint32_t pend = __shfl(end, prev < 0 ? 0 : prev);
+                        if ((sel >> lane) & 1ull)
+                            sseq[nseq + uint32_t(__popcll(below))] = zstd::pack_seq(
+                              wb + lane - (prev < 0 ? anchor : pend), ml, cand[w]);
+                        nseq += cnt;
+                        p0 = rdlane(end, 63u - uint32_t(__clzll(static_cast<long long>(sel))));
+                        anchor = p0;
+                        full = nseq == kZSubSeq;
+                        any = true;
+                    }
+                    if (cap && !full) {
+                        // a local match that reached kLenCap: measured on,
+                        // 64 bytes per ballot
+                        const uint32_t qq = wb + s;
+                        const uint32_t dist = rdlane(cand[w], s);
+                        const uint32_t cc = qq - dist;
+                        uint32_t len = kLenCap;
+                        for (;;) {
+                            const uint32_t a = qq + len + lane;
+                            const bool eq = a < matchlimit && sb[a] == sb[cc + len + lane];
+                            const uint64_t miss = __ballot(!eq);
+                            if (miss == 0) {
+                                len += 64;
+                                continue;
+                            }
+                            len += uint32_t(__ffsll(static_cast<long long>(miss))) - 1;
+                            break;
+                        }
+                        if (lane == 0)
+                            sseq[nseq] = zstd::pack_seq(qq - anchor, len, dist);
+                        ++nseq;
+                        full = nseq == kZSubSeq;
+                        p0 = qq + len;
+                        anchor = p0;
+                        any = true;
+                    }
+                }
             }
             misses = any ? 0 : misses + 1;
-            const uint32_t skip = misses > 1 ? (misses - 1) * 64 * kWin : 0;
+            const uint32_t skip =
+              misses > 1 && !(p.dbg & 8u) ? (misses - 1) * 64 * kWin : 0;
             base = max(base + 64 * kWin + skip, p0 & ~63u);
         }
     }
@@ -1196,11 +1275,12 @@ zstd_parse(const ZstdParams p)
         for (uint32_t j = 0; j < m; ++j) {
             const zstd::Seq v =
               zstd::unpack_seq(uint64_t(rdlane(mlo, j)) | uint64_t(rdlane(mhi, j)) << 32);
-            for (uint32_t i = lane; i < v.lit; i += 64) {
-                const uint8_t x = sb[pos + i];
-                lo[at + i] = x;
-                atomicAdd(&lh[x], 1u);
-            }
+            if (!(p.dbg & 16u)) // A/B: 16 = no literal gather (frames invalid)
+                for (uint32_t i = lane; i < v.lit; i += 64) {
+                    const uint8_t x = sb[pos + i];
+                    lo[at + i] = x;
+                    atomicAdd(&lh[x], 1u);
+                }
             at += v.lit;
             pos += v.lit + v.len;
         }
