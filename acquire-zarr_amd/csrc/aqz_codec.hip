@@ -1425,6 +1425,67 @@ zseq_codes(const zstd::Seq& v)
            uint64_t(v.len - zstd::ml_base(mlc)) << 30 | uint64_t(ofv - (1u << ofc)) << 41;
 }
 
+// zstd::BitW's bitstream with 4-byte stores: whole bytes until the output
+// is 4-byte aligned, then a dword per 32 bits (a lane per block writes its
+// own stream, so every store instruction touches 64 lines: 4x fewer of them)
+struct BitW32
+{
+    uint8_t* p;
+    uint32_t cap, pos, n;
+    uint64_t acc;
+    bool ovf;
+    __device__ void init(uint8_t* dst, uint32_t c)
+    {
+        p = dst;
+        cap = c;
+        pos = 0;
+        n = 0;
+        acc = 0;
+        ovf = false;
+    }
+    __device__ void byte()
+    {
+        if (pos < cap)
+            p[pos] = uint8_t(acc);
+        else
+            ovf = true;
+        ++pos;
+        acc >>= 8;
+        n -= 8;
+    }
+    __device__ void add(uint64_t v, uint32_t nb) // nb <= 32
+    {
+        acc |= (v & ((1ull << nb) - 1ull)) << n;
+        n += nb;
+        if (n < 32)
+            return;
+        while (n >= 8 && ((reinterpret_cast<uintptr_t>(p) + pos) & 3u))
+            byte();
+        if (n >= 32) {
+            if (pos + 4 <= cap)
+                *reinterpret_cast<uint32_t*>(p + pos) = uint32_t(acc);
+            else
+                ovf = true;
+            pos += 4;
+            acc >>= 32;
+            n -= 32;
+        }
+    }
+    // end mark (one 1 bit), then the whole bytes and the padded last one
+    __device__ uint32_t close()
+    {
+        add(1, 1);
+        while (n >= 8)
+            byte();
+        if (n) {
+            n = 8;
+            byte();
+            n = 0;
+        }
+        return ovf ? 0 : pos;
+    }
+};
+
 // zstd::encode_sequences over pre-coded sequences (same bitstream), with
 // the predefined tables (LDS) or a segment's fitted ones (global)
 template<class TL, class TO, class TM>
@@ -1438,7 +1499,7 @@ zseq_encode(const TL& tll, const TO& tof, const TM& tml, const uint64_t* sv, uin
         const TO& of;
         const TM& ml;
     } t{ tll, tof, tml };
-    zstd::BitW w;
+    BitW32 w;
     w.init(out, cap);
     uint64_t v = sv[n - 1];
     uint32_t llc = uint32_t(v & 63u), mlc = uint32_t((v >> 6) & 63u), ofc = uint32_t((v >> 12) & 31u);

@@ -199,18 +199,18 @@ fse_init(const FseTable<LOG>& ct, uint32_t s)
     return ct.st[int32_t(v >> nbo) + ct.dfs[s]];
 }
 
-template<uint32_t LOG>
+template<uint32_t LOG, class W>
 __host__ __device__ inline void
-fse_enc(BitW& w, uint32_t& state, const FseTable<LOG>& ct, uint32_t s)
+fse_enc(W& w, uint32_t& state, const FseTable<LOG>& ct, uint32_t s)
 {
     const uint32_t nbo = (state + ct.dnb[s]) >> 16;
     w.add(state, nbo);
     state = ct.st[int32_t(state >> nbo) + ct.dfs[s]];
 }
 
-template<uint32_t LOG>
+template<uint32_t LOG, class W>
 __host__ __device__ inline void
-fse_flush(BitW& w, uint32_t state, const FseTable<LOG>& ct)
+fse_flush(W& w, uint32_t state, const FseTable<LOG>& ct)
 {
     w.add(state, ct.al);
 }
