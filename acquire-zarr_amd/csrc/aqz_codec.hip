@@ -1792,8 +1792,10 @@ zstd_encode(const ZstdParams p)
 // beat the predefined distributions.  The serial part runs on lane 0.
 __device__ bool
 zfit(const uint32_t* cnt, uint32_t maxlog, int16_t* norm, uint32_t& al_out,
-     uint32_t& maxsym_out, float& bits_out)
+     uint32_t& maxsym_out, float& bits_out, int16_t* nm, uint8_t* tmp)
 {
+    // nm [kFseMaxSym] and tmp [128]: LDS workspaces of the caller (private
+    // arrays indexed at run time would live in scratch memory)
     uint32_t ms = 0, nz = 0;
     uint64_t total = 0;
     for (uint32_t s = 0; s < 64; ++s)
@@ -1805,8 +1807,6 @@ zfit(const uint32_t* cnt, uint32_t maxlog, int16_t* norm, uint32_t& al_out,
     if (nz < 2 || ms >= zstd::kFseMaxSym)
         return false;
     float best = 3.0e38f;
-    int16_t nm[zstd::kFseMaxSym];
-    uint8_t tmp[128];
     for (uint32_t al = 5; al <= maxlog; ++al) {
         const int ts = 1 << al;
         int used = 0, big = -1;
@@ -1831,7 +1831,7 @@ zfit(const uint32_t* cnt, uint32_t maxlog, int16_t* norm, uint32_t& al_out,
         if (nm[big] < 0 || fix < 1)
             continue;
         nm[big] = int16_t(fix);
-        const uint32_t d = zstd::fse_write_ncount(tmp, sizeof(tmp), nm, ms, al);
+        const uint32_t d = zstd::fse_write_ncount(tmp, 128, nm, ms, al);
         if (!d)
             continue;
         float b = 8.0f * float(d);
@@ -1868,7 +1868,16 @@ zstd_seqtab(const ZstdParams p)
 {
     __shared__ uint32_t cnt[3][64];
     __shared__ int16_t norm[3][zstd::kFseMaxSym];
-    __shared__ zstd::FseBuildWorkT<zstd::kSeqMaxLog> bw;
+    __shared__ int16_t nmw[3][zstd::kFseMaxSym];
+    __shared__ uint8_t tmpw[3][128];
+    __shared__ zstd::FseBuildWorkT<zstd::kSeqMaxLog> bw[3];
+    // the tables and their descriptions are built in LDS, one lane per table
+    // (LL, OF, ML), then copied out by the wave
+    __shared__ zstd::FseTable<zstd::kSeqMaxLog> tt[3];
+    __shared__ uint8_t desc[sizeof(ZstdSeqSeg::desc)];
+    __shared__ uint32_t al[3], ms[3], okf[3], okb[3];
+    __shared__ float fb[3], pb[3];
+    __shared__ uint32_t res_mode, res_n;
     const uint32_t s = blockIdx.x, t = threadIdx.x;
     ZstdSeqSeg& Q = p.sqt[s];
     if (zchunk_skip(p, s / p.nseg)) {
@@ -1879,36 +1888,55 @@ zstd_seqtab(const ZstdParams p)
     for (uint32_t f = 0; f < 3; ++f)
         cnt[f][t] = p.scount[uint64_t(s) * 192 + f * 64 + t];
     __syncthreads();
-    if (t != 0)
-        return;
-    uint32_t al[3] = { 0, 0, 0 }, ms[3] = { 0, 0, 0 };
-    float fb[3];
-    const uint32_t maxlog[3] = { 9, 8, 9 };
-    bool ok = true;
-    for (uint32_t f = 0; f < 3 && ok; ++f)
-        ok = zfit(cnt[f], maxlog[f], norm[f], al[f], ms[f], fb[f]);
-    Q.mode = 0;
-    Q.desc_n = 0;
-    if (!ok || !p.fit)
-        return;
-    const float pre = zpredef_bits(cnt[0], zstd::ll_default_norm(), 35, 6) +
-                      zpredef_bits(cnt[1], zstd::of_default_norm(), 28, 5) +
-                      zpredef_bits(cnt[2], zstd::ml_default_norm(), 52, 6);
-    if (fb[0] + fb[1] + fb[2] >= pre)
-        return;
-    uint32_t n = 0;
-    for (uint32_t f = 0; f < 3 && ok; ++f) {
-        const uint32_t d = zstd::fse_write_ncount(Q.desc + n, sizeof(Q.desc) - n, norm[f],
-                                                  ms[f], al[f]);
-        ok = d != 0;
-        n += d;
+    if (t < 3) {
+        const uint32_t maxlog[3] = { 9, 8, 9 };
+        uint32_t a = 0, m = 0;
+        float b = 0.f;
+        okf[t] = zfit(cnt[t], maxlog[t], norm[t], a, m, b, nmw[t], tmpw[t]) ? 1u : 0u;
+        al[t] = a;
+        ms[t] = m;
+        fb[t] = b;
+        pb[t] = t == 0   ? zpredef_bits(cnt[0], zstd::ll_default_norm(), 35, 6)
+                : t == 1 ? zpredef_bits(cnt[1], zstd::of_default_norm(), 28, 5)
+                         : zpredef_bits(cnt[2], zstd::ml_default_norm(), 52, 6);
     }
-    ok = ok && zstd::fse_build(Q.ll, norm[0], ms[0], al[0], bw) &&
-         zstd::fse_build(Q.of, norm[1], ms[1], al[1], bw) &&
-         zstd::fse_build(Q.ml, norm[2], ms[2], al[2], bw);
-    if (ok) {
-        Q.desc_n = n;
-        Q.mode = 2;
+    __syncthreads();
+    const bool want = okf[0] && okf[1] && okf[2] && p.fit &&
+                      fb[0] + fb[1] + fb[2] < pb[0] + pb[1] + pb[2];
+    if (t == 0) {
+        res_mode = 0;
+        res_n = 0;
+        if (want) {
+            uint32_t n = 0;
+            bool ok = true;
+            for (uint32_t f = 0; f < 3 && ok; ++f) {
+                const uint32_t d = zstd::fse_write_ncount(desc + n, sizeof(desc) - n,
+                                                          norm[f], ms[f], al[f]);
+                ok = d != 0;
+                n += d;
+            }
+            if (ok) {
+                res_n = n;
+                res_mode = 2;
+            }
+        }
+    }
+    if (t < 3)
+        okb[t] = want && zstd::fse_build(tt[t], norm[t], ms[t], al[t], bw[t]) ? 1u : 0u;
+    __syncthreads();
+    const bool fitted = res_mode == 2 && okb[0] && okb[1] && okb[2];
+    if (fitted) {
+        for (uint32_t i = t; i < sizeof(tt[0]) / 4; i += 64) {
+            reinterpret_cast<uint32_t*>(&Q.ll)[i] = reinterpret_cast<const uint32_t*>(&tt[0])[i];
+            reinterpret_cast<uint32_t*>(&Q.of)[i] = reinterpret_cast<const uint32_t*>(&tt[1])[i];
+            reinterpret_cast<uint32_t*>(&Q.ml)[i] = reinterpret_cast<const uint32_t*>(&tt[2])[i];
+        }
+        for (uint32_t i = t; i < res_n; i += 64)
+            Q.desc[i] = desc[i];
+    }
+    if (t == 0) {
+        Q.desc_n = fitted ? res_n : 0;
+        Q.mode = fitted ? 2u : 0u;
     }
 }
 
