@@ -1353,6 +1353,7 @@ zstd_table(const ZstdParams p)
     if (t == 0)
         npresent = 0;
     __syncthreads();
+    uint32_t mx = 0, tot = 0;
     for (uint32_t k = t; k < 256; k += 64) {
         uint32_t a = 0;
         for (uint32_t b = b0; b < b1; ++b)
@@ -1363,8 +1364,27 @@ zstd_table(const ZstdParams p)
         code[k] = 0;
         if (a)
             atomicAdd(&npresent, 1u);
+        mx = max(mx, a);
+        tot += a;
+    }
+    for (int d = 32; d > 0; d >>= 1) {
+        mx = max(mx, uint32_t(__shfl_xor(int(mx), d)));
+        tot += uint32_t(__shfl_xor(int(tot), d));
     }
     __syncthreads();
+    if (zstd::huf_flat(npresent, mx, tot)) {
+        // raw literals: no sort, no construction
+        ZstdSegTable& T0 = p.tab[gi];
+        for (uint32_t k = t; k < 256; k += 64) {
+            T0.code[k] = 0;
+            T0.len[k] = 0;
+        }
+        if (t == 0) {
+            T0.mode = 0;
+            T0.tree_n = 0;
+        }
+        return;
+    }
     // bitonic sort of (count, symbol), 64 lanes x 2 pairs
     for (uint32_t size = 2; size <= 256; size <<= 1)
         for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {

@@ -348,6 +348,15 @@ huf_lengths(const uint32_t* cnt_in, uint8_t* len, uint32_t maxbits)
     return n;
 }
 
+// A literal histogram too flat for Huffman to pay: every byte value present
+// and none above 5/4 of the mean (entropy >= 7.68 bits; random bytes, the low
+// bit planes of noisy data).  Literals stay raw; the encoders skip the table.
+__host__ __device__ inline bool
+huf_flat(uint32_t present, uint32_t maxcnt, uint64_t total)
+{
+    return present == 256 && uint64_t(maxcnt) * 1024u < total * 5u;
+}
+
 // Workspace of the tree description (LDS in the kernel).
 struct TreeWork
 {

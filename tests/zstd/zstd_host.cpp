@@ -36,6 +36,17 @@ Table
 make_table(const uint32_t* hist)
 {
     Table t;
+    uint32_t present = 0, mx = 0;
+    uint64_t total = 0;
+    for (int k = 0; k < 256; ++k) {
+        present += hist[k] != 0;
+        mx = hist[k] > mx ? hist[k] : mx;
+        total += hist[k];
+    }
+    if (huf_flat(present, mx, total)) {
+        std::memset(t.len, 0, sizeof t.len);
+        return t; // raw literals
+    }
     const uint32_t n = huf_lengths(hist, t.len, kHufMaxBits);
     if (n == 1)
         t.mode = 1;
