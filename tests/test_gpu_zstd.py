@@ -325,3 +325,59 @@ def shuffle_block(kind, ts, blk):
     if kind == 0:
         return blk
     return shuffle({1: "shuffle", 2: "bitshuffle"}[kind], ts, blk)
+
+
+@needs_zstd
+@pytest.mark.parametrize("level", [3, 9])
+def test_plain_zstd_far_candidates_large_chunks(gpu, monkeypatch, level):
+    """Plain zstd at the far-candidate levels (zstd_far: 4 / 8 hash slices)
+    on chunks of 16 MiB (tag bits 7) and 2 MiB, camera-like, dim and random
+    bands: every frame decodes to its chunk, and the far pass pays (fewer
+    bytes than level 1 on the same layer)."""
+    monkeypatch.setenv("AQZ_ZSTD_HOST", "0")
+    rng = np.random.default_rng(30 + level)
+    for T, hw in ((8, 1024), (4, 512)):
+        dims = [(TIME, 0, T, 1), (SPACE, 2 * hw, hw, 1), (SPACE, hw, hw, 1)]
+        cam = camera_like(rng, T * 2 * hw * hw, np.uint16).reshape(T, 2 * hw, hw)
+        dim = camera_like(rng, T * hw * hw, np.uint16, level=100.0, noise=3.0,
+                          amp=0.0).reshape(T, hw, hw)
+        frames = cam.copy()
+        frames[:, hw:, :] = dim                                  # chunk 1: dim sCMOS
+        frames[:, hw:hw + hw // 8, :] = rng.integers(0, 65535, (T, hw // 8, hw))  # random band
+        st = gpu.Stage(dims, U16, MEAN, multiscale=False, layer_slots=2, max_batch_frames=T)
+        st.append(np.ascontiguousarray(frames))
+        layer, _ = st.copy_layer(0, 0)
+        bpc = st.layout(0)["bytes_per_chunk"]
+        assert bpc == T * hw * hw * 2
+        sizes = {}
+        for lv in (1, level):
+            st.compress_layer(0, 0, codec=3, clevel=lv, shuffle=0)
+            data, off = st.copy_compressed(0, 0)
+            sizes[lv] = int(off[-1])
+            for c, _, _, o, nb in st.compressed_entries(0, 0):
+                assert zstd_decode(data[o:o + nb].tobytes(), bpc) == \
+                    layer[c * bpc:(c + 1) * bpc].tobytes(), (T, lv, c)
+        st.close()
+        print(f"{bpc >> 20} MiB chunks: bytes by level {sizes}")
+        assert sizes[level] < sizes[1]
+
+
+@needs_zstd
+def test_plain_zstd_far_unaligned_chunks(gpu, monkeypatch):
+    """u8 chunks of an odd byte count (3 x 127 x 129): the far pass needs
+    4-byte aligned segments and is skipped; level 3 still decodes."""
+    monkeypatch.setenv("AQZ_ZSTD_HOST", "0")
+    dims = [(TIME, 0, 3, 1), (SPACE, 254, 127, 1), (SPACE, 258, 129, 1)]
+    frames = _frames(U8, 3, 254, 258, 91)
+    st = gpu.Stage(dims, U8, MEAN, multiscale=False, layer_slots=2, max_batch_frames=3)
+    st.append(frames)
+    layer, flags = st.copy_layer(0, 0)
+    bpc = st.layout(0)["bytes_per_chunk"]
+    assert bpc % 4 != 0
+    st.compress_layer(0, 0, codec=3, clevel=3, shuffle=0)
+    data, _ = st.copy_compressed(0, 0)
+    for c, _, _, o, nb in st.compressed_entries(0, 0):
+        if flags[c]:
+            assert zstd_decode(data[o:o + nb].tobytes(), bpc) == \
+                layer[c * bpc:(c + 1) * bpc].tobytes(), c
+    st.close()
