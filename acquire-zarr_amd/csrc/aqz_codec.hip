@@ -867,7 +867,9 @@ zstd_far(const ZstdParams p)
             const uint32_t i = i0 + k;
             if (i < nkey && (sbits == 0 || (h[k] >> (32u - sbits)) == slice)) {
                 const uint32_t e = T[(h[k] >> bshift) & ((1u << FL) - 1u)];
-                far[i] = (e != 0 && (e & tmask) == (h[k] & tmask)) ? (e >> TB) : 0u;
+                const uint32_t fv = (e != 0 && (e & tmask) == (h[k] & tmask)) ? (e >> TB) : 0u;
+                if (!(p.dbg & 32u)) // A/B: 32 = no far[] stores (frames invalid)
+                    far[i] = fv;
             }
         }
         __syncthreads();
@@ -875,7 +877,7 @@ zstd_far(const ZstdParams p)
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {
             const uint32_t i = i0 + k;
-            if (i < nkey && (sbits == 0 || (h[k] >> (32u - sbits)) == slice))
+            if (i < nkey && (sbits == 0 || (h[k] >> (32u - sbits)) == slice) && !(p.dbg & 64u))
                 atomicMax(&T[(h[k] >> bshift) & ((1u << FL) - 1u)],
                           ((i + 1) << TB) | (h[k] & tmask));
         }
