@@ -112,13 +112,20 @@ namespace aqz {
 // blocks; tools/zstd_lab.cpp with far candidates: dim sCMOS 3.20 -> 3.37,
 // camera 1.972 -> 1.983, c-blosc clevel 5 3.14 / 1.974) -- four times the
 // tables to build (zstd_table 0.5 -> 2.5 ms per 512 MiB layer).
+// Unshuffled data (plain zstd, or blosc without a shuffle) keeps its
+// statistics across a chunk: groups of kHufGroupPlain blocks (256 KiB),
+// a quarter of the tables to build (tools/zstd_lab.cpp hufgroup=8/16/32:
+// camera-like 1.596 / 1.596 / 1.596, dim 3.260 / 3.260 / 3.260).
 // The first Huffman block of a group carries the tree, the rest are Treeless.
 constexpr uint32_t kHufGroup = 8;
+constexpr uint32_t kHufGroupPlainLog2 = 5;
 
 // log2 of the blocks per Huffman group for a segment of seg_bytes
 inline uint32_t
 zstd_huf_group_log2(uint32_t shuffle, uint32_t typesize, uint32_t seg_bytes, int32_t clevel)
 {
+    if (shuffle == 0)
+        return kHufGroupPlainLog2;
     uint32_t lg = 3; // kHufGroup
     if (shuffle == 2 && typesize > 0 && clevel >= 7) {
         const uint32_t plane = seg_bytes / (8u * typesize);
@@ -168,7 +175,7 @@ struct ZstdParams
     uint32_t phist;         // parse history: bytes before a unit its matches
                             // may reach (0, kZHist1, kZHist2: the level)
     uint32_t ngrp;          // Huffman groups per segment
-    uint32_t hgrp_log2;     // log2 of the zstd blocks per Huffman group (<= 3)
+    uint32_t hgrp_log2;     // log2 of the zstd blocks per Huffman group (<= 5)
     uint32_t fit;           // 1: fitted sequence tables allowed (AQZ_ZSTD_FIT=0: predefined)
     // far candidates (zstd_far; plain zstd at level >= 5): per segment
     // position the most recent earlier position with the same 5-byte key,

@@ -2033,8 +2033,10 @@ zstd_seqenc(const ZstdParams p)
 __global__ __launch_bounds__(64) void
 zstd_segment(const ZstdParams p)
 {
-    static_assert(64 % kHufGroup == 0, "a wave step holds whole groups");
+    static_assert(64 % kHufGroup == 0 && 64 % (1u << kHufGroupPlainLog2) == 0,
+                  "a wave step holds whole groups");
     const uint32_t gl = p.hgrp_log2, gn = 1u << gl;
+    const uint64_t gmask = gn >= 64 ? ~0ull : (1ull << gn) - 1ull;
     const uint32_t s = blockIdx.x, lane = threadIdx.x;
     if (zchunk_skip(p, s / p.nseg)) {
         if (lane == 0)
@@ -2052,9 +2054,9 @@ zstd_segment(const ZstdParams p)
         const uint64_t huf = __ballot(cmp && p.bltype[g] == 2);
         const uint64_t sqb = __ballot(cmp && p.bnseq[g] > 0);
         if (lane < (64u >> gl) && b0 + (lane << gl) < z0.nb) {
-            const uint32_t m = uint32_t(huf >> (lane << gl)) & ((1u << gn) - 1u);
+            const uint64_t m = (huf >> (lane << gl)) & gmask;
             p.carrier[s * p.ngrp + (b0 >> gl) + lane] =
-              m ? b0 + (lane << gl) + uint32_t(__builtin_ctz(m)) : ~0u;
+              m ? b0 + (lane << gl) + uint32_t(__builtin_ctzll(m)) : ~0u;
         }
         if (scar == ~0u && sqb)
             scar = b0 + uint32_t(__ffsll(static_cast<long long>(sqb))) - 1;
@@ -2284,7 +2286,7 @@ launch_zstd(const ZstdParams& p, hipStream_t stream)
     if (nblk * kZSubBlocks > 0x7fffffffull || p.nseg == 0 || p.bps == 0 ||
         uint64_t(p.bps) * zstd::kBlock < p.seg_bytes)
         return hipErrorInvalidValue;
-    if (p.hgrp_log2 > 3 || p.ngrp != ((p.bps + (1u << p.hgrp_log2) - 1) >> p.hgrp_log2))
+    if (p.hgrp_log2 > 5 || p.ngrp != ((p.bps + (1u << p.hgrp_log2) - 1) >> p.hgrp_log2))
         return hipErrorInvalidValue;
     if (!p.store_only) {
         hipError_t e = hipMemsetAsync(p.scount, 0, nseg * 192 * 4, stream);

@@ -292,8 +292,8 @@ def test_device_frames_equal_serial_model(gpu, monkeypatch, codec, shuffle, clev
         if not flags[c]:
             continue
         chunk = layer[c * bpc:(c + 1) * bpc].tobytes()
-        if codec == 3:
-            assert fr == model_frame(chunk), c
+        if codec == 3:  # unshuffled: Huffman groups of 32 blocks
+            assert fr == model_frame(chunk, glog2=5), c
             checked += 1
             continue
         h = header(fr)
@@ -310,8 +310,9 @@ def test_device_frames_equal_serial_model(gpu, monkeypatch, codec, shuffle, clev
             if cs == len(blk):
                 assert rec == sh, (c, j)
             else:
-                # bitshuffle at clevel >= 7: a Huffman group is one bit plane
-                glog2 = 3
+                # bitshuffle at clevel >= 7: a Huffman group is one bit plane;
+                # no shuffle: 32 blocks
+                glog2 = 5 if shuffle == 0 else 3
                 while (shuffle == 2 and clevel >= 7 and glog2 > 0
                        and (8192 << glog2) > len(blk) // 16):
                     glog2 -= 1

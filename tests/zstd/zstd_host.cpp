@@ -289,7 +289,7 @@ zh_encode_frame_g(const uint8_t* src, uint64_t n, int lz, uint32_t glog2, uint8_
 {
     static SeqTables st;
     static const bool ok = build_seq_tables(st);
-    if (!ok || glog2 > 3)
+    if (!ok || glog2 > 5)
         return 0;
     const std::vector<uint8_t> f = encode_frame(src, n, lz != 0, st, glog2);
     if (f.size() > cap)
