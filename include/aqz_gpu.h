@@ -390,7 +390,8 @@ aqz_status aqz_stage_device_layer(aqz_stage* st, uint32_t level,
  *  - AQZ_CODEC_ZSTD: one zstd frame per chunk (ZSTD_compress,
  *    zarr.common.cpp:142-166), made on the device.
  *  The device zstd encoder: Huffman literals (one table per 64 KiB group of
- *  blocks, or per bit plane under bitshuffle), sequence tables fitted per
+ *  a shuffled block -- per bit plane under bitshuffle at clevel >= 7 -- or
+ *  per 256 KiB of unshuffled data), sequence tables fitted per
  *  frame, a greedy LZ parse in 4 KiB units; the level sets how far back
  *  matches reach (zstd level L; blosc clevel c is L = 2c - 1): plain zstd
  *  L 1-2 unit-local, L 3-6 + far candidates from a 2^17-entry table over
