@@ -1922,8 +1922,15 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
         p.fit = uint32_t(std::atoi(e));
     p.src = chunks;
     p.src_pitch = pitch;
-    if (const char* e = std::getenv("AQZ_ZSTD_DBG")) // tuning knob (A/B)
+    if (const char* e = std::getenv("AQZ_ZSTD_DBG")) { // tuning knob (A/B timing only)
+        // bits 1/2/4/8 change the parse (frames stay valid); 16/32/64 skip
+        // work the frames need and are honoured only with
+        // AQZ_ZSTD_DBG_INVALID=1, for timing experiments
         p.dbg = uint32_t(std::atoi(e));
+        const char* inv = std::getenv("AQZ_ZSTD_DBG_INVALID");
+        if (!(inv && std::atoi(inv) == 1))
+            p.dbg &= 15u;
+    }
     const bool shuffle = blosc && !store_only_ &&
                          (c_.shuffle == 2 || (c_.shuffle == 1 && typesize_ > 1));
     if (shuffle) {

@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 O=gpurun_out/pab
 mkdir -p $O
 for dbg in ${DBGS:-0 1 2}; do
-  AQZ_ZSTD_DBG=$dbg timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/d$dbg -o run -- python3 tools/codec_bench.py --codec zstd --shuffle 0 --clevel 3 --kinds camera --reps 2 > $O/d$dbg.log 2>&1 || exit 1
+  AQZ_ZSTD_DBG_INVALID=1 AQZ_ZSTD_DBG=$dbg timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/d$dbg -o run -- python3 tools/codec_bench.py --codec zstd --shuffle 0 --clevel 3 --kinds camera --reps 2 > $O/d$dbg.log 2>&1 || exit 1
   f=$(find $O/d$dbg -name 'run_kernel_stats.csv' | head -1)
   echo "== dbg $dbg"; grep device $O/d$dbg.log || true
   python3 - "$f" <<'PY'
