@@ -2,11 +2,13 @@
 //
 // A serial encoder over the format pieces of csrc/aqz_zstd.hh with the
 // knobs the device encoder could take: parse window / unit, hash-chain depth,
-// lazy matching, minimum match, repeat offsets, Huffman table scope, and
-// predefined vs custom FSE sequence tables.  Every frame is decoded by
-// libzstd and compared; sizes are set against libzstd's levels on the same
-// payloads (camera-like and dim sCMOS u16, plain 8 MiB chunks and byte-
-// shuffled 256 KiB blosc blocks).
+// lazy matching, minimum match, repeat offsets, Huffman table scope,
+// predefined vs custom FSE sequence tables, and the far candidates of
+// zstd_far (far=<log2 table entries>, farbatch, fartag, farmin, farcap,
+// farcost).  Every frame is decoded by libzstd and compared; sizes are set
+// against libzstd's levels on the same payloads (camera-like and dim sCMOS
+// u16: plain 8 MiB chunks, byte-shuffled (_shuf) and bitshuffled (_bit)
+// 256 KiB blosc blocks).
 //
 //   hipcc -x hip --cuda-host-only -std=c++20 -O2 -I acquire-zarr_amd/csrc \
 //         tools/zstd_lab.cpp -ldl -o tools/zstd_lab
