@@ -62,14 +62,42 @@ class ArrayDescC(C.Structure):
 class StageOptionsC(C.Structure):
     _fields_ = [("layer_slots", C.c_uint32), ("max_batch_frames", C.c_uint32),
                 ("first_frame", C.c_uint64), ("z_slab_begin", C.c_uint32),
-                ("z_slab_end", C.c_uint32)]
+                ("z_slab_end", C.c_uint32), ("placement_tries", C.c_uint32),
+                ("reserved", C.c_uint32)]
 
 
 class StageBenchOptionsC(C.Structure):
     """aqz_stage_bench_options (include/aqz_gpu_bench.h): not drop-in ABI."""
     _fields_ = [("force_levels", C.c_uint32), ("skip_level0_split", C.c_int32),
                 ("placement_tries", C.c_uint32), ("placement_mode", C.c_uint32),
-                ("placement_spacer_bytes", C.c_uint64)]
+                ("placement_spacer_bytes", C.c_uint64),
+                ("placement_reps", C.c_uint32), ("knobs", C.c_uint32),
+                ("nt_policy", C.c_uint32), ("xcd_rot", C.c_uint32),
+                ("region_rows_log2", C.c_uint32), ("zstd_flags", C.c_uint32),
+                ("ring_malloc_flags", C.c_uint32), ("chunk_pad_bytes", C.c_uint64),
+                ("ring_spacer_bytes", C.c_uint64)]
+
+
+# zstd_flags bits of aqz_stage_bench_options
+ZSTD_LITERALS_ONLY, ZSTD_NO_FAR, ZSTD_NO_FIT = 1, 2, 4
+BENCH_FIELDS = tuple(f for f, _ in StageBenchOptionsC._fields_ if f != "reserved")
+
+
+def _bench_options(bench):
+    """StageBenchOptionsC from a dict of bench-header fields (None if empty).
+    skip_level0_split may be a bool; nt (a policy 0-7) maps to nt_policy."""
+    bench = {k: v for k, v in (bench or {}).items() if v}
+    if "nt" in bench:
+        bench["nt_policy"] = 8 | (bench.pop("nt") & 7)
+    if not bench:
+        return None
+    unknown = set(bench) - set(BENCH_FIELDS)
+    if unknown:
+        raise TypeError(f"unknown bench options {sorted(unknown)}")
+    b = StageBenchOptionsC()
+    for k, v in bench.items():
+        setattr(b, k, int(v))
+    return b
 
 
 class PlacementReportC(C.Structure):
@@ -229,6 +257,8 @@ def lib():
         "aqz_compressor_scratch_bytes": ([C.POINTER(CompressionC), u64, u32, u32], u64),
         "aqz_compressor_run": ([vp, vp, u64, u32, vp, sz, vp, vp], i32),
         "aqz_compressor_blocksize": ([vp], u32),
+        "aqz_stage_bench_replace_rings": ([vp, u32], i32),
+        "aqz_stage_compression_done": ([vp, u32, u64, C.POINTER(C.c_int32)], i32),
         "aqz_stage_compressed_entries": ([vp, u32, u64, C.POINTER(ChunkEntryC), sz], i32),
         "aqz_stage_shard_geometry": ([vp, u32, C.POINTER(u32), C.POINTER(u32),
                                       C.POINTER(u32)], i32),
@@ -362,19 +392,17 @@ def downsampling_metadata_json(method):
 
 
 def estimate_memory(dims, dtype, method, max_levels=0, layer_slots=0,
-                    max_batch_frames=0, storage_order=None, force_levels=0,
-                    skip_level0_split=False, placement_tries=0, placement_mode=0,
-                    placement_spacer_bytes=0):
-    """aqz_stage_estimate_memory: upper bound of a stage's footprint (no GPU).
-    With bench options (force_levels, placement_*), the bench-header
-    aqz_stage_estimate_memory_bench, which includes the placement search's
-    creation peak."""
+                    max_batch_frames=0, storage_order=None, placement_tries=0,
+                    **bench):
+    """aqz_stage_estimate_memory: upper bound of a stage's footprint (no GPU),
+    including the placement search's creation peak when placement_tries > 1.
+    With bench-header options (force_levels, skip_level0_split,
+    placement_mode, ...), aqz_stage_estimate_memory_bench."""
     d, keep = _desc(dims, dtype, method, max_levels, True, storage_order, 0)
-    o = StageOptionsC(layer_slots, max_batch_frames, 0)
+    o = StageOptionsC(layer_slots, max_batch_frames, 0, 0, 0, placement_tries)
     m = MemoryUsageC()
-    if force_levels or skip_level0_split or placement_tries:
-        b = StageBenchOptionsC(force_levels, 1 if skip_level0_split else 0,
-                               placement_tries, placement_mode, placement_spacer_bytes)
+    b = _bench_options(bench)
+    if b is not None:
         _check(lib().aqz_stage_estimate_memory_bench(C.byref(d), C.byref(o), C.byref(b),
                                                      C.byref(m)),
                "aqz_stage_estimate_memory_bench")
@@ -509,24 +537,24 @@ class Downsampler:
 class Stage:
     """Device-resident multiscale stage: tile split + pyramid of every level.
 
-    force_levels / skip_level0_split are the bench-only extensions of
-    include/aqz_gpu_bench.h (aqz_stage_create_bench); everything else is the
-    drop-in ABI of include/aqz_gpu.h."""
+    Keyword arguments beyond the drop-in options of include/aqz_gpu.h
+    (force_levels, skip_level0_split, knobs, nt, chunk_pad_bytes,
+    zstd_flags, placement_mode, ...) are the bench-only fields of
+    include/aqz_gpu_bench.h (aqz_stage_create_bench)."""
 
     def __init__(self, dims, dtype, method, max_levels=0, multiscale=True,
                  storage_order=None, device=0, layer_slots=0,
-                 max_batch_frames=0, force_levels=0, skip_level0_split=False,
-                 first_frame=0, placement_tries=0, placement_mode=0,
-                 placement_spacer_bytes=0, z_slab=None):
+                 max_batch_frames=0, first_frame=0, z_slab=None,
+                 placement_tries=0, **bench):
         self.dtype = dtype
         d, self._keep = _desc(dims, dtype, method, max_levels, multiscale,
                               storage_order, device)
         zb, ze = z_slab if z_slab else (0, 0)
-        o = StageOptionsC(layer_slots, max_batch_frames, first_frame, zb, ze)
+        o = StageOptionsC(layer_slots, max_batch_frames, first_frame, zb, ze,
+                          placement_tries)
         h = C.c_void_p()
-        if force_levels or skip_level0_split or placement_tries:
-            b = StageBenchOptionsC(force_levels, 1 if skip_level0_split else 0,
-                                   placement_tries, placement_mode, placement_spacer_bytes)
+        b = _bench_options(bench)
+        if b is not None:
             rc = lib().aqz_stage_create_bench(C.byref(d), C.byref(o), C.byref(b), C.byref(h))
         else:
             rc = lib().aqz_stage_create(C.byref(d), C.byref(o), C.byref(h))
@@ -560,6 +588,11 @@ class Stage:
 
     def set_stream(self, stream_ptr):
         _check(lib().aqz_stage_set_stream(self.h, stream_ptr), "set_stream")
+
+    def replace_rings(self, level_mask):
+        """Bench: fresh chunk-layer rings for the levels in level_mask (the
+        old ones stay allocated); placement experiments only."""
+        _check(lib().aqz_stage_bench_replace_rings(self.h, level_mask), "replace_rings")
 
     def set_tuning(self, knobs=0, nt=0):
         _check(lib().aqz_stage_set_tuning(self.h, knobs, nt), "set_tuning")
@@ -711,6 +744,12 @@ class Stage:
         c = CompressionC(codec, clevel, shuffle)
         _check(lib().aqz_stage_compress_layer(self.h, level, layer, C.byref(c)),
                "compress_layer")
+
+    def compression_done(self, level, layer):
+        d = C.c_int32(0)
+        _check(lib().aqz_stage_compression_done(self.h, level, layer, C.byref(d)),
+               "compression_done")
+        return bool(d.value)
 
     def compressed_offsets(self, level, layer):
         n = self.layout(level)["chunks_per_layer"] + 1

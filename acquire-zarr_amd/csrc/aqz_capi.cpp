@@ -448,12 +448,42 @@ apply_bench(const aqz_stage_bench_options* bench, StageOptions& o)
         return;
     o.force_levels = bench->force_levels;
     o.skip_level0_split = bench->skip_level0_split != 0;
-    o.placement_tries = bench->placement_tries;
+    if (bench->placement_tries)
+        o.placement_tries = bench->placement_tries;
     o.placement_mode = bench->placement_mode;
     if (o.placement_mode > 1)
         throw Error(AQZ_STATUS_INVALID_ARGUMENT, "placement_mode must be 0 or 1");
     if (bench->placement_spacer_bytes)
         o.placement_spacer = bench->placement_spacer_bytes;
+    if (bench->placement_reps)
+        o.placement_reps = bench->placement_reps;
+    o.knobs = bench->knobs;
+    if (bench->nt_policy)
+        o.nt_mode = bench->nt_policy & 7u;
+    o.xcd_rot = bench->xcd_rot;
+    o.region_rows_log2 = bench->region_rows_log2;
+    o.chunk_pad = bench->chunk_pad_bytes;
+    o.ring_malloc_flags = bench->ring_malloc_flags;
+    o.ring_spacer = bench->ring_spacer_bytes;
+    const uint32_t z = bench->zstd_flags;
+    o.codec.match = (z & 1u) ? 0 : 1;
+    o.codec.far = (z & 2u) ? 0 : 1;
+    o.codec.fit = (z & 4u) ? 0 : 1;
+    o.codec.phist = (z >> 8) & 0xffu;
+    o.codec.parse = (z >> 16) & 0xfu;
+}
+
+static void
+apply_options(const aqz_stage_options* opt, StageOptions& o)
+{
+    if (!opt)
+        return;
+    o.layer_slots = opt->layer_slots;
+    o.max_batch_frames = opt->max_batch_frames;
+    o.first_frame = opt->first_frame;
+    o.z_slab_begin = opt->z_slab_begin;
+    o.z_slab_end = opt->z_slab_end;
+    o.placement_tries = opt->placement_tries;
 }
 
 static aqz_status
@@ -466,13 +496,7 @@ create_stage(const aqz_array_desc* desc, const aqz_stage_options* opt,
     return guard([&] {
         const ArrayDesc a = to_desc(desc);
         StageOptions o;
-        if (opt) {
-            o.layer_slots = opt->layer_slots;
-            o.max_batch_frames = opt->max_batch_frames;
-            o.first_frame = opt->first_frame;
-            o.z_slab_begin = opt->z_slab_begin;
-            o.z_slab_end = opt->z_slab_end;
-        }
+        apply_options(opt, o);
         apply_bench(bench, o);
         auto* s = new aqz_stage;
         try {
@@ -508,13 +532,7 @@ aqz_stage_estimate_memory_bench(const aqz_array_desc* desc, const aqz_stage_opti
     return guard([&] {
         const ArrayDesc a = to_desc(desc);
         StageOptions o;
-        if (opt) {
-            o.layer_slots = opt->layer_slots;
-            o.max_batch_frames = opt->max_batch_frames;
-            o.first_frame = opt->first_frame;
-            o.z_slab_begin = opt->z_slab_begin;
-            o.z_slab_end = opt->z_slab_end;
-        }
+        apply_options(opt, o);
         apply_bench(bench, o);
         const Footprint f = Stage::estimate_memory(a, o);
         *out = aqz_memory_usage{ f.device, f.pinned };
@@ -612,6 +630,12 @@ aqz_stage_set_tuning(aqz_stage* st, uint32_t knobs, uint32_t nt)
     if (!st)
         return AQZ_STATUS_INVALID_ARGUMENT;
     return guard([&] { st->st->set_tuning(knobs, nt); });
+}
+
+aqz_status
+aqz_stage_bench_replace_rings(aqz_stage* st, uint32_t level_mask)
+{
+    return guard_sticky(st, [&] { st->st->replace_rings(level_mask); });
 }
 
 aqz_status
@@ -935,6 +959,15 @@ aqz_compressor_run(aqz_compressor* c, const void* chunks, uint64_t pitch,
 }
 
 // ---- shard packing ---------------------------------------------------------
+aqz_status
+aqz_stage_compression_done(aqz_stage* st, uint32_t level, uint64_t layer, int32_t* done)
+{
+    if (!done)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    *done = 0;
+    return guard_sticky(st, [&] { *done = st->st->compression_done(level, layer) ? 1 : 0; });
+}
+
 aqz_status
 aqz_stage_compressed_entries(aqz_stage* st, uint32_t level, uint64_t layer,
                              aqz_chunk_entry* out, size_t n)

@@ -54,7 +54,7 @@ DevBuf::operator=(DevBuf&& o) noexcept
 }
 
 void
-DevBuf::alloc(size_t bytes)
+DevBuf::alloc(size_t bytes, unsigned flags)
 {
     if (p && n >= bytes)
         return;
@@ -65,16 +65,10 @@ DevBuf::alloc(size_t bytes)
     if (bytes == 0)
         return;
     void* q = nullptr;
-    static const unsigned flags = [] {
-        const char* s = std::getenv("AQZ_MALLOC_FLAGS"); // tuning knob
-        return s ? unsigned(std::atoi(s)) : 0u;
-    }();
     if (flags)
         hip_check(hipExtMallocWithFlags(&q, bytes, flags), "hipExtMallocWithFlags");
     else
         hip_check(hipMalloc(&q, bytes), "hipMalloc");
-    if (std::getenv("AQZ_DEBUG_ALLOC") && bytes >= (size_t(1) << 24))
-        fprintf(stderr, "aqz alloc %p %zu MiB\n", q, bytes >> 20);
     p = static_cast<uint8_t*>(q);
     n = bytes;
 }
@@ -108,12 +102,7 @@ PinnedBuf::alloc(size_t bytes)
 static size_t
 copy_piece_bytes()
 {
-    static const size_t v = [] {
-        const char* s = std::getenv("AQZ_COPY_PIECE_MB");
-        const long mb = s ? std::atol(s) : 32;
-        return size_t(mb > 0 ? mb : 1 << 20) << 20;
-    }();
-    return v;
+    return size_t(32) << 20;
 }
 
 static void
@@ -151,18 +140,8 @@ copy_chunks(void* dst, const uint8_t* src, uint64_t bpc, uint64_t pitch, uint32_
     }
 }
 
-// Device chunk pitch: bpc, or bpc plus a pad that staggers the chunks of a
-// layer across HBM channels (AQZ_CHUNK_PAD bytes; tuning knob).
-static uint64_t
-chunk_pitch(uint64_t bpc, uint32_t n_chunks)
-{
-    (void)n_chunks;
-    if (const char* s = std::getenv("AQZ_CHUNK_PAD"))
-        return bpc + uint64_t(std::max(0L, std::atol(s)));
-    return bpc;
-}
-
-// host threads for the pageable -> pinned staging copy (AQZ_COPY_THREADS)
+// host threads for the pageable -> pinned staging copy (AQZ_COPY_THREADS, a
+// deployment setting: it changes no output byte)
 static unsigned
 copy_workers()
 {
@@ -235,6 +214,9 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
 
     const size_t n = base->ndims();
     const uint32_t B = opt_.max_batch_frames;
+    DevBuf spacer;
+    if (opt_.ring_spacer)
+        spacer.alloc(opt_.ring_spacer, opt_.ring_malloc_flags);
     lv_.resize(levels.size());
     for (size_t k = 0; k < levels.size(); ++k) {
         StageLevel& L = lv_[k];
@@ -258,7 +240,7 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         if (F == 0 || F > 0x7fffffffull)
             throw Error(9, "unsupported frames per chunk layer");
         L.F = uint32_t(F);
-        L.pitch = chunk_pitch(L.bpc, L.n_chunks);
+        L.pitch = L.bpc + opt_.chunk_pad; // bench option: chunks staggered
         L.slot_bytes = L.pitch * L.n_chunks;
         L.layer_bytes = L.bpc * L.n_chunks;
         L.n_slots = std::max<uint32_t>(opt_.layer_slots,
@@ -290,6 +272,8 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
                             hipMemcpyHostToDevice),
                   "hipMemcpy");
     }
+
+    spacer = DevBuf{}; // freed: only the rings' placement needed it
 
     // 2-D fast path: z never shrinks and XY shrinks at every level, so every
     // input frame emits exactly one frame per level (downsampler.cpp:358-399)
@@ -340,14 +324,12 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
                         (1u << rh_log2_) <= uint32_t(kMaxRegionRows);
         }
     }
-    if (const char* ev = std::getenv("AQZ_KNOBS")) // tuning knob
-        knobs_ = uint32_t(std::atoi(ev));
-    if (const char* ev = std::getenv("AQZ_XCD_ROT")) // tuning knob
-        xcd_rot_ = uint32_t(std::atoi(ev));
-    if (const char* ev = std::getenv("AQZ_NT")) // tuning knob
-        nt_mode_ = uint32_t(std::atoi(ev)) & 7u;
-    if (const char* ev = std::getenv("AQZ_REGION_ROWS_LOG2")) { // tuning knob
-        const uint32_t v = uint32_t(std::atoi(ev));
+    // tuning (bench options only; the drop-in create leaves them at the
+    // shipped values and no environment variable reaches them)
+    knobs_ = opt_.knobs;
+    xcd_rot_ = opt_.xcd_rot;
+    nt_mode_ = opt_.nt_mode & 7u;
+    if (const uint32_t v = opt_.region_rows_log2) {
         if (v >= std::max<uint32_t>(4, n_fused_) && (1u << v) <= uint32_t(kMaxRegionRows))
             rh_log2_ = v;
     }
@@ -412,38 +394,16 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
     // pool of their own; their work is DMA and small blits, so priority costs
     // the kernels nothing.  AQZ_COPY_PRIORITY=0 keeps them at normal priority (2: lowest).
     {
-        const char* e = std::getenv("AQZ_COPY_PRIORITY");
         int least = 0, greatest = 0;
         hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest),
                   "hipDeviceGetStreamPriorityRange");
-        const int mode = e ? std::atoi(e) : 1;
-        if (mode == 0) {
-            hip_check(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking), "hipStreamCreate");
-            hip_check(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking), "hipStreamCreate");
-        } else {
-            const int prio = mode == 2 ? least : greatest;
-            hip_check(hipStreamCreateWithPriority(&h2d_, hipStreamNonBlocking, prio),
-                      "hipStreamCreate");
-            hip_check(hipStreamCreateWithPriority(&d2h_, hipStreamNonBlocking, prio),
-                      "hipStreamCreate");
-        }
-    }
-    {
-        // compression stream: normal priority (AQZ_COMP_PRIORITY=1: greatest,
-        // 2: lowest) -- tuning knob
-        const char* e = std::getenv("AQZ_COMP_PRIORITY");
-        const int mode = e ? std::atoi(e) : 0;
-        int least = 0, greatest = 0;
-        hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest),
-                  "hipDeviceGetStreamPriorityRange");
-        for (hipStream_t* cs : { &comp_, &comp_lo_ }) {
-            if (mode == 0)
-                hip_check(hipStreamCreateWithFlags(cs, hipStreamNonBlocking), "hipStreamCreate");
-            else
-                hip_check(hipStreamCreateWithPriority(cs, hipStreamNonBlocking,
-                                                      mode == 2 ? least : greatest),
-                          "hipStreamCreate");
-        }
+        hip_check(hipStreamCreateWithPriority(&h2d_, hipStreamNonBlocking, greatest),
+                  "hipStreamCreate");
+        hip_check(hipStreamCreateWithPriority(&d2h_, hipStreamNonBlocking, greatest),
+                  "hipStreamCreate");
+        // compression streams: normal priority
+        for (hipStream_t* cs : { &comp_, &comp_lo_ })
+            hip_check(hipStreamCreateWithFlags(cs, hipStreamNonBlocking), "hipStreamCreate");
         // the smallest levels' layers (a few chunks: their codec kernels are
         // a handful of workgroups, pure latency) on a stream of the least
         // priority, whose hardware queue pool is not the normal one's, so
@@ -480,7 +440,7 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
 void
 Stage::place_level(StageLevel& L)
 {
-    L.ring.alloc(L.slot_bytes * L.n_slots);
+    L.ring.alloc(L.slot_bytes * L.n_slots, opt_.ring_malloc_flags);
     L.flags.alloc(size_t(L.n_chunks) * L.n_slots * 4);
     hip_check(hipMemsetAsync(L.ring.p, 0, L.ring.n, stream_), "hipMemsetAsync");
     hip_check(hipMemsetAsync(L.flags.p, 0, L.flags.n, stream_), "hipMemsetAsync");
@@ -521,15 +481,7 @@ Stage::calibrate_placement()
     uint32_t tries = opt_.placement_tries;
     uint32_t mode = opt_.placement_mode;
     uint64_t spacer = opt_.placement_spacer;
-    uint32_t reps = 10;
-    if (const char* e = std::getenv("AQZ_PLACEMENT_TRIES")) // tuning knobs
-        tries = uint32_t(std::max(0, std::atoi(e)));
-    if (const char* e = std::getenv("AQZ_PLACEMENT_MODE"))
-        mode = uint32_t(std::atoi(e));
-    if (const char* e = std::getenv("AQZ_PLACEMENT_SPACER_MB"))
-        spacer = uint64_t(std::max(0, std::atoi(e))) << 20;
-    if (const char* e = std::getenv("AQZ_PLACEMENT_REPS"))
-        reps = uint32_t(std::max(1, std::atoi(e)));
+    const uint32_t reps = std::max<uint32_t>(1, opt_.placement_reps);
     uint64_t ring_bytes = 0, set_bytes = 0;
     std::vector<bool> has_ring(lv_.size());
     for (size_t k = 0; k < lv_.size(); ++k) {
@@ -658,6 +610,22 @@ Stage::calibrate_placement()
     hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
+}
+
+void
+Stage::replace_rings(uint32_t mask)
+{
+    synchronize();
+    for (size_t k = 0; k < lv_.size() && k < 32; ++k) {
+        StageLevel& L = lv_[k];
+        if (!((mask >> k) & 1u) || !L.ring.p)
+            continue;
+        held_.push_back(std::move(L.ring));
+        held_.push_back(std::move(L.flags));
+        held_.push_back(std::move(L.ref_table));
+        place_level(L);
+    }
+    hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
 
 Stage::~Stage()
@@ -854,7 +822,11 @@ Stage::issue_ticket()
     }
     hip_check(hipEventRecord(e, d2h_), "hipEventRecord");
     tickets_.push_back(e);
-    return ++tickets_issued_;
+    ++tickets_issued_;
+    // retire what has landed, so a caller that never asks does not hold one
+    // live event per copy for the stage's lifetime
+    (void)copies_completed();
+    return tickets_issued_;
 }
 
 uint64_t
@@ -884,6 +856,7 @@ Stage::wait_copies()
     hip_check(hipStreamSynchronize(comp_lo_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(comp_lo2_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(d2h_), "hipStreamSynchronize");
+    (void)copies_completed(true); // every ticket has landed
 }
 
 void
@@ -897,7 +870,15 @@ Stage::append(const void* frames, uint64_t n_frames, int mem)
     const uint64_t fbytes = uint64_t(lv_[0].W) * lv_[0].H * bpp_;
     uint64_t n_ok = n_frames;
     if (max_frames_ > 0) {
-        const uint64_t room = max_frames_ - std::min(max_frames_, lv_[0].frames_written);
+        uint64_t room = max_frames_ - std::min(max_frames_, lv_[0].frames_written);
+        if (slab_len_) {
+            // frame ids jump over the other slabs' planes: count room in this
+            // stage's own frames, (z stacks left) * slab - frames of this slab
+            const uint64_t p0 = lv_[0].planes;
+            const uint64_t stack = lv_[0].frames_written / p0;
+            const uint64_t stacks = max_frames_ / p0;
+            room = stack < stacks ? (stacks - stack) * slab_len_ - slab_done_ : 0;
+        }
         n_ok = std::min(n_ok, room);
     }
     const auto* src = static_cast<const uint8_t*>(frames);
@@ -1586,7 +1567,7 @@ Stage::estimate_memory(const ArrayDesc& desc, const StageOptions& opt_in)
         const uint64_t slots = std::max<uint64_t>(opt.layer_slots, (B - 1 + F - 1) / F + 1);
         const uint64_t lfb = W * H * bpp;
         if (!(k == 0 && opt.skip_level0_split)) {
-            const uint64_t ring = chunk_pitch(bpc, uint32_t(nc)) * nc * slots;
+            const uint64_t ring = (bpc + opt.chunk_pad) * nc * slots;
             const uint64_t set = ring + nc * slots * 4 + slots * F * sizeof(FrameRef);
             f.device += set;        // ring, has_data words, frame table
             f.device += nc * slots; // has_data bytes
@@ -1757,8 +1738,10 @@ Stage::shard_geometry(uint32_t level, uint32_t* chunks_per_shard, uint32_t* n_sh
 }
 
 // ---- device compression of resident layers ----------
-Compressor::Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compression& c)
+Compressor::Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compression& c,
+                       const CodecTuning& tune)
   : c_(c)
+  , tune_(tune)
   , nbytes_(chunk_bytes)
   , typesize_(typesize)
 {
@@ -1911,26 +1894,15 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
     // A parse history (matches into the 12 / 28 KiB before a unit, loaded and
     // hashed per unit) is kept only as a tuning knob: the far candidates
     // reach every earlier unit at a fraction of its cost.
-    p.phist = 0;
-    if (const char* e = std::getenv("AQZ_ZSTD_HIST")) // tuning knob
-        p.phist = uint32_t(std::atoi(e));
+    p.phist = tune_.phist;
     // a match must save the bits of a sequence: ~12 with the fitted tables
     // of unshuffled data, 16 on shuffled planes (tools/zstd_lab.cpp sweep)
     p.match_bits = uint32_t(blosc ? zstd::kMatchBits : zstd::kMatchBitsFitted);
-    p.fit = 1;
-    if (const char* e = std::getenv("AQZ_ZSTD_FIT")) // tuning knob
-        p.fit = uint32_t(std::atoi(e));
+    p.fit = tune_.fit;
     p.src = chunks;
     p.src_pitch = pitch;
-    if (const char* e = std::getenv("AQZ_ZSTD_DBG")) { // tuning knob (A/B timing only)
-        // bits 1/2/4/8 change the parse (frames stay valid); 16/32/64 skip
-        // work the frames need and are honoured only with
-        // AQZ_ZSTD_DBG_INVALID=1, for timing experiments
-        p.dbg = uint32_t(std::atoi(e));
-        const char* inv = std::getenv("AQZ_ZSTD_DBG_INVALID");
-        if (!(inv && std::atoi(inv) == 1))
-            p.dbg &= 15u;
-    }
+    // parse variants for A/B timing (bits 1/2/4/8; the frames stay valid)
+    p.dbg = tune_.parse & 15u;
     const bool shuffle = blosc && !store_only_ &&
                          (c_.shuffle == 2 || (c_.shuffle == 1 && typesize_ > 1));
     if (shuffle) {
@@ -1942,10 +1914,9 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
         p.src_pitch = nbytes_;
     }
     const uint64_t nseg = uint64_t(n_chunks) * p.nseg, nblk = nseg * p.bps;
-    // LZ matches unless AQZ_ZSTD_MATCH=0 (literals only: the serial model's
+    // LZ matches unless tuned off (literals only: the serial model's
     // byte-exact mode, tests/test_gpu_zstd.py)
-    const char* me = std::getenv("AQZ_ZSTD_MATCH");
-    p.match = (me && std::atoi(me) == 0) ? 0 : 1;
+    p.match = tune_.match ? 1 : 0;
     if (!store_only_) {
         if (!seqt_.p) {
             zstd::SeqTables t;
@@ -1955,8 +1926,7 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
             hip_check(hipMemcpy(seqt_.p, &t, sizeof(t), hipMemcpyHostToDevice), "hipMemcpy");
         }
         // far candidates (zstd_far) in place of a parse history, where a
-        // history pays: zstd_far_slices (the level), 4-byte aligned segments;
-        // AQZ_ZSTD_FAR=0 off
+        // history pays: zstd_far_slices (the level), 4-byte aligned segments
         p.far_slices = zstd_far_slices(c_, typesize_);
         // a blosc block (256 KiB) needs no more than 2^13 entries (bitshuffle
         // camera 1.972 -> 1.969, tools/zstd_lab.cpp far=13), a quarter of the
@@ -1965,8 +1935,7 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
         p.far_tb = p.far_slices ? zstd_far_tag_bits(p.seg_bytes, p.far_slices, p.far_log) : 0;
         bool far = p.match && p.far_tb != 0 && (reinterpret_cast<uintptr_t>(p.src) & 3u) == 0 &&
                    (p.src_pitch & 3u) == 0 && (p.seg_bytes & 3u) == 0;
-        if (const char* e = std::getenv("AQZ_ZSTD_FAR")) // tuning knob
-            far = far && std::atoi(e) != 0;
+        far = far && tune_.far != 0;
         if (far) {
             far_.alloc(nseg * p.seg_bytes * 4);
             p.far = reinterpret_cast<uint32_t*>(far_.p);
@@ -2189,7 +2158,7 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
         L.comp_cfg.shuffle != c.shuffle) {
         hip_check(hipStreamSynchronize(cs), "hipStreamSynchronize");
         hip_check(hipStreamSynchronize(d2h_), "hipStreamSynchronize");
-        L.comp = std::make_unique<Compressor>(L.bpc, uint32_t(bpp_), c);
+        L.comp = std::make_unique<Compressor>(L.bpc, uint32_t(bpp_), c, opt_.codec);
         L.comp_cfg = c;
     }
     ensure_comp_slots(L);
@@ -2249,6 +2218,24 @@ Stage::compressed_offsets(uint32_t level, uint64_t layer, uint64_t* offsets, siz
     std::memcpy(offsets, L.h_coffsets[slot].p, (size_t(L.n_chunks) + 1) * 8);
 }
 
+bool
+Stage::compression_done(uint32_t level, uint64_t layer)
+{
+    if (level >= lv_.size())
+        throw Error(3, "level out of range");
+    StageLevel& L = lv_[level];
+    const uint32_t slot = L.n_slots ? uint32_t(layer % L.n_slots) : 0;
+    if (L.comp_layer.empty() || L.comp_layer[slot] != int64_t(layer))
+        throw Error(3, "layer was not compressed (or its slot was reused)");
+    if (L.comp_host[slot])
+        return L.zjob[slot]->finished();
+    const hipError_t q = hipEventQuery(L.comp_ev[slot]);
+    if (q == hipErrorNotReady)
+        return false;
+    hip_check(q, "hipEventQuery");
+    return true;
+}
+
 void
 Stage::copy_compressed_async(uint32_t level, uint64_t layer, void* dst, size_t cap)
 {
@@ -2267,6 +2254,7 @@ Stage::copy_compressed_async(uint32_t level, uint64_t layer, void* dst, size_t c
         if (cap < j.offsets[L.n_chunks])
             throw Error(2, "destination too small for the compressed layer");
         j.gather(static_cast<uint8_t*>(dst));
+        last_ticket_ = issue_ticket(); // complete as soon as it is issued
         return;
     }
     hip_check(hipEventSynchronize(L.comp_ev[slot]), "hipEventSynchronize");

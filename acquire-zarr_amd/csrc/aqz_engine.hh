@@ -53,7 +53,8 @@ struct DevBuf
     DevBuf& operator=(const DevBuf&) = delete;
     DevBuf(DevBuf&& o) noexcept;
     DevBuf& operator=(DevBuf&& o) noexcept;
-    void alloc(size_t bytes);
+    // flags: hipExtMallocWithFlags flags (0 = hipMalloc)
+    void alloc(size_t bytes, unsigned flags = 0);
 };
 
 // Owning pinned host allocation.
@@ -85,6 +86,17 @@ struct Compression
     int32_t shuffle = 1; // 0 none, 1 byte, 2 bit
 };
 
+// A/B switches of the device zstd encoder (aqz_stage_bench_options): every
+// setting still writes frames that decode to the chunk bytes.
+struct CodecTuning
+{
+    uint32_t match = 1;    // 0: literals only (the serial model's byte-exact mode)
+    uint32_t far = 1;      // 0: no far candidates
+    uint32_t fit = 1;      // 0: predefined sequence tables only
+    uint32_t phist = 0;    // parse history (KiB before a unit; 0 none)
+    uint32_t parse = 0;    // parse variants for timing (bits 1/2/4/8)
+};
+
 // Device frames of arrays of equally sized device chunks (aqz_codec.hip):
 // blosc1-lz4, blosc1-zstd or plain zstd.
 // hash slices of the device zstd far-candidate pass (0: none); aqz_engine.cpp
@@ -93,7 +105,8 @@ uint32_t zstd_far_slices(const Compression& c, uint32_t typesize);
 class Compressor
 {
   public:
-    Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compression& c);
+    Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compression& c,
+               const CodecTuning& tune = CodecTuning{});
     // bytes that always hold the frames of n_chunks chunks (any codec).
     // blosc frames never pass nbytes + 16 (the memcpyed rule); a plain zstd
     // frame of incompressible data is its header (<= 13 B) plus one raw
@@ -143,6 +156,7 @@ class Compressor
                   const uint32_t* flags, uint32_t tag, uint8_t* out, uint64_t* offsets,
                   hipStream_t stream, const uint32_t* order);
     Compression c_;
+    CodecTuning tune_;
     uint64_t nbytes_ = 0;
     uint32_t typesize_ = 1;
     BloscGeom g_{};
@@ -181,6 +195,17 @@ struct StageOptions
     uint32_t placement_tries = 0;
     uint32_t placement_mode = 0;
     uint64_t placement_spacer = uint64_t(128) << 20;
+    uint32_t placement_reps = 10;
+    // Kernel tuning (aqz_stage_bench_options; never read from the
+    // environment, so a deployed library always runs the shipped kernels).
+    uint32_t knobs = 0;            // A/B switches (0 = the shipped kernels)
+    uint32_t nt_mode = 7;          // nontemporal policy (loads 1, L0 2, L1/2 4)
+    uint32_t xcd_rot = 0;          // regions each XCD's walk is rotated by
+    uint32_t region_rows_log2 = 0; // 0 = automatic
+    uint64_t chunk_pad = 0;        // device bytes between chunks of a layer
+    uint32_t ring_malloc_flags = 0; // hipExtMallocWithFlags flags of the rings
+    uint64_t ring_spacer = 0;       // allocated before the rings, freed after
+    CodecTuning codec;             // device zstd encoder A/B switches
 };
 
 // What the creation-time placement search did (aqz_stage_placement_report).
@@ -295,6 +320,10 @@ class Stage
     // the stage's stream waits for the work enqueued so far on s
     void wait_stream(hipStream_t s);
     void set_tuning(uint32_t knobs, uint32_t nt) { knobs_ = knobs; nt_mode_ = nt & 7u; }
+    // bench: allocate fresh rings (+ has_data words, frame tables) for the
+    // levels in `mask`, holding the old ones until the stage is destroyed so
+    // the new ones land elsewhere (placement experiments)
+    void replace_rings(uint32_t mask);
     void append(const void* frames, uint64_t n_frames, int mem);
     void synchronize();
     uint64_t frames_written(uint32_t level) const;
@@ -324,6 +353,8 @@ class Stage
     // waits for that compression; offsets[0..n_chunks] (frame starts + total)
     void compressed_offsets(uint32_t level, uint64_t layer, uint64_t* offsets,
                             size_t n);
+    // has that compression finished (no wait)?
+    bool compression_done(uint32_t level, uint64_t layer);
     // D2H of the frames (offsets[n_chunks] bytes) on the hand-off stream
     void copy_compressed_async(uint32_t level, uint64_t layer, void* dst, size_t cap);
     // waits; one entry per chunk in output order
@@ -446,6 +477,7 @@ class Stage
     hipEvent_t mark_ev_[2] = { nullptr, nullptr };
     hipEvent_t ext_ev_ = nullptr;  // wait_stream
     PlacementReport placement_;         // creation-time placement search
+    std::vector<DevBuf> held_;          // replace_rings: old rings kept allocated
     bool finalized_ = false;
 };
 

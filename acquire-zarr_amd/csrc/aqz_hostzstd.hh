@@ -103,6 +103,11 @@ struct HostLayerJob
     bool done = true;
     int32_t status = 0; // 0 ok, else an AQZ status code
     void wait();
+    bool finished()
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        return done;
+    }
     // frames in output order -> dst (offsets[n_chunks] bytes)
     void gather(uint8_t* dst) const;
 };

@@ -30,11 +30,11 @@ U8, U16, F32 = 0, 1, 8
 MEAN = 1
 BPP = {U8: 1, U16: 2, F32: 4}
 
-# Creation-time placement search (bench-only option): up to 16
-# placements of the chunk-layer rings timed on random frames, a losing
-# placement freed and a 128 MiB spacer held until the search ends (peak: two
-# ring sets + the spacers, counted by aqz_stage_estimate_memory_bench).
-PLACEMENT = dict(placement_tries=16, placement_mode=0, placement_spacer_bytes=128 << 20)
+# Creation-time placement search (aqz_stage_options.placement_tries, DESIGN.md
+# section 3): up to 16 placements of the chunk-layer rings timed on random
+# frames, a losing placement freed and a 128 MiB spacer held until the search
+# ends (peak: two ring sets + the spacers, counted by aqz_stage_estimate_memory).
+PLACEMENT = dict(placement_tries=16)
 
 DTYPE_WORDS = {U8: "uint8", U16: "uint16", F32: "float32"}
 
@@ -513,8 +513,15 @@ def main():
                          "last two dims; the frames stay in acquisition order)")
     ap.add_argument("--no-hbm-probe", action="store_true",
                     help="skip the live streaming probe of this device's HBM rates")
+    ap.add_argument("--placement-tries", type=int, default=PLACEMENT["placement_tries"],
+                    help="aqz_stage_options.placement_tries of the device-resident stages "
+                         "(0: keep the first allocation)")
+    ap.add_argument("--tune", action="append", default=[], metavar="FIELD=VALUE",
+                    help="bench-header stage option (aqz_stage_bench_options field, e.g. "
+                         "knobs=8, nt=3, placement_mode=1); repeatable")
     ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    args.tune = {k: int(v, 0) for k, v in (t.split("=", 1) for t in args.tune)}
     if args.codec == "none" and args.compress:
         args.codec = "lz4"
 
@@ -570,7 +577,8 @@ def main():
         barrier + device sync on both sides; max over ranks."""
         kw = dict(force_levels=cfg["force_levels"], max_batch_frames=B,
                   layer_slots=layer_slots_for(cfg, B),
-                  skip_level0_split=pyramid_only, **PLACEMENT)
+                  skip_level0_split=pyramid_only, placement_tries=args.placement_tries)
+        kw.update(args.tune)
         if args.xy:
             nd = len(cfg["dims"])
             kw["storage_order"] = list(range(nd - 2)) + [nd - 1, nd - 2]
@@ -705,9 +713,19 @@ def main():
         "input_rate_frac_of_peak": round(value / world / HBM_PEAK_GBS, 4),
     }
     pl = result["roofline"]["placement"]
+    pl["placement_tries"] = args.placement_tries
     if pl.get("kept_ms_final"):
         # the steady state against the kept placement's own re-time
         pl["steady_over_kept_final"] = round(avg_ms / pl["kept_ms_final"], 4)
+    if pl.get("candidates_ms"):
+        # candidate 0 is the first allocation: what a stage created without
+        # the search (placement_tries 0) runs at -- reported beside the kept
+        # one with the same weight (same random frames, same launches)
+        c0 = pl["candidates_ms"][0]
+        result["roofline"]["candidate0_ms"] = c0
+        result["roofline"]["frac_at_candidate0"] = round(
+            alg_per_launch / (c0 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        result["roofline"]["kept_ms"] = pl["candidates_ms"][pl["kept"]]
     if probe:
         # this device's practical HBM rates, measured in this run (SURVEY
         # 8(d)): the dominant kernel against a plain streaming kernel of the

@@ -239,6 +239,18 @@ typedef struct
                                   first frame is first_frame + begin, with
                                   first_frame a multiple of the stack size.
                                   0, 0 = every plane. */
+    uint32_t placement_tries;  /* creation-time placement of the chunk-layer
+                                  rings: 0/1 = the first allocation; n > 1 =
+                                  time up to n placements on random frames
+                                  (10 launches each) and keep the fastest.
+                                  The fused kernels' launch time depends on
+                                  the physical memory the rings land in
+                                  (up to ~10% on 2-D
+                                  stages); only rings >= 256 MiB search.  The
+                                  transient peak (two ring sets, one batch of
+                                  random frames and 128 MiB spacers) is in
+                                  aqz_stage_estimate_memory. */
+    uint32_t reserved;
 } aqz_stage_options;
 
 typedef struct
@@ -438,6 +450,13 @@ aqz_status aqz_stage_compressed_offsets(aqz_stage* st, uint32_t level,
  * call returns. */
 aqz_status aqz_stage_copy_compressed_async(aqz_stage* st, uint32_t level,
                                            uint64_t layer, void* dst, size_t cap);
+/* *done = 1 once the compression of that layer has finished (no wait): then
+ * aqz_stage_compressed_offsets / _entries and aqz_stage_copy_compressed_async
+ * do not block the caller.  A consumer thread issues the frames' D2H only
+ * for finished layers, as the reference's flush jobs hand a chunk to its
+ * shard once compress_and_take_buffer returned (array.cpp:722-736). */
+aqz_status aqz_stage_compression_done(aqz_stage* st, uint32_t level, uint64_t layer,
+                                      int32_t* done);
 
 /* ---- shard packing -----------------------------------
  * The frames of a compressed layer in output order, with their place in

@@ -37,6 +37,29 @@ typedef struct
                                   (peak: 2 ring sets + the spacers);
                                   1: every candidate is held (peak: n sets) */
     uint64_t placement_spacer_bytes; /* mode 0 spacer (0 = 128 MiB) */
+    uint32_t placement_reps;   /* timed launches per candidate (0 = 10) */
+    /* Kernel tuning for A/B runs.  The library reads none of these from the
+     * environment: a stage made by aqz_stage_create always runs the shipped
+     * kernels.  Knob bits that skip stores (timing experiments only) exist
+     * only here. */
+    uint32_t knobs;            /* kernel A/B switches (0 = shipped kernels) */
+    uint32_t nt_policy;        /* 0 = shipped (7); 8 | p = nontemporal policy p
+                                  (bit 0 input loads, 1 level-0 stores,
+                                  2 level-1/2 stores) */
+    uint32_t xcd_rot;          /* regions each XCD's walk is rotated by */
+    uint32_t region_rows_log2; /* 0 = automatic */
+    uint32_t zstd_flags;       /* device zstd encoder A/B (frames still decode):
+                                  1 literals only (no LZ matches: the serial
+                                  model's byte-exact mode), 2 no far
+                                  candidates, 4 predefined sequence tables
+                                  only; bits 8-15 the parse history, bits
+                                  16-19 parse variants */
+    uint32_t ring_malloc_flags; /* hipExtMallocWithFlags flags of the chunk-layer
+                                   rings (0 = hipMalloc) */
+    uint64_t chunk_pad_bytes;  /* device bytes added between the chunks of a
+                                  resident layer (chunk_pitch) */
+    uint64_t ring_spacer_bytes; /* a device allocation (ring_malloc_flags) made
+                                   before the rings and freed after them */
 } aqz_stage_bench_options;
 
 /* aqz_stage_estimate_memory including the placement search's transient
@@ -68,6 +91,12 @@ aqz_status aqz_stage_create_bench(const aqz_array_desc* desc,
 
 /* Kernel A/B switches for tuning runs (0, 0 = the shipped kernels). */
 aqz_status aqz_stage_set_tuning(aqz_stage* st, uint32_t knobs, uint32_t nt);
+
+/* Placement experiments: allocate fresh chunk-layer rings (with their
+ * has_data words and frame tables) for the levels whose bit is set in
+ * level_mask; the old ones stay allocated until the stage is destroyed, so
+ * the new ones land in other memory.  Ring contents are lost (timing only). */
+aqz_status aqz_stage_bench_replace_rings(aqz_stage* st, uint32_t level_mask);
 
 /* Time every launch of the dominant (fused pyramid) kernel with HIP events
  * recorded on the stream it is launched on. */

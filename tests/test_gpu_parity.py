@@ -161,14 +161,16 @@ def test_downsampler_metadata_and_errors(gpu):
 # ---------------------------------------------------------------------------
 # Stage: level-0 tile split + pyramid + tile split of every level
 # ---------------------------------------------------------------------------
-def _run_stage(gpu, dims, dtype, method, frames, max_levels=0, batch=0, chunks=None):
-    # keep every chunk layer of the run resident so all can be checked
+def _run_stage(gpu, dims, dtype, method, frames, max_levels=0, batch=0, chunks=None,
+               knobs=0):
+    # keep every chunk layer of the run resident so all can be checked;
+    # knobs: the bench-header kernel switches (aqz_stage_bench_options)
     f0 = dims[0][2]
     for d in dims[1:-2]:
         f0 *= d[1]
     slots = -(-len(frames) // f0) + 2
     st = gpu.Stage(dims, dtype, method, max_levels=max_levels,
-                   max_batch_frames=batch, layer_slots=slots)
+                   max_batch_frames=batch, layer_slots=slots, knobs=knobs)
     if chunks is None:
         st.append(frames)
     else:
@@ -310,41 +312,40 @@ def test_stage_timing_marks(gpu):
 # the register-cascade kernel (fused_pyramid_strip3d; tuning knob 512: its
 # variant without the next-plane prefetch) and, with knob 256, the
 # LDS-cascade kernel it replaced (fused_pyramid_3d)
-KERNELS_3D = {"strip3d": ("0", "fused_pyramid_strip3d"),
-              "strip3d_nopf": ("512", "fused_pyramid_strip3d"),
-              "lds3d": ("256", "fused_pyramid_3d")}
+KERNELS_3D = {"strip3d": (0, "fused_pyramid_strip3d"),
+              "strip3d_nopf": (512, "fused_pyramid_strip3d"),
+              "lds3d": (256, "fused_pyramid_3d")}
 
 
 @pytest.mark.parametrize("kernel", sorted(KERNELS_3D))
 @pytest.mark.parametrize("dtype", [U8, U16, I16, U32, F32], ids=lambda d: DTYPE_NAMES[d])
-def test_stage_3d_fused_regular(gpu, monkeypatch, dtype, kernel):
+def test_stage_3d_fused_regular(gpu, dtype, kernel):
     # every level halves x, y and z: G = 8 planes per workgroup
     knobs, name = KERNELS_3D[kernel]
-    monkeypatch.setenv("AQZ_KNOBS", knobs)
     dims = [(TIME, 0, 1, 1), (CHANNEL, 2, 1, 1), (SPACE, 32, 4, 1),
             (SPACE, 512, 64, 1), (SPACE, 512, 64, 1)]
-    st = gpu.Stage(dims, dtype, MEAN)
+    st = gpu.Stage(dims, dtype, MEAN, knobs=knobs)
     assert st.dominant_kernel() == name
     st.close()
     for m in ALL_METHODS:
         frames = _frames(dtype, 2 * 32, 512, 512, 40 + m + dtype)
         # appends that leave and regain group alignment (fused <-> generic)
-        _check_stage(gpu, dims, dtype, m, frames, batch=16, chunks=[3, 13, 32, 16])
+        _check_stage(gpu, dims, dtype, m, frames, batch=16, chunks=[3, 13, 32, 16],
+                     knobs=knobs)
 
 
 @pytest.mark.parametrize("kernel", sorted(KERNELS_3D))
-def test_stage_c4_volume(gpu, monkeypatch, kernel):
+def test_stage_c4_volume(gpu, kernel):
     # BASELINE configs[3] level structure (z 64 -> 32 -> 16 -> 16 with
     # 16-plane z chunks; xy 2048 -> 256 with 256-px chunks): fused 2x2x2
     knobs, name = KERNELS_3D[kernel]
-    monkeypatch.setenv("AQZ_KNOBS", knobs)
     dims = [(TIME, 0, 1, 1), (SPACE, 64, 16, 1), (SPACE, 2048, 256, 1),
             (SPACE, 2048, 256, 1)]
     frames = synthetic_frames(U16, 64, 2048, 2048, 77)
-    st = gpu.Stage(dims, U16, MEAN)
+    st = gpu.Stage(dims, U16, MEAN, knobs=knobs)
     assert st.dominant_kernel() == name
     st.close()
-    _check_stage(gpu, dims, U16, MEAN, frames, batch=32)
+    _check_stage(gpu, dims, U16, MEAN, frames, batch=32, knobs=knobs)
 
 
 @pytest.mark.parametrize("kernel", sorted(KERNELS_3D))
@@ -354,20 +355,19 @@ def test_stage_c4_volume(gpu, monkeypatch, kernel):
     # 3 levels (two fused levels, G = 4)
     ([(TIME, 0, 1, 1), (SPACE, 8, 2, 1), (SPACE, 1024, 256, 1), (SPACE, 1024, 256, 1)], 3),
 ], ids=["2lvl", "3lvl"])
-def test_stage_3d_shallow(gpu, monkeypatch, kernel, dims, levels):
+def test_stage_3d_shallow(gpu, kernel, dims, levels):
     """Shallow 2x2x2 pyramids (1 or 2 fused levels) through every 2x2x2
     kernel: the strip kernel's early exits after level 1 / level 2."""
     knobs, name = KERNELS_3D[kernel]
-    monkeypatch.setenv("AQZ_KNOBS", knobs)
     h = dims[-2][1]
     for dtype in (U8, U16, F32):
-        st = gpu.Stage(dims, dtype, MEAN)
+        st = gpu.Stage(dims, dtype, MEAN, knobs=knobs)
         assert st.dominant_kernel() == name
         assert st.n_levels() == levels
         st.close()
         for m in ALL_METHODS:
             frames = _frames(dtype, 16, h, h, 7 + m + dtype)
-            _check_stage(gpu, dims, dtype, m, frames, batch=8)
+            _check_stage(gpu, dims, dtype, m, frames, batch=8, knobs=knobs)
 
 
 @pytest.mark.parametrize("dtype", [U8, U16, F32], ids=lambda d: DTYPE_NAMES[d])
@@ -469,19 +469,19 @@ def test_stage_z_slab_rejects_misaligned(gpu):
 
 
 @pytest.mark.parametrize("pad", [0, 4224])
-def test_stage_async_handoff_pinned_and_pageable(gpu, pad, monkeypatch):
+def test_stage_async_handoff_pinned_and_pageable(gpu, pad):
     """The ingestion / hand-off pipeline: pinned and pageable (multi-threaded
     staging copy) host sources, H2D on the copy stream, and every chunk layer
     handed off with copy_layer_async while the 3-slot ring wraps several
     times -- the copies must see each layer whole (a slot is not rewritten
     before its D2H has finished).  pad > 0: chunks `bpc + pad` apart on the
-    device (AQZ_CHUNK_PAD), packed back to bpc by the strided D2H."""
-    monkeypatch.setenv("AQZ_CHUNK_PAD", str(pad))
+    device (bench option chunk_pad_bytes), packed back to bpc by the strided
+    D2H."""
     dims = [(TIME, 0, 2, 1), (SPACE, 1024, 128, 1), (SPACE, 1024, 128, 1)]
     n, B = 20, 4
     frames = synthetic_frames(U16, n, 1024, 1024, 31)
     exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
-    st = gpu.Stage(dims, U16, MEAN, layer_slots=2, max_batch_frames=B)
+    st = gpu.Stage(dims, U16, MEAN, layer_slots=2, max_batch_frames=B, chunk_pad_bytes=pad)
     L = st.n_levels()
     lay = [st.layout(l) for l in range(L)]
     assert all(x["chunk_pitch"] == x["bytes_per_chunk"] + pad for x in lay)
@@ -576,15 +576,14 @@ def test_stage_storage_dimension_order(gpu, perm):
 # kernel's loads (load_region_xy): storage rows = acquisition X (chunk 128,
 # so 64-row regions), 4 levels, interior and edge regions; knob 4096 forces
 # the separate transpose_frames pass, whose output must be the same.
-XY_KERNELS = {"fused": ("0", "fused_pyramid_strip (XY load)"),
-              "pass": ("4096", "transpose_frames + fused_pyramid_strip")}
+XY_KERNELS = {"fused": (0, "fused_pyramid_strip (XY load)"),
+              "pass": (4096, "transpose_frames + fused_pyramid_strip")}
 
 
 @pytest.mark.parametrize("path", sorted(XY_KERNELS))
 @pytest.mark.parametrize("dtype", [U8, U16, I16, U32, F32], ids=lambda d: DTYPE_NAMES[d])
-def test_stage_xy_fused_strip(gpu, monkeypatch, dtype, path):
+def test_stage_xy_fused_strip(gpu, dtype, path):
     knobs, name = XY_KERNELS[path]
-    monkeypatch.setenv("AQZ_KNOBS", knobs)
     # acquisition Y x X = 1000 x 1088 -> storage 1088 rows x 1000 columns
     acq = [(TIME, 0, 4, 1), (SPACE, 1000, 128, 1), (SPACE, 1088, 128, 1)]
     methods = [MEAN, MIN] if path == "fused" else [MEAN]
@@ -593,7 +592,7 @@ def test_stage_xy_fused_strip(gpu, monkeypatch, dtype, path):
         stored = np.ascontiguousarray(frames.transpose(0, 2, 1))
         exp, fw, ldims = expected_stage_layers([acq[0], acq[2], acq[1]], dtype, m, stored)
         st = gpu.Stage(acq, dtype, m, storage_order=[0, 2, 1], max_batch_frames=4,
-                       layer_slots=4)
+                       layer_slots=4, knobs=knobs)
         assert st.dominant_kernel() == name
         assert st.n_levels() >= 4
         st.append(frames[:4])
@@ -621,4 +620,32 @@ def test_stage_xy_transpose_sizes(gpu, dtype):
         got, gflags = st.copy_layer(l, layer)
         assert_same_pixels(got, buf, dtype, f"L{l} layer{layer}")
         assert (gflags == flags).all()
+    st.close()
+
+
+@pytest.mark.parametrize("env", [{"AQZ_KNOBS": "8"}, {"AQZ_KNOBS": "32"},
+                                 {"AQZ_KNOBS": "4", "AQZ_NT": "0",
+                                  "AQZ_REGION_ROWS_LOG2": "4", "AQZ_CHUNK_PAD": "4096"}],
+                         ids=["skip-deep-levels", "skip-flags", "mixed"])
+def test_environment_cannot_change_drop_in_output(gpu, monkeypatch, env):
+    """Kernel tuning lives only in the bench header (aqz_stage_bench_options):
+    the round-3 library read AQZ_KNOBS & co. from the environment, where bit
+    8 skipped levels >= 3 and bit 32 every has_data flush.  A drop-in stage
+    made with such variables set must still be oracle-exact."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    dims = [(TIME, 0, 4, 1), (SPACE, 1024, 128, 1), (SPACE, 1024, 128, 1)]
+    frames = synthetic_frames(U16, 8, 1024, 1024, 5)
+    frames[4:] = 0  # an all-zero chunk layer: has_data must still be right
+    exp, fw, ldims = expected_stage_layers(dims, U16, MEAN, frames)
+    st = gpu.Stage(dims, U16, MEAN, layer_slots=3, max_batch_frames=8)
+    assert st.n_levels() == len(ldims) >= 4
+    assert all(st.layout(l)["chunk_pitch"] == st.layout(l)["bytes_per_chunk"]
+               for l in range(st.n_levels()))
+    st.append(frames)
+    st.finalize()
+    for (l, layer), (buf, flags) in sorted(exp.items()):
+        got, gflags = st.copy_layer(l, layer)
+        assert_same_pixels(got, buf, U16, f"env {env} L{l} layer{layer}")
+        assert (gflags == flags).all(), (l, layer)
     st.close()

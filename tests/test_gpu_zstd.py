@@ -275,10 +275,10 @@ def test_device_frames_equal_serial_model(gpu, monkeypatch, codec, shuffle, clev
     frame -- plain zstd per chunk, blosc-zstd per record of a shuffled
     block."""
     monkeypatch.setenv("AQZ_ZSTD_HOST", "0")
-    monkeypatch.setenv("AQZ_ZSTD_MATCH", "0")
     dims = [(TIME, 0, 4, 1), (SPACE, 512, 256, 1), (SPACE, 384, 128, 1)]
     frames = _frames(U16, 4, 512, 384, 77)
-    st = gpu.Stage(dims, U16, MEAN, multiscale=False, layer_slots=2, max_batch_frames=4)
+    st = gpu.Stage(dims, U16, MEAN, multiscale=False, layer_slots=2, max_batch_frames=4,
+                   zstd_flags=gpu.ZSTD_LITERALS_ONLY)
     st.append(frames)
     layer, flags = st.copy_layer(0, 0)
     bpc = st.layout(0)["bytes_per_chunk"]

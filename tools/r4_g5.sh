@@ -1,0 +1,15 @@
+# placement search variants through bench.py (fresh process each)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r4e
+mkdir -p $O
+run() { timeout -k 10 180 python3 bench.py --steps 200 --warmup 5 --no-cpu-baseline --no-pyramid-only-line --no-hbm-probe "$@" > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open('$O/tmp.json')); r=d['roofline']; p=r['placement']; print(json.dumps({'args': sys.argv[1:], 'frac': r['frac'], 'ms': r['kernel_avg_ms'], 'cand': p['candidates_ms'], 'kept': p['kept'], 'peak_gb': round(p['peak_device_bytes']/1e9,2)}))" "$@" >> $O/runs.jsonl; }
+run --placement-tries 16
+run --placement-tries 16 --tune ring_malloc_flags=4
+run --placement-tries 8 --tune placement_mode=1
+run --placement-tries 8 --tune placement_mode=1 --tune ring_malloc_flags=4
+run --placement-tries 16 --tune placement_spacer_bytes=1073741824
+run --placement-tries 16 --tune placement_spacer_bytes=4294967296 --tune ring_malloc_flags=4
+cat $O/runs.jsonl
