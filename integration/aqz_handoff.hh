@@ -4,61 +4,175 @@
 //
 // It replaces, for a multiscale array, what the reference's consumer thread
 // does per frame (MultiscaleArray::write_frame, multiscale.array.cpp:57-74,
-// 291-325, and Array::write_frame, array.cpp:153-223):
+// 291-325, and Array::write_frame, array.cpp:153-223) and what its flush
+// jobs do per chunk (Array::dispatch_chunk_job_, array.cpp:664-760):
 //
-//   * frames are copied into one of two pinned batch buffers; a full batch
-//     is appended asynchronously (aqz_stage_append reads pinned memory by
-//     DMA) and the buffer is refilled only after aqz_stage_wait_consumed
-//     says the stage has read it -- the frame queue's buffer swap
-//     (frame.queue.cpp:48-73) without a spin;
-//   * every complete unit of every level -- a dim-1 band where
-//     Array::flush_completed_bands_ applies (array.cpp:873-908), else a
-//     chunk layer -- is copied D2H asynchronously into a ring of pinned host
-//     buffers (aqz_stage_copy_band_async / aqz_stage_copy_layer_async);
-//   * a unit whose copy has landed (aqz_stage_copies_completed: hand-off
-//     tickets complete in issue order) is installed into the caller's chunk
-//     buffers and committed -- the tail of Array::write_frame that triggers
-//     flush / rollover (array.cpp:196-219) -- strictly in frame order per
-//     level.  Nothing waits for a copy except to reuse its host buffer.
+//   * frames are copied into one of two pinned batch buffers (by a few copy
+//     threads); a full batch is appended asynchronously (aqz_stage_append
+//     reads pinned memory by DMA) and the buffer is refilled only after
+//     aqz_stage_wait_consumed says the stage has read it -- the frame
+//     queue's buffer swap (frame.queue.cpp:48-73) without a spin;
+//   * every unit of every level is handed off as soon as its frames are
+//     written: a dim-1 band where Array::flush_completed_bands_ applies
+//     (array.cpp:873-908), else a chunk layer (should_flush_, array.cpp:
+//     910-922).  Raw units are copied D2H (aqz_stage_copy_band_async /
+//     aqz_stage_copy_layer_async); with a codec the whole layer is
+//     compressed on the device (aqz_stage_compress_layer, the codecs of
+//     Chunk::compress_and_take_buffer, chunk.cpp:78-106) and only its frames
+//     cross PCIe, once the compression has finished (aqz_stage_compression_
+//     done) -- the consumer thread never waits for a kernel;
+//   * a unit whose copy has landed (hand-off tickets complete in issue
+//     order) goes to the sink strictly in frame order per level, with a
+//     Lease on its host buffer: the sink's writer jobs hold the lease, and
+//     the buffer is refilled only once every lease is released.
+//
+// Device selection (no ABI change): select_device() reads
+// AQZ_DEVICE.
 #pragma once
 
 #include "aqz_gpu.h"
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
 #include <vector>
 
 namespace aqz_binding {
 
-// Where handed-off units go (GpuArray in the reference binding).
+// A reference on a host hand-off buffer.  The Handoff refills a buffer only
+// when no lease on it is alive; a sink copies the lease into every job that
+// reads the buffer after unit() returned.
+class Lease
+{
+  public:
+    Lease() = default;
+    explicit Lease(std::atomic<int>* pins)
+      : p_(pins)
+    {
+        if (p_)
+            p_->fetch_add(1);
+    }
+    Lease(const Lease& o)
+      : Lease(o.p_)
+    {
+    }
+    Lease(Lease&& o) noexcept
+      : p_(o.p_)
+    {
+        o.p_ = nullptr;
+    }
+    Lease& operator=(Lease o) noexcept
+    {
+        std::swap(p_, o.p_);
+        return *this;
+    }
+    ~Lease() { release(); }
+    void release()
+    {
+        if (p_ && p_->fetch_sub(1) == 1)
+            p_->notify_all();
+        p_ = nullptr;
+    }
+
+  private:
+    std::atomic<int>* p_ = nullptr;
+};
+
+// One handed-off unit of a level: chunk slots [c0, c0 + n_chunks) of a chunk
+// layer, raw (chunks + has_data) or compressed (frames + entries, the whole
+// layer in shard-major order).
+struct Unit
+{
+    uint32_t level = 0;
+    uint64_t layer = 0;   // chunk layer of the level (frames_written / F)
+    uint32_t band = 0, n_bands = 1;
+    uint32_t c0 = 0, n_chunks = 0;
+    uint64_t first = 0;   // the unit's first frame id of the level
+    uint64_t frames = 0;  // frames of the level inside this unit
+    bool complete = true; // false only at close: the zero-filled remainder
+    bool last_in_layer = true;
+    uint64_t bytes_per_chunk = 0;
+    // raw
+    const uint8_t* chunks = nullptr;   // n_chunks x bytes_per_chunk
+    const uint8_t* has_data = nullptr; // n_chunks bytes
+    // compressed
+    const uint8_t* data = nullptr;     // the layer's frames back to back
+    const aqz_chunk_entry* entries = nullptr; // n_chunks, shard-major
+    Lease lease;
+};
+
 struct HandoffSink
 {
     virtual ~HandoffSink() = default;
-    // chunk slots [c0, c0 + n) of level's current layer: n chunks of
-    // bytes_per_chunk bytes and their has_data bytes
-    virtual void install(uint32_t level, const uint8_t* chunks, const uint8_t* has_data,
-                         uint32_t c0, uint32_t n) = 0;
-    // `frames` more frames of level are in its chunk buffers; flush = false
-    // only for the zero-filled partial last unit (Array::close_ flushes it)
-    virtual aqz_status commit(uint32_t level, uint64_t frames, bool flush) = 0;
+    // units arrive in frame order per level; non-success stops the stream
+    virtual aqz_status unit(Unit& u) = 0;
 };
+
+struct HandoffOptions
+{
+    uint32_t batch_frames = 64; // frames per append
+    uint32_t host_slots = 2;    // host unit buffers per level (>= 1)
+    uint32_t copy_threads = 4;  // threads copying frames into the batch
+    aqz_compression comp{};     // codec 0: raw chunk units
+};
+
+// AQZ_DEVICE (a deployment setting read where the reference configures an
+// array, zarr.stream.cpp:1231-1279; no ABI change):
+//   unset or "auto"  the next device, round robin over the visible devices,
+//                    per multiscale array created by the process (BASELINE
+//                    configs[4]: one camera stream per GPU);
+//   "N"              device N;  "a,b,..." round robin over that list;
+//   "off" or "-1"    no GPU: the reference's CPU path.
+// Returns -1 for "no GPU".
+inline int32_t
+select_device(int32_t n_visible)
+{
+    static std::atomic<uint32_t> next{ 0 };
+    const char* e = std::getenv("AQZ_DEVICE");
+    std::string s = e ? e : "auto";
+    if (s == "off" || s == "-1" || n_visible <= 0)
+        return -1;
+    std::vector<int32_t> list;
+    if (s == "auto" || s.empty()) {
+        for (int32_t d = 0; d < n_visible; ++d)
+            list.push_back(d);
+    } else {
+        size_t i = 0;
+        while (i < s.size()) {
+            const size_t j = std::min(s.find(',', i), s.size());
+            const int32_t d = std::atoi(s.substr(i, j - i).c_str());
+            if (d < 0 || d >= n_visible)
+                return -1;
+            list.push_back(d);
+            i = j + 1;
+        }
+        if (list.empty())
+            return -1;
+    }
+    return list[next.fetch_add(1) % list.size()];
+}
 
 class Handoff
 {
   public:
-    // host_slots: pinned unit buffers per level (>= 1; 2-3 keep the D2H of
-    // one unit in flight while an earlier one is installed)
-    Handoff(aqz_stage* st, uint64_t frame_bytes, uint32_t batch, uint32_t host_slots,
-            HandoffSink& sink)
+    Handoff(aqz_stage* st, uint64_t frame_bytes, const HandoffOptions& o, HandoffSink& sink)
       : st_(st)
       , frame_bytes_(frame_bytes)
-      , batch_(batch)
+      , opt_(o)
       , sink_(sink)
     {
-        host_slots = std::max<uint32_t>(1, host_slots);
+        opt_.batch_frames = std::max<uint32_t>(1, opt_.batch_frames);
+        opt_.host_slots = std::max<uint32_t>(1, opt_.host_slots);
         for (int j = 0; j < 2; ++j)
-            status_ = worse(status_, aqz_host_alloc(size_t(batch_) * frame_bytes_,
+            status_ = worse(status_, aqz_host_alloc(size_t(opt_.batch_frames) * frame_bytes_,
                                                     reinterpret_cast<void**>(&buf_[j])));
         const uint32_t nl = aqz_stage_n_levels(st_);
         levels_.resize(nl);
@@ -69,26 +183,50 @@ class Handoff
             status_ = worse(status_, aqz_stage_band_geometry(st_, l, &banded, &L.n_bands,
                                                              &L.frames_per_band,
                                                              &L.chunks_per_band));
-            L.banded = banded != 0;
-            L.unit = L.banded ? L.frames_per_band : L.lay.frames_per_layer;
-            L.slots.resize(host_slots);
-            for (Slot& s : L.slots) {
-                status_ = worse(status_, aqz_host_alloc(unit_bytes(L),
-                                                        reinterpret_cast<void**>(&s.chunks)));
+            // a compressed unit is a whole layer (the device compresses
+            // layers); raw units follow the reference's dim-1 bands
+            L.compressed = opt_.comp.codec != AQZ_CODEC_NONE;
+            if (L.compressed || !banded) {
+                L.n_bands = 1;
+                L.frames_per_band = L.lay.frames_per_layer;
+                L.chunks_per_band = L.lay.chunks_per_layer;
+            }
+            const size_t cap =
+              L.compressed ? size_t(aqz_compressor_max_bytes(L.lay.bytes_per_chunk,
+                                                            L.lay.chunks_per_layer))
+                           : size_t(L.lay.bytes_per_chunk) * L.chunks_per_band;
+            for (uint32_t i = 0; i < opt_.host_slots; ++i) {
+                auto s = std::make_unique<Slot>();
+                s->cap = cap;
+                status_ = worse(status_, aqz_host_alloc(cap, reinterpret_cast<void**>(&s->buf)));
                 status_ = worse(status_, aqz_host_alloc(L.chunks_per_band,
-                                                        reinterpret_cast<void**>(&s.has)));
+                                                        reinterpret_cast<void**>(&s->has)));
+                s->ent.resize(L.chunks_per_band);
+                L.slots.push_back(std::move(s));
             }
         }
+        const uint32_t nt = std::max<uint32_t>(1, opt_.copy_threads);
+        for (uint32_t t = 1; t < nt; ++t)
+            copiers_.emplace_back([this, t] { copier_(t); });
     }
 
     ~Handoff()
     {
-        // a unit still in flight must land before its buffer is freed
+        {
+            std::lock_guard<std::mutex> lk(cmu_);
+            cstop_ = true;
+        }
+        ccv_.notify_all();
+        for (auto& t : copiers_)
+            t.join();
+        // units still in flight must land, and every lease end, before the
+        // buffers are freed
         (void)aqz_stage_wait_copies(st_);
         for (Level& L : levels_)
-            for (Slot& s : L.slots) {
-                aqz_host_free(s.chunks);
-                aqz_host_free(s.has);
+            for (auto& s : L.slots) {
+                wait_pins_(*s);
+                aqz_host_free(s->buf);
+                aqz_host_free(s->has);
             }
         for (uint8_t* b : buf_)
             aqz_host_free(b);
@@ -100,12 +238,13 @@ class Handoff
     aqz_status status() const { return status_; }
     uint64_t frames_accepted() const { return accepted_; }
 
-    // pinned host bytes held (batch buffers + unit rings)
+    // pinned host bytes held (batch buffers + unit buffers)
     size_t host_bytes() const
     {
-        size_t n = 2 * size_t(batch_) * frame_bytes_;
+        size_t n = 2 * size_t(opt_.batch_frames) * frame_bytes_;
         for (const Level& L : levels_)
-            n += L.slots.size() * (unit_bytes(L) + L.chunks_per_band);
+            for (const auto& s : L.slots)
+                n += s->cap + L.chunks_per_band;
         return n;
     }
 
@@ -120,17 +259,19 @@ class Handoff
             if (s != AQZ_STATUS_SUCCESS)
                 return status_ = s;
         }
-        std::memcpy(buf_[cur_] + size_t(n_batched_) * frame_bytes_, frame, frame_bytes_);
+        copy_frame_(buf_[cur_] + size_t(n_batched_) * frame_bytes_, frame);
         ++n_batched_;
         ++accepted_;
-        if (n_batched_ == batch_)
+        if (n_batched_ == opt_.batch_frames)
             return append_batch_();
-        return AQZ_STATUS_SUCCESS;
+        // units whose copies landed meanwhile go to the sink now
+        return retire_(false);
     }
 
     // MultiscaleArray::close_ (multiscale.array.cpp:112-135): the partial
-    // batch, the zero-filled partial last layer of every level (chunk.cpp:
-    // 8-15), every remaining unit installed.
+    // batch, the zero-filled remainder of every level's last layer (chunk.cpp:
+    // 8-15) and every remaining unit (Array::close_ flushes them, array.cpp:
+    // 374-424).
     aqz_status close()
     {
         if (status_ != AQZ_STATUS_SUCCESS)
@@ -142,45 +283,105 @@ class Handoff
         if (s != AQZ_STATUS_SUCCESS)
             return status_ = s;
         s = issue_(true);
+        if (s == AQZ_STATUS_SUCCESS)
+            s = drain_();
         if (s != AQZ_STATUS_SUCCESS)
             return status_ = s;
-        return retire_(true);
+        for (Level& L : levels_)
+            for (auto& sl : L.slots)
+                wait_pins_(*sl);
+        return AQZ_STATUS_SUCCESS;
     }
 
   private:
     struct Slot
     {
-        uint8_t* chunks = nullptr;
+        uint8_t* buf = nullptr;
         uint8_t* has = nullptr;
-        bool busy = false;
+        size_t cap = 0;
+        std::vector<aqz_chunk_entry> ent;
+        std::atomic<int> pins{ 0 };
+        bool busy = false; // compressing, or its copy in flight
     };
     struct Level
     {
         aqz_level_layout lay{};
-        bool banded = false;
+        bool compressed = false;
         uint32_t n_bands = 1, chunks_per_band = 0;
-        uint64_t frames_per_band = 0, unit = 0;
-        uint64_t issued = 0; // frames of this level handed off (copies issued)
-        std::vector<Slot> slots;
+        uint64_t frames_per_band = 0;
+        uint64_t layer = 0; // next unit to hand off: (layer, band)
+        uint32_t band = 0;
+        std::vector<std::unique_ptr<Slot>> slots;
         uint32_t next = 0;
     };
-    struct Unit
+    struct Pending
     {
-        uint32_t level, slot, band;
+        uint32_t level, slot;
+        uint64_t layer;
+        uint32_t band;
         uint64_t frames;
-        bool flush;
-        uint64_t ticket;
+        bool complete;
+        uint64_t ticket = 0; // 0: compression issued, frames not copied yet
     };
 
     static aqz_status worse(aqz_status a, aqz_status b)
     {
         return a != AQZ_STATUS_SUCCESS ? a : b;
     }
-    static size_t unit_bytes(const Level& L)
+
+    static void wait_pins_(Slot& s)
     {
-        return size_t(L.lay.bytes_per_chunk) * L.chunks_per_band;
+        for (int v = s.pins.load(); v != 0; v = s.pins.load())
+            s.pins.wait(v);
     }
 
+    // ---- frame copy into the pinned batch, split over copy_threads ----------
+    void copy_frame_(uint8_t* dst, const void* src)
+    {
+        const size_t nt = copiers_.size() + 1;
+        if (nt == 1 || frame_bytes_ < (size_t(1) << 20)) {
+            std::memcpy(dst, src, frame_bytes_);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(cmu_);
+            cdst_ = dst;
+            csrc_ = static_cast<const uint8_t*>(src);
+            cleft_ = uint32_t(nt - 1);
+            ++cgen_;
+        }
+        ccv_.notify_all();
+        copy_part_(0);
+        std::unique_lock<std::mutex> lk(cmu_);
+        cdone_cv_.wait(lk, [&] { return cleft_ == 0; });
+    }
+    void copy_part_(uint32_t t)
+    {
+        const size_t nt = copiers_.size() + 1;
+        const size_t per = (frame_bytes_ / nt + 4095) & ~size_t(4095);
+        const size_t a = std::min(frame_bytes_, per * t);
+        const size_t b = std::min(frame_bytes_, a + per);
+        if (b > a)
+            std::memcpy(cdst_ + a, csrc_ + a, b - a);
+    }
+    void copier_(uint32_t t)
+    {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(cmu_);
+        for (;;) {
+            ccv_.wait(lk, [&] { return cstop_ || cgen_ != seen; });
+            if (cstop_)
+                return;
+            seen = cgen_;
+            lk.unlock();
+            copy_part_(t);
+            lk.lock();
+            if (--cleft_ == 0)
+                cdone_cv_.notify_one();
+        }
+    }
+
+    // ---- batches and units ------------------------------------------------------
     aqz_status append_batch_()
     {
         if (n_batched_ == 0)
@@ -192,89 +393,221 @@ class Handoff
         end_[cur_] = accepted_;
         cur_ ^= 1;
         n_batched_ = 0;
-        const aqz_status h = issue_(false);
-        if (h != AQZ_STATUS_SUCCESS)
-            return status_ = h;
-        return retire_(false);
+        aqz_status h = issue_(false);
+        if (h == AQZ_STATUS_SUCCESS)
+            h = retire_(false);
+        return h == AQZ_STATUS_SUCCESS ? h : (status_ = h);
     }
 
-    // Copy every complete unit of every level D2H (final: the partial last
-    // one too) into a free host buffer of its level.
+    // Hand off every unit of every level whose frames are all written (final:
+    // also every unit of each level's last, partially written layer).  Unit
+    // (layer, band) covers the level's frames [layer F + band fpb,
+    // layer F + min((band + 1) fpb, F)): the trailing band of a ragged dim 1
+    // is complete with its layer (array.cpp:884-886).
     aqz_status issue_(bool final)
     {
         for (uint32_t l = 0; l < levels_.size(); ++l) {
             Level& L = levels_[l];
-            const uint64_t written = aqz_stage_frames_written(st_, l);
-            while (L.issued + L.unit <= written || (final && L.issued < written)) {
-                Slot& slot = L.slots[L.next];
-                while (slot.busy) { // its unit has not been installed yet
-                    const aqz_status s = retire_one_(true);
-                    if (s != AQZ_STATUS_SUCCESS)
-                        return s;
-                }
-                const uint64_t F = L.lay.frames_per_layer;
-                const uint64_t layer = L.issued / F;
-                const uint32_t band = L.banded ? uint32_t((L.issued % F) / L.unit) : 0;
-                aqz_status s;
-                if (L.banded)
-                    s = aqz_stage_copy_band_async(st_, l, layer, band, slot.chunks,
-                                                  unit_bytes(L), slot.has, L.chunks_per_band);
-                else
-                    s = aqz_stage_copy_layer_async(st_, l, layer, slot.chunks, unit_bytes(L),
-                                                   slot.has, L.chunks_per_band);
+            const uint64_t F = L.lay.frames_per_layer;
+            for (;;) {
+                const uint64_t written = aqz_stage_frames_written(st_, l);
+                const uint64_t lo = L.layer * F + uint64_t(L.band) * L.frames_per_band;
+                const uint64_t hi =
+                  L.layer * F + std::min<uint64_t>((uint64_t(L.band) + 1) * L.frames_per_band, F);
+                const bool complete = written >= hi;
+                if (!complete && !(final && written > L.layer * F))
+                    break;
+                const uint32_t si = L.next;
+                aqz_status s = take_slot_(L, *L.slots[si]);
                 if (s != AQZ_STATUS_SUCCESS)
                     return s;
-                const uint64_t n = std::min(L.unit, written - L.issued);
-                pending_.push_back(Unit{ l, L.next, band, n, n == L.unit,
-                                         aqz_stage_last_ticket(st_) });
+                Slot& slot = *L.slots[si];
+                Pending p{ l, si, L.layer, L.band,
+                           std::min(written, hi) - std::min(written, lo), complete, 0 };
+                if (L.compressed) {
+                    // the previous occupant of this layer's device frame slot
+                    // must be on its way out before the slot is rewritten
+                    s = flush_compressions_(l, L.layer);
+                    if (s == AQZ_STATUS_SUCCESS)
+                        s = aqz_stage_compress_layer(st_, l, L.layer, &opt_.comp);
+                    if (s != AQZ_STATUS_SUCCESS)
+                        return s;
+                    compressing_.push_back(p);
+                } else {
+                    const size_t cap = size_t(L.lay.bytes_per_chunk) * L.chunks_per_band;
+                    s = L.n_bands > 1
+                          ? aqz_stage_copy_band_async(st_, l, L.layer, L.band, slot.buf, cap,
+                                                      slot.has, L.chunks_per_band)
+                          : aqz_stage_copy_layer_async(st_, l, L.layer, slot.buf, cap, slot.has,
+                                                       L.chunks_per_band);
+                    if (s != AQZ_STATUS_SUCCESS)
+                        return s;
+                    p.ticket = aqz_stage_last_ticket(st_);
+                    inflight_.push_back(p);
+                }
                 slot.busy = true;
-                L.issued += n;
                 L.next = (L.next + 1) % uint32_t(L.slots.size());
+                if (++L.band == L.n_bands) {
+                    L.band = 0;
+                    ++L.layer;
+                }
             }
+        }
+        return advance_compressions_(false);
+    }
+
+    // Wait until a host slot is free: neither compressing nor in flight, and
+    // no lease on it.
+    aqz_status take_slot_(Level& L, Slot& slot)
+    {
+        (void)L;
+        while (slot.busy) {
+            const aqz_status s = progress_(true);
+            if (s != AQZ_STATUS_SUCCESS)
+                return s;
+        }
+        wait_pins_(slot);
+        return AQZ_STATUS_SUCCESS;
+    }
+
+    // Compressed layers of level l that share the device frame slot of
+    // `layer` (layer - layer_slots and earlier) get their D2H issued.
+    aqz_status flush_compressions_(uint32_t l, uint64_t layer)
+    {
+        const uint64_t ns = std::max<uint32_t>(1, levels_[l].lay.layer_slots);
+        for (;;) {
+            bool found = false;
+            for (const Pending& p : compressing_)
+                found |= p.level == l && p.layer + ns <= layer;
+            if (!found)
+                return AQZ_STATUS_SUCCESS;
+            const aqz_status s = advance_compressions_(true);
+            if (s != AQZ_STATUS_SUCCESS)
+                return s;
+        }
+    }
+
+    // Finished compressions (oldest first; block: the oldest one at least)
+    // get their frames copied D2H.
+    aqz_status advance_compressions_(bool block)
+    {
+        while (!compressing_.empty()) {
+            Pending p = compressing_.front();
+            if (!block) {
+                int32_t done = 0;
+                const aqz_status s = aqz_stage_compression_done(st_, p.level, p.layer, &done);
+                if (s != AQZ_STATUS_SUCCESS)
+                    return s;
+                if (!done)
+                    return AQZ_STATUS_SUCCESS;
+            }
+            Slot& slot = *levels_[p.level].slots[p.slot];
+            aqz_status s =
+              aqz_stage_copy_compressed_async(st_, p.level, p.layer, slot.buf, slot.cap);
+            if (s != AQZ_STATUS_SUCCESS)
+                return s;
+            p.ticket = aqz_stage_last_ticket(st_);
+            compressing_.pop_front();
+            inflight_.push_back(p);
+            block = false;
         }
         return AQZ_STATUS_SUCCESS;
     }
 
-    // Install the oldest pending unit (wait: block until its copy landed;
-    // else only if it has).  Tickets complete in issue order, so pending_ is
-    // retired in frame order per level.
+    // One step: landed units to the sink; with block, wait for the oldest
+    // copy (or compression) when nothing has landed.
+    aqz_status progress_(bool block)
+    {
+        aqz_status s = advance_compressions_(false);
+        if (s != AQZ_STATUS_SUCCESS)
+            return s;
+        const size_t before = inflight_.size() + compressing_.size();
+        s = retire_(false);
+        if (s != AQZ_STATUS_SUCCESS || !block)
+            return s;
+        if (inflight_.size() + compressing_.size() < before)
+            return AQZ_STATUS_SUCCESS;
+        if (!inflight_.empty())
+            return retire_one_(true);
+        if (!compressing_.empty())
+            return advance_compressions_(true);
+        return AQZ_STATUS_INTERNAL_ERROR; // waiting for a slot nothing holds
+    }
+
+    // Deliver the oldest in-flight unit (wait: block until its copy landed;
+    // else only if it has).  Tickets complete in issue order, and per level
+    // they are issued in frame order.
     aqz_status retire_one_(bool wait)
     {
-        if (pending_.empty())
+        if (inflight_.empty())
             return AQZ_STATUS_SUCCESS;
-        const Unit u = pending_.front();
+        const Pending p = inflight_.front();
         if (wait) {
-            const aqz_status s = aqz_stage_wait_ticket(st_, u.ticket);
+            const aqz_status s = aqz_stage_wait_ticket(st_, p.ticket);
             if (s != AQZ_STATUS_SUCCESS)
                 return s;
-        } else if (aqz_stage_copies_completed(st_) < u.ticket) {
+        } else if (aqz_stage_copies_completed(st_) < p.ticket) {
             return AQZ_STATUS_SUCCESS;
         }
-        pending_.pop_front();
-        Level& L = levels_[u.level];
-        Slot& slot = L.slots[u.slot];
-        sink_.install(u.level, slot.chunks, slot.has, u.band * L.chunks_per_band,
-                      L.chunks_per_band);
+        inflight_.pop_front();
+        Level& L = levels_[p.level];
+        Slot& slot = *L.slots[p.slot];
+        Unit u;
+        u.level = p.level;
+        u.layer = p.layer;
+        u.band = p.band;
+        u.n_bands = L.n_bands;
+        u.c0 = p.band * L.chunks_per_band;
+        u.n_chunks = L.chunks_per_band;
+        u.first = p.layer * L.lay.frames_per_layer + uint64_t(p.band) * L.frames_per_band;
+        u.frames = p.frames;
+        u.complete = p.complete;
+        u.last_in_layer = p.band + 1 == L.n_bands;
+        u.bytes_per_chunk = L.lay.bytes_per_chunk;
+        if (L.compressed) {
+            const aqz_status s = aqz_stage_compressed_entries(st_, p.level, p.layer,
+                                                              slot.ent.data(), slot.ent.size());
+            if (s != AQZ_STATUS_SUCCESS)
+                return s;
+            u.data = slot.buf;
+            u.entries = slot.ent.data();
+        } else {
+            u.chunks = slot.buf;
+            u.has_data = slot.has;
+        }
+        u.lease = Lease(&slot.pins);
         slot.busy = false;
-        return sink_.commit(u.level, u.frames, u.flush);
+        return sink_.unit(u);
     }
 
     aqz_status retire_(bool wait_all)
     {
-        while (!pending_.empty()) {
-            const uint64_t before = pending_.size();
+        while (!inflight_.empty()) {
+            const size_t before = inflight_.size();
             const aqz_status s = retire_one_(wait_all);
             if (s != AQZ_STATUS_SUCCESS)
                 return status_ = s;
-            if (pending_.size() == before) // the oldest copy is still in flight
+            if (inflight_.size() == before) // the oldest copy is still in flight
                 break;
+        }
+        return AQZ_STATUS_SUCCESS;
+    }
+
+    aqz_status drain_()
+    {
+        while (!compressing_.empty() || !inflight_.empty()) {
+            aqz_status s = advance_compressions_(inflight_.empty());
+            if (s == AQZ_STATUS_SUCCESS)
+                s = retire_(true);
+            if (s != AQZ_STATUS_SUCCESS)
+                return s;
         }
         return AQZ_STATUS_SUCCESS;
     }
 
     aqz_stage* st_;
     const uint64_t frame_bytes_;
-    const uint32_t batch_;
+    HandoffOptions opt_;
     HandoffSink& sink_;
     aqz_status status_ = AQZ_STATUS_SUCCESS;
     uint8_t* buf_[2] = { nullptr, nullptr };
@@ -283,7 +616,17 @@ class Handoff
     uint32_t n_batched_ = 0;
     uint64_t accepted_ = 0;
     std::vector<Level> levels_;
-    std::deque<Unit> pending_;
+    std::deque<Pending> compressing_; // compression issued, in issue order
+    std::deque<Pending> inflight_;    // copies issued, in ticket order
+    // frame copy threads
+    std::vector<std::thread> copiers_;
+    std::mutex cmu_;
+    std::condition_variable ccv_, cdone_cv_;
+    bool cstop_ = false;
+    uint64_t cgen_ = 0;
+    uint32_t cleft_ = 0;
+    uint8_t* cdst_ = nullptr;
+    const uint8_t* csrc_ = nullptr;
 };
 
 } // namespace aqz_binding

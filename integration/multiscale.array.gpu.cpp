@@ -6,26 +6,28 @@
 // headers (tests/test_abi_pin_cpu.py), so every member it touches exists
 // with the type used here.
 //
-//   GpuArray            : zarr::Array (array.hh:12-104) that accepts chunk
-//                         layers (or dim-1 bands) filled on the GPU instead
-//                         of running write_frame_to_chunks_ (array.cpp:
-//                         507-622), then runs the reference's own flush /
-//                         rollover / band logic (array.cpp:196-219, 762-908).
+//   GpuArray            : zarr::Array (array.hh:12-104) whose chunks arrive
+//                         from the GPU -- raw, or already compressed on the
+//                         device -- instead of from write_frame_to_chunks_
+//                         (array.cpp:507-622) and Chunk::compress_and_take_
+//                         buffer (chunk.cpp:78-106).  Each chunk goes to its
+//                         Shard with write_chunk / skip_chunk on the thread
+//                         pool, with the reference's retries, ragged-padding
+//                         skips, layer advance and rollover (array.cpp:
+//                         664-908).
 //   GpuMultiscaleArray  : zarr::MultiscaleArray (multiscale.array.hh:9-65)
 //                         whose write_frame (multiscale.array.cpp:57-74)
 //                         appends frames to the aqz stage -- level-0 tile
-//                         split, Downsampler::add_frame and every level's
-//                         tile split on the device -- and hands completed
-//                         layers to the per-level GpuArrays through the
-//                         asynchronous hand-off of aqz_handoff.hh.  Metadata
-//                         (zarr.json, OME multiscales) stays the reference's:
-//                         the base class keeps its Downsampler for level
-//                         geometry and get_metadata(), which aqz reproduces
-//                         byte for byte.
-//
-// ZarrStream_s::configure_array_ (zarr.stream.cpp:1231-1279) constructs a
-// GpuMultiscaleArray instead of zarr::make_array's MultiscaleArray when the
-// array is multiscale and a device is present.
+//                         split, Downsampler::add_frame, every level's tile
+//                         split and the chunk codec on the device -- and
+//                         hands every unit to the per-level GpuArrays through
+//                         aqz_handoff.hh.  Metadata (zarr.json, OME
+//                         multiscales) stays the reference's: the base class
+//                         keeps its Downsampler for level geometry and
+//                         get_metadata(), which aqz reproduces byte for byte.
+//   make_gpu_multiscale_array : the hook ZarrStream_s::configure_array_
+//                         (zarr.stream.cpp:1231-1279) calls before
+//                         zarr::make_array; nullptr = the reference path.
 #include "array.hh"
 #include "macros.hh"
 #include "multiscale.array.hh"
@@ -34,67 +36,153 @@
 #include "aqz_gpu.h"
 #include "aqz_handoff.hh"
 
+#include <chrono>
+#include <cmath>
 #include <memory>
+#include <thread>
 #include <vector>
 
 namespace zarr {
+
+// ZarrCompressionSettings as the reference applies them (compression_params,
+// zarr.stream.cpp:191-208; chunk.cpp:78-106) -> the device codec.
+inline aqz_compression
+aqz_codec_for(const std::optional<CompressionParams>& params)
+{
+    aqz_compression c{ AQZ_CODEC_NONE, 0, 0 };
+    if (!params)
+        return c;
+    if (const auto* b = std::get_if<BloscCompressionParams>(&*params)) {
+        c.codec = b->codec_id == "zstd" ? AQZ_CODEC_BLOSC_ZSTD : AQZ_CODEC_BLOSC_LZ4;
+        c.clevel = b->clevel;
+        c.shuffle = b->shuffle;
+    } else if (const auto* z = std::get_if<ZstdCompressionParams>(&*params)) {
+        c.codec = AQZ_CODEC_ZSTD;
+        c.clevel = z->level;
+    }
+    return c;
+}
 
 class GpuArray final : public Array
 {
   public:
     using Array::Array;
 
-    // Chunk slots [c0, c0 + n) of the current layer from a handed-off
-    // buffer (n chunks of bytes_per_chunk) and their has_data bytes.  An
-    // all-zero chunk keeps an empty slot, which dispatch_chunk_job_ skips
-    // exactly like a chunk whose has_data is false (array.cpp:713-720).
-    void install_chunks(const uint8_t* chunks, const uint8_t* has_data, uint32_t c0,
-                        uint32_t n)
+    // Every chunk of a handed-off unit to its shard: the chunk job of
+    // Array::dispatch_chunk_job_ (array.cpp:664-760) with the bytes already
+    // made -- raw when no codec is configured, else the device's frame -- and
+    // Shard::skip_chunk for a chunk without data (array.cpp:713-720).  On the
+    // layer's last unit the ragged-padding slots of every shard are skipped
+    // (array.cpp:771-790, 852-862) so each shard's countdown completes.
+    void write_unit(const aqz_binding::Unit& u)
     {
-        const size_t bpc = config_->dimensions->bytes_per_chunk();
-        const size_t bpp = bytes_of_type(config_->dtype);
-        for (uint32_t i = 0; i < n; ++i) {
-            const uint32_t c = c0 + i;
-            std::unique_lock lock(chunk_mutexes_[c]);
-            if (!has_data[i]) {
-                chunks_[c].reset();
-                continue;
+        if (data_paths_.empty())
+            make_shards_();
+        const auto& dims = config_->dimensions;
+        const uint32_t chunk_offset = current_layer_ * dims->number_of_chunks_in_memory();
+        for (uint32_t i = 0; i < u.n_chunks; ++i) {
+            uint32_t local;
+            const uint8_t* p;
+            size_t n;
+            if (u.entries) {
+                const aqz_chunk_entry& e = u.entries[i];
+                local = e.chunk;
+                p = u.data + e.offset;
+                n = e.nbytes;
+            } else {
+                local = u.c0 + i;
+                p = u.chunks + size_t(i) * u.bytes_per_chunk;
+                n = u.has_data[i] ? u.bytes_per_chunk : 0;
             }
-            auto chunk = std::make_shared<Chunk>(bpc, bpp);
-            // one "row" of the whole chunk: Chunk's only writer
-            chunk->write_tile_rows(0, chunks + size_t(i) * bpc, bpc, bpc, bpc, 1);
-            chunks_[c] = std::move(chunk);
+            const uint32_t chunk_idx = chunk_offset + local;
+            const uint32_t shard_idx = dims->shard_index_for_chunk(chunk_idx);
+            const uint32_t internal_idx = dims->shard_internal_index(chunk_idx);
+            if (n == 0)
+                dispatch_skip_job_(shards_[shard_idx], internal_idx, shard_idx);
+            else
+                dispatch_bytes_job_(shards_[shard_idx], chunk_idx, internal_idx, shard_idx, p,
+                                    n, u.lease);
         }
+        if (u.last_in_layer)
+            for (uint32_t s = 0; s < dims->number_of_shards(); ++s)
+                for (const auto& idx :
+                     dims->skipped_internal_indices_for_shard_layer(s, current_layer_))
+                    dispatch_skip_job_(shards_[s], idx, s);
     }
 
-    // `frames` more frames are in the chunk buffers: the tail of
-    // Array::write_frame after write_frame_to_chunks_ (array.cpp:196-219).
-    // flush = false only for the zero-filled partial last layer, which
-    // Array::close_ flushes (array.cpp:380-387).
-    WriteResult commit_frames(uint64_t frames, bool flush = true)
+    // `frames` more frames are in the shards: the tail of Array::write_frame
+    // (array.cpp:196-219) with the layer advance of compress_and_flush_data_
+    // (:799-803) / flush_completed_bands_ (:888-898).  The last, partial
+    // layer at close is already written, so close_ has nothing to flush.
+    WriteResult commit_unit(const aqz_binding::Unit& u)
     {
-        const uint64_t nbytes = frames * bytes_per_frame_;
+        const uint64_t nbytes = u.frames * bytes_per_frame_;
         if (max_bytes_ > 0 && total_bytes_written_ + nbytes > max_bytes_)
             return WriteResult::OutOfBounds;
-        last_successful_frame_id_ = frames_written_() + frames - 1;
-        bytes_to_flush_ += nbytes;
+        if (u.frames)
+            last_successful_frame_id_ = frames_written_() + u.frames - 1;
         total_bytes_written_ += nbytes;
-        if (!flush)
-            return WriteResult::Ok;
-        if (config_->dimensions->supports_dim1_banding()) {
-            CHECK(flush_completed_bands_());
-        } else if (should_flush_()) {
-            CHECK(compress_and_flush_data_());
+        bytes_to_flush_ = 0;
+        flushed_band_count_ = u.last_in_layer ? 0 : u.band + 1;
+        if (u.last_in_layer && u.complete) {
             if (should_rollover_()) {
                 rollover_();
                 CHECK(write_metadata_());
+                current_layer_ = 0;
+            } else {
+                ++current_layer_;
             }
-            bytes_to_flush_ = 0;
         }
         return WriteResult::Ok;
     }
 
-    bool close_array() { return close_(); }
+  private:
+    void dispatch_bytes_job_(std::shared_ptr<Shard> shard,
+                             uint32_t chunk_idx,
+                             uint32_t internal_idx,
+                             uint32_t shard_idx,
+                             const uint8_t* bytes,
+                             size_t nbytes,
+                             aqz_binding::Lease lease)
+    {
+        write_counter_.fetch_add(1);
+        write_counter_cv_.notify_all();
+        auto job = [this, shard, chunk_idx, internal_idx, shard_idx, bytes, nbytes,
+                    lease = std::move(lease)](std::string& err) mutable {
+            ThreadPool::TaskResult result = ThreadPool::TaskResult::Success;
+            try {
+                // Shard::write_chunk takes a vector (shard.hh:38); the copy
+                // out of the pinned hand-off buffer runs here, on the pool
+                const std::vector<uint8_t> buffer(bytes, bytes + nbytes);
+                lease.release();
+                constexpr size_t n_retries = 3;
+                bool ok = false;
+                for (size_t retry = 0; retry < n_retries && !ok; ++retry) {
+                    ok = shard->write_chunk(internal_idx, buffer);
+                    if (!ok)
+                        std::this_thread::sleep_for(std::chrono::milliseconds(
+                          static_cast<int>(std::pow(10, retry))));
+                }
+                if (!ok) {
+                    err = "Failed to write chunk " + std::to_string(chunk_idx) + " of shard " +
+                          std::to_string(shard_idx) + " after " + std::to_string(n_retries) +
+                          " attempts";
+                    result = ThreadPool::TaskResult::Fatal;
+                }
+            } catch (const std::exception& exc) {
+                err = std::string("Failed to write chunk: ") + exc.what();
+                result = ThreadPool::TaskResult::Fatal;
+            }
+            write_counter_.fetch_sub(1);
+            write_counter_cv_.notify_all();
+            return result;
+        };
+        if (thread_pool_->n_threads() == 1 || !thread_pool_->push_job(job)) {
+            if (!thread_pool_->execute_job_with_retry(std::move(job), 2))
+                LOG_ERROR("Failed to write chunk ", chunk_idx, " (internal index ",
+                          internal_idx, ") of shard ", shard_idx);
+        }
+    }
 };
 
 class GpuMultiscaleArray final
@@ -103,19 +191,20 @@ class GpuMultiscaleArray final
 {
   public:
     // settings: the ZarrArraySettings the stream was configured with
-    // (acquisition-order dims + storage order, zarr.types.h:157-169).
+    // (acquisition-order dims + storage order, zarr.types.h:157-169);
+    // device: a HIP device ordinal (aqz_binding::select_device).
     GpuMultiscaleArray(std::shared_ptr<ArrayConfig> config,
                        std::shared_ptr<ThreadPool> thread_pool,
                        std::shared_ptr<FileHandlePool> file_handle_pool,
                        std::shared_ptr<S3ConnectionPool> s3_connection_pool,
                        const ZarrArraySettings& settings,
-                       int device,
+                       int32_t device,
                        uint32_t batch_frames = 64,
                        uint32_t host_slots = 2)
       : MultiscaleArray(config, thread_pool, file_handle_pool, s3_connection_pool)
     {
         EXPECT(downsampler_ != nullptr, "GpuMultiscaleArray needs a downsampling method");
-        // per-level writers that take GPU-filled layers (create_arrays_,
+        // per-level writers that take GPU-made chunks (create_arrays_,
         // multiscale.array.cpp:137-159, with GpuArray for Array)
         gpu_arrays_.clear();
         for (const auto& [lod, cfg] : downsampler_->writer_configurations()) {
@@ -144,13 +233,20 @@ class GpuMultiscaleArray final
         aqz_stage_options opt{};
         opt.max_batch_frames = batch_frames;
         opt.layer_slots = 2;
+        // the fused kernels' rate depends on where the chunk-layer rings
+        // land; the search's transient peak is in
+        // aqz_stage_estimate_memory
+        opt.placement_tries = 16;
         EXPECT(aqz_stage_create(&desc, &opt, &stage_) == AQZ_STATUS_SUCCESS,
-               "aqz_stage_create failed");
+               "aqz_stage_create failed: ", aqz_last_error());
         EXPECT(aqz_stage_n_levels(stage_) == arrays_.size(),
                "level count differs from the Downsampler's");
+        aqz_binding::HandoffOptions ho;
+        ho.batch_frames = batch_frames;
+        ho.host_slots = host_slots;
+        ho.comp = aqz_codec_for(config_->compression_params);
         aqz_binding::HandoffSink& sink = *this;
-        handoff_ = std::make_unique<aqz_binding::Handoff>(stage_, bytes_per_frame_,
-                                                          batch_frames, host_slots, sink);
+        handoff_ = std::make_unique<aqz_binding::Handoff>(stage_, bytes_per_frame_, ho, sink);
         EXPECT(handoff_->status() == AQZ_STATUS_SUCCESS, "aqz hand-off buffers: ",
                aqz_status_message(handoff_->status()));
     }
@@ -187,7 +283,8 @@ class GpuMultiscaleArray final
         const aqz_status s = handoff_->write_frame(frame.data());
         if (s == AQZ_STATUS_WRITE_OUT_OF_BOUNDS)
             return WriteResult::OutOfBounds;
-        EXPECT(s == AQZ_STATUS_SUCCESS, "aqz stage: ", aqz_status_message(s));
+        EXPECT(s == AQZ_STATUS_SUCCESS, "aqz stage: ", aqz_status_message(s), ": ",
+               aqz_last_error());
         bytes_written = frame.size();
         return WriteResult::Ok;
     }
@@ -197,7 +294,8 @@ class GpuMultiscaleArray final
     {
         try {
             const aqz_status s = handoff_->close();
-            EXPECT(s == AQZ_STATUS_SUCCESS, "aqz stage: ", aqz_status_message(s));
+            EXPECT(s == AQZ_STATUS_SUCCESS, "aqz stage: ", aqz_status_message(s), ": ",
+                   aqz_last_error());
         } catch (const std::exception& exc) {
             LOG_ERROR("Failed to finalize the GPU stage: ", exc.what());
             return false;
@@ -207,17 +305,17 @@ class GpuMultiscaleArray final
 
   private:
     // aqz_binding::HandoffSink: units land in frame order per level
-    void install(uint32_t level, const uint8_t* chunks, const uint8_t* has_data, uint32_t c0,
-                 uint32_t n) override
+    aqz_status unit(aqz_binding::Unit& u) override
     {
-        gpu_arrays_[level]->install_chunks(chunks, has_data, c0, n);
-    }
-
-    aqz_status commit(uint32_t level, uint64_t frames, bool flush) override
-    {
-        return gpu_arrays_[level]->commit_frames(frames, flush) == WriteResult::Ok
-                 ? AQZ_STATUS_SUCCESS
-                 : AQZ_STATUS_WRITE_OUT_OF_BOUNDS;
+        try {
+            gpu_arrays_[u.level]->write_unit(u);
+            return gpu_arrays_[u.level]->commit_unit(u) == WriteResult::Ok
+                     ? AQZ_STATUS_SUCCESS
+                     : AQZ_STATUS_WRITE_OUT_OF_BOUNDS;
+        } catch (const std::exception& exc) {
+            LOG_ERROR("Failed to write a GPU chunk unit: ", exc.what());
+            return AQZ_STATUS_INTERNAL_ERROR;
+        }
     }
 
     aqz_stage* stage_ = nullptr;
@@ -225,5 +323,37 @@ class GpuMultiscaleArray final
     std::vector<GpuArray*> gpu_arrays_;
     std::unique_ptr<aqz_binding::Handoff> handoff_;
 };
+
+// The hook of ZarrStream_s::configure_array_ (zarr.stream.cpp:1231-1279):
+//
+//     #ifdef ZARR_WITH_AQZ
+//         output->array = zarr::make_gpu_multiscale_array(
+//           config, thread_pool_, file_handle_pool_, s3_connection_pool_, *settings);
+//         if (!output->array)
+//     #endif
+//         output->array = zarr::make_array(config, thread_pool_, ...);
+//
+// A multiscale array gets the GPU stage on the device AQZ_DEVICE selects
+// (aqz_handoff.hh: round robin over the visible devices by default, one
+// stream per GPU); nullptr -- no device, AQZ_DEVICE=off, not multiscale --
+// keeps the reference's CPU path.
+inline std::unique_ptr<ArrayBase>
+make_gpu_multiscale_array(std::shared_ptr<ArrayConfig> config,
+                          std::shared_ptr<ThreadPool> thread_pool,
+                          std::shared_ptr<FileHandlePool> file_handle_pool,
+                          std::shared_ptr<S3ConnectionPool> s3_connection_pool,
+                          const ZarrArraySettings& settings)
+{
+    if (!settings.multiscale || !config->downsampling_method)
+        return nullptr;
+    int32_t n = 0;
+    if (aqz_device_count(&n) != AQZ_STATUS_SUCCESS)
+        return nullptr;
+    const int32_t device = aqz_binding::select_device(n);
+    if (device < 0)
+        return nullptr;
+    return std::make_unique<GpuMultiscaleArray>(config, thread_pool, file_handle_pool,
+                                                s3_connection_pool, settings, device);
+}
 
 } // namespace zarr

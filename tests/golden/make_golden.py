@@ -76,7 +76,56 @@ DIGEST_CASES = [
                               (ob.SPACE, 2048, 256, 1)], ob.U16, ob.MEAN, 64),
     ("c5_f32_8192_mean", [(ob.TIME, 0, 1, 1), (ob.SPACE, 8192, 128, 1), (ob.SPACE, 8192, 128, 1)],
      ob.F32, ob.MEAN, 1),
+    # round 4: the other methods, the signed / wrapping integer types and
+    # float specials at full frame sizes, and C4 at BASELINE's geometry
+    ("c2_u16_2048_min_c128", [(ob.TIME, 0, 4, 1), (ob.SPACE, 2048, 128, 1),
+                              (ob.SPACE, 2048, 128, 1)], ob.U16, ob.MIN, 2),
+    ("c2_u16_2048_max_c128", [(ob.TIME, 0, 4, 1), (ob.SPACE, 2048, 128, 1),
+                              (ob.SPACE, 2048, 128, 1)], ob.U16, ob.MAX, 2),
+    ("i8_1000x1030_mean_specials", [(ob.TIME, 0, 2, 1), (ob.SPACE, 1000, 64, 1),
+                                    (ob.SPACE, 1030, 64, 1)], ob.I8, ob.MEAN, 2),
+    ("i16_1024_mean_specials", [(ob.TIME, 0, 2, 1), (ob.SPACE, 1024, 128, 1),
+                                (ob.SPACE, 1024, 128, 1)], ob.I16, ob.MEAN, 2),
+    ("i32_1024_mean_specials", [(ob.TIME, 0, 2, 1), (ob.SPACE, 1024, 128, 1),
+                                (ob.SPACE, 1024, 128, 1)], ob.I32, ob.MEAN, 2),
+    ("u32_777x1001_max_specials", [(ob.TIME, 0, 2, 1), (ob.SPACE, 777, 64, 1),
+                                   (ob.SPACE, 1001, 64, 1)], ob.U32, ob.MAX, 2),
+    ("u64_512_mean_specials", [(ob.TIME, 0, 2, 1), (ob.SPACE, 512, 64, 1),
+                               (ob.SPACE, 512, 64, 1)], ob.U64, ob.MEAN, 2),
+    ("i64_300x700_min_specials", [(ob.TIME, 0, 2, 1), (ob.SPACE, 300, 32, 1),
+                                  (ob.SPACE, 700, 32, 1)], ob.I64, ob.MIN, 2),
+    ("f32_2048_mean_specials", [(ob.TIME, 0, 2, 1), (ob.SPACE, 2048, 128, 1),
+                                (ob.SPACE, 2048, 128, 1)], ob.F32, ob.MEAN, 2),
+    ("f32_1536_min_specials", [(ob.TIME, 0, 2, 1), (ob.SPACE, 1536, 128, 1),
+                               (ob.SPACE, 1536, 128, 1)], ob.F32, ob.MIN, 2),
+    ("f64_512_max_specials", [(ob.TIME, 0, 2, 1), (ob.SPACE, 512, 64, 1),
+                              (ob.SPACE, 512, 64, 1)], ob.F64, ob.MAX, 2),
+    ("f64_600x500_decimate_specials", [(ob.TIME, 0, 2, 1), (ob.SPACE, 600, 64, 1),
+                                       (ob.SPACE, 500, 64, 1)], ob.F64, ob.DECIMATE, 2),
+    # BASELINE configs[3] as stated: 2048 x 2048 x 256 planes, z chunk 64
+    ("c4_u16_2048x256z_mean", [(ob.TIME, 0, 1, 1), (ob.SPACE, 256, 64, 1),
+                               (ob.SPACE, 2048, 256, 1), (ob.SPACE, 2048, 256, 1)],
+     ob.U16, ob.MEAN, 256),
 ]
+
+
+def digest_frame(key, dt, h, w, seed, i):
+    """Input frame i of a digest case: splitmix64 from the case's seed, with
+    edge values sprinkled in for the *_specials cases."""
+    fr = ob.synthetic_frames(dt, 1, h, w, seed + i)
+    if key.endswith("_specials"):
+        fr = with_specials(fr, dt, seed + i + 7919, frac=0.05)
+    return fr[0]
+
+
+def frame_digest(img, dt):
+    """sha256 of a level frame; float NaNs canonicalised first (their sign
+    and payload are not part of the parity contract: tests/helpers.py)."""
+    a = np.ascontiguousarray(img)
+    if dt in (ob.F32, ob.F64):
+        a = a.copy()
+        a[np.isnan(a)] = np.nan
+    return hashlib.sha256(a.tobytes()).hexdigest()
 
 
 def digest_seed(key):
@@ -110,6 +159,12 @@ def main():
     write_metadata()
     if sys.argv[1:] == ["metadata"]:
         return
+    if sys.argv[1:] != ["digests"]:
+        write_small()
+    write_digests()
+
+
+def write_small():
     arrays = {}
     for key, dims, dt, m, frames in cascade_cases():
         ds = ob.OracleDownsampler(dims, dt, m, 0, use_ref=True)
@@ -141,20 +196,23 @@ def main():
         tiles[f"{key}/has_data"] = flags
     np.savez_compressed(os.path.join(HERE, "tile_split.npz"), **tiles)
 
+
+def write_digests():
     digests = {}
     for key, dims, dt, m, n in DIGEST_CASES:
         ds = ob.OracleDownsampler(dims, dt, m, 0, use_ref=True)
         h, w = dims[-2][1], dims[-1][1]
         seed = digest_seed(key)
         rec = {"dims": dims, "dtype": dt, "method": m, "frames": n, "seed": seed,
+               "specials": key.endswith("_specials"),
                "levels": [ds.level_dims(lvl) for lvl in range(ds.n_levels())], "out": []}
         for i in range(n):
-            fr = ob.synthetic_frames(dt, 1, h, w, seed + i)[0]
+            fr = digest_frame(key, dt, h, w, seed, i)
             ds.add_frame(fr)
             for lvl in range(1, ds.n_levels()):
                 img = ds.take_frame(lvl)
                 if img is not None:
-                    rec["out"].append([i, lvl, hashlib.sha256(img.tobytes()).hexdigest()])
+                    rec["out"].append([i, lvl, frame_digest(img, dt)])
         digests[key] = rec
         print(key, len(rec["out"]), "level frames", flush=True)
     with open(os.path.join(HERE, "digests.json"), "w") as f:

@@ -1,75 +1,200 @@
 // handoff_replay -- runs the reference-side binding's hand-off
 // (integration/aqz_handoff.hh, the code GpuMultiscaleArray drives) over the C
 // ABI with a recording sink in place of zarr::GpuArray, so the binding's
-// batching, asynchronous appends, ticketed D2H hand-off and frame-order
-// commits run on the GPU without the reference library.
+// batching, asynchronous appends, device compression, ticketed D2H hand-off
+// and frame-order commits run on the GPU without the reference library.
+// The sink does what GpuArray::write_unit does per chunk -- the bytes copied
+// out of the pinned hand-off buffer into a vector by a pool thread holding
+// the unit's lease (Shard::write_chunk takes a vector, shard.hh:38) -- and,
+// instead of a shard write, records them.
 //
-//   handoff_replay JOB OUT
+//   handoff_replay JOB OUT      (OUT "-": record nothing, time only)
 //
 // JOB (little endian, written by tests/test_gpu_handoff.py):
-//   "AQZJ", u32 ndims, ndims x {i32 type, u32 size, u32 chunk, u32 shard},
-//   i32 dtype, i32 method, u32 batch, u32 host_slots, u64 n_frames,
-//   u64 frame_bytes, n_frames frames.
-// OUT: "AQZO", u32 n_levels, then per level {u64 n_layers, u64 layer_bytes,
-//   u32 n_chunks, then per layer {u64 layer, layer bytes, has_data bytes}}.
-// stdout: one JSON line per commit and a final summary; exit 0 only if every
-// check held (commits contiguous in frame order per level, flush = false
-// only on a level's last unit, every frame committed).
+//   "AQZ2", u32 ndims, ndims x {i32 type, u32 size, u32 chunk, u32 shard},
+//   i32 dtype, i32 method, u32 batch, u32 host_slots, i32 device,
+//   i32 codec, i32 clevel, i32 shuffle, u32 copy_threads, u32 pool_threads,
+//   u32 synth (0: frames follow; 1: camera-like u16/u8 frames made here;
+//   2: random bytes made here), u32 placement_tries, u64 n_frames,
+//   u64 frame_bytes, [n_frames frames].
+// OUT: "AQZ3", u32 n_levels, then per level {u64 n, n x {u64 layer,
+//   u32 chunk, u32 shard, u32 internal, u64 nbytes, nbytes bytes}}: every
+//   chunk the sink received (nbytes 0: skipped, no data).
+// stdout: one JSON line per unit and a final summary; exit 0 only if every
+// check held: units contiguous in frame order per level, only a level's
+// last layer incomplete, every frame committed, every chunk's shard and
+// internal index equal to ArrayDimensions' (aqz_dims_*).
 #include "aqz_gpu.h"
 #include "aqz_handoff.hh"
 
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <map>
+#include <mutex>
+#include <queue>
+#include <thread>
 #include <vector>
 
 namespace {
 
-struct LevelStore
+// a minimal stand-in for zarr::ThreadPool (thread.pool.hh): FIFO jobs
+class Pool
 {
-    uint64_t F = 0, bpc = 0;
-    uint32_t n_chunks = 0;
-    uint64_t committed = 0;
-    bool closed = false; // a flush = false commit was seen
-    std::map<uint64_t, std::pair<std::vector<uint8_t>, std::vector<uint8_t>>> layers;
+  public:
+    explicit Pool(unsigned n)
+    {
+        for (unsigned i = 0; i < n; ++i)
+            t_.emplace_back([this] { run(); });
+    }
+    ~Pool()
+    {
+        drain();
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : t_)
+            t.join();
+    }
+    void push(std::function<void()> f)
+    {
+        if (t_.empty()) {
+            f();
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            q_.push(std::move(f));
+            ++pending_;
+        }
+        cv_.notify_one();
+    }
+    void drain()
+    {
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [&] { return pending_ == 0; });
+    }
+
+  private:
+    void run()
+    {
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+                if (q_.empty())
+                    return;
+                f = std::move(q_.front());
+                q_.pop();
+            }
+            f();
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0)
+                done_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> t_;
+    std::queue<std::function<void()>> q_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    size_t pending_ = 0;
+    bool stop_ = false;
+};
+
+struct Record
+{
+    uint64_t layer;
+    uint32_t chunk, shard, internal;
+    std::vector<uint8_t> bytes;
+};
+
+struct LevelState
+{
+    uint64_t F = 0, bpc = 0, committed = 0;
+    uint32_t n_chunks = 0, layers_per_shard = 1;
+    bool incomplete_seen = false;
+    uint64_t incomplete_layer = 0;
+    aqz_dims* dims = nullptr;
+    std::mutex mu;
+    std::vector<Record> rec;
 };
 
 struct RecordingSink final : aqz_binding::HandoffSink
 {
-    std::vector<LevelStore> lv;
-    bool ok = true;
-    uint64_t installs = 0;
+    std::vector<std::unique_ptr<LevelState>> lv;
+    Pool* pool = nullptr;
+    bool record = true, quiet = false;
+    std::atomic<bool> ok{ true };
+    std::atomic<uint64_t> units{ 0 }, chunk_bytes{ 0 };
 
-    void install(uint32_t level, const uint8_t* chunks, const uint8_t* has, uint32_t c0,
-                 uint32_t n) override
+    aqz_status unit(aqz_binding::Unit& u) override
     {
-        LevelStore& L = lv.at(level);
-        const uint64_t layer = L.committed / L.F;
-        auto& [buf, hd] = L.layers[layer];
-        if (buf.empty()) {
-            buf.assign(L.bpc * L.n_chunks, 0);
-            hd.assign(L.n_chunks, 0);
-        }
-        if (c0 + n > L.n_chunks) {
+        LevelState& L = *lv.at(u.level);
+        // frame order: a unit starts where the level's last one ended, and
+        // only the last layer's units may be incomplete (close)
+        if (L.incomplete_seen && (u.complete || u.layer != L.incomplete_layer))
             ok = false;
-            return;
+        if (!u.complete) {
+            L.incomplete_seen = true;
+            L.incomplete_layer = u.layer;
+        } else if (u.frames == 0) {
+            ok = false;
         }
-        std::memcpy(buf.data() + c0 * L.bpc, chunks, n * L.bpc);
-        std::memcpy(hd.data() + c0, has, n);
-        ++installs;
-    }
-
-    aqz_status commit(uint32_t level, uint64_t frames, bool flush) override
-    {
-        LevelStore& L = lv.at(level);
-        if (L.closed || frames == 0)
-            ok = false; // nothing may follow the partial last unit
-        printf("{\"level\": %u, \"first\": %llu, \"frames\": %llu, \"flush\": %s}\n", level,
-               (unsigned long long)L.committed, (unsigned long long)frames,
-               flush ? "true" : "false");
-        L.committed += frames;
-        if (!flush)
-            L.closed = true;
+        if (u.frames ? L.committed != u.first : (u.complete || u.first < L.committed))
+            ok = false;
+        if (!quiet)
+            printf("{\"level\": %u, \"layer\": %llu, \"band\": %u, \"first\": %llu, "
+                   "\"frames\": %llu, \"complete\": %s, \"compressed\": %s}\n",
+                   u.level, (unsigned long long)u.layer, u.band,
+                   (unsigned long long)L.committed, (unsigned long long)u.frames,
+                   u.complete ? "true" : "false", u.entries ? "true" : "false");
+        L.committed += u.frames;
+        ++units;
+        const uint32_t chunk_offset = uint32_t(u.layer % L.layers_per_shard) * L.n_chunks;
+        for (uint32_t i = 0; i < u.n_chunks; ++i) {
+            uint32_t local, shard, internal;
+            const uint8_t* p;
+            size_t n;
+            const uint32_t cidx0 = chunk_offset + (u.entries ? u.entries[i].chunk : u.c0 + i);
+            const uint32_t ref_shard = aqz_dims_shard_index_for_chunk(L.dims, cidx0);
+            const uint32_t ref_internal = aqz_dims_shard_internal_index(L.dims, cidx0);
+            if (u.entries) {
+                const aqz_chunk_entry& e = u.entries[i];
+                local = e.chunk;
+                shard = e.shard;
+                internal = e.internal;
+                p = u.data + e.offset;
+                n = e.nbytes;
+                if (shard != ref_shard || internal != ref_internal)
+                    ok = false;
+            } else {
+                local = u.c0 + i;
+                shard = ref_shard;
+                internal = ref_internal;
+                p = u.chunks + size_t(i) * u.bytes_per_chunk;
+                n = u.has_data[i] ? u.bytes_per_chunk : 0;
+            }
+            if (local >= L.n_chunks)
+                ok = false;
+            chunk_bytes += n;
+            // GpuArray::dispatch_bytes_job_: the copy out of the pinned buffer
+            // on a pool thread that holds the lease
+            pool->push([this, &L, layer = u.layer, local, shard, internal, p, n,
+                        lease = u.lease]() mutable {
+                std::vector<uint8_t> v(p, p + n);
+                lease.release();
+                if (record) {
+                    std::lock_guard<std::mutex> lk(L.mu);
+                    L.rec.push_back(Record{ layer, local, shard, internal, std::move(v) });
+                }
+            });
+        }
         return AQZ_STATUS_SUCCESS;
     }
 };
@@ -79,6 +204,50 @@ bool
 rd(FILE* f, T* v, size_t n = 1)
 {
     return fread(v, sizeof(T), n, f) == n;
+}
+
+uint64_t
+splitmix(uint64_t& s)
+{
+    uint64_t z = (s += 0x9e3779b97f4a7c15ull);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+// camera-like frames (smooth background + noise; bench.py run_e2e) or
+// random bytes, R distinct frames reused round robin
+std::vector<uint8_t>
+synth_frames(uint32_t kind, int32_t dtype, uint64_t fbytes, uint32_t R)
+{
+    std::vector<uint8_t> v(size_t(R) * fbytes);
+    uint64_t s = 0x5eed;
+    if (kind == 2 || (dtype != 0 && dtype != 1)) {
+        for (size_t i = 0; i + 8 <= v.size(); i += 8) {
+            const uint64_t x = splitmix(s);
+            std::memcpy(&v[i], &x, 8);
+        }
+        return v;
+    }
+    const size_t bpp = dtype == 1 ? 2 : 1;
+    const size_t n = v.size() / bpp;
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t r = splitmix(s);
+        // sum of 4 uniforms: roughly normal noise, sigma ~ 30
+        const double g = (double(r & 0xffff) + double((r >> 16) & 0xffff) +
+                          double((r >> 32) & 0xffff) + double(r >> 48)) / 65536.0 - 2.0;
+        double x = 1000.0 + 200.0 * std::sin(double(i % (n / R)) / 977.0) + 52.0 * g;
+        if (bpp == 1)
+            x /= 8.0;
+        x = std::max(0.0, std::min(bpp == 1 ? 255.0 : 65535.0, x));
+        if (bpp == 2) {
+            const uint16_t w = uint16_t(x);
+            std::memcpy(&v[i * 2], &w, 2);
+        } else {
+            v[i] = uint8_t(x);
+        }
+    }
+    return v;
 }
 
 } // namespace
@@ -95,28 +264,40 @@ main(int argc, char** argv)
         return 2;
     char magic[4];
     uint32_t nd = 0;
-    if (!rd(f, magic, 4) || memcmp(magic, "AQZJ", 4) || !rd(f, &nd) || nd > 16)
+    if (!rd(f, magic, 4) || memcmp(magic, "AQZ2", 4) || !rd(f, &nd) || nd > 16)
         return 2;
     std::vector<aqz_dimension> dims(nd);
     for (auto& d : dims)
         if (!rd(f, &d.type) || !rd(f, &d.array_size_px) || !rd(f, &d.chunk_size_px) ||
             !rd(f, &d.shard_size_chunks))
             return 2;
-    int32_t dtype, method;
-    uint32_t batch, slots;
+    int32_t dtype, method, device, codec, clevel, shuffle;
+    uint32_t batch, slots, copy_threads, pool_threads, synth, tries;
     uint64_t n_frames, fbytes;
     if (!rd(f, &dtype) || !rd(f, &method) || !rd(f, &batch) || !rd(f, &slots) ||
+        !rd(f, &device) || !rd(f, &codec) || !rd(f, &clevel) || !rd(f, &shuffle) ||
+        !rd(f, &copy_threads) || !rd(f, &pool_threads) || !rd(f, &synth) || !rd(f, &tries) ||
         !rd(f, &n_frames) || !rd(f, &fbytes))
         return 2;
-    std::vector<uint8_t> frames(n_frames * fbytes);
-    if (!rd(f, frames.data(), frames.size()))
-        return 2;
+    std::vector<uint8_t> frames;
+    uint32_t R = 0;
+    if (synth == 0) {
+        frames.resize(n_frames * fbytes);
+        if (!rd(f, frames.data(), frames.size()))
+            return 2;
+        R = uint32_t(n_frames);
+    } else {
+        R = uint32_t(std::min<uint64_t>(n_frames, 8));
+        frames = synth_frames(synth, dtype, fbytes, R);
+    }
     fclose(f);
+    const bool record = std::strcmp(argv[2], "-") != 0;
 
-    aqz_array_desc desc{ dims.data(), dims.size(), dtype, 1, method, 0, nullptr, 0 };
+    aqz_array_desc desc{ dims.data(), dims.size(), dtype, 1, method, 0, nullptr, device };
     aqz_stage_options opt{};
     opt.max_batch_frames = batch;
     opt.layer_slots = 2;
+    opt.placement_tries = tries;
     aqz_stage* st = nullptr;
     if (aqz_stage_create(&desc, &opt, &st) != AQZ_STATUS_SUCCESS) {
         fprintf(stderr, "aqz_stage_create: %s\n", aqz_last_error());
@@ -124,21 +305,41 @@ main(int argc, char** argv)
     }
     const uint32_t nl = aqz_stage_n_levels(st);
     RecordingSink sink;
-    sink.lv.resize(nl);
+    sink.record = record;
+    sink.quiet = !record;
+    Pool pool(pool_threads);
+    sink.pool = &pool;
     for (uint32_t l = 0; l < nl; ++l) {
+        auto L = std::make_unique<LevelState>();
         aqz_level_layout lay{};
         aqz_stage_level_layout(st, l, &lay);
-        sink.lv[l].F = lay.frames_per_layer;
-        sink.lv[l].bpc = lay.bytes_per_chunk;
-        sink.lv[l].n_chunks = lay.chunks_per_layer;
+        L->F = lay.frames_per_layer;
+        L->bpc = lay.bytes_per_chunk;
+        L->n_chunks = lay.chunks_per_layer;
+        aqz_stage_shard_geometry(st, l, nullptr, nullptr, &L->layers_per_shard);
+        std::vector<aqz_dimension> ld(16);
+        size_t n = 0;
+        aqz_stage_level_dims(st, l, ld.data(), ld.size(), &n);
+        if (aqz_dims_create(ld.data(), n, dtype, nullptr, &L->dims) != AQZ_STATUS_SUCCESS)
+            return 1;
+        sink.lv.push_back(std::move(L));
     }
     int rc = 0;
+    double seconds = 0;
     {
-        aqz_binding::Handoff h(st, fbytes, batch, slots, sink);
-        if (h.status() != AQZ_STATUS_SUCCESS)
+        aqz_binding::HandoffOptions ho;
+        ho.batch_frames = batch;
+        ho.host_slots = slots;
+        ho.copy_threads = copy_threads;
+        ho.comp = aqz_compression{ codec, clevel, shuffle };
+        aqz_binding::Handoff h(st, fbytes, ho, sink);
+        if (h.status() != AQZ_STATUS_SUCCESS) {
+            fprintf(stderr, "handoff: %s\n", aqz_last_error());
             return 1;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
         for (uint64_t i = 0; i < n_frames; ++i)
-            if (h.write_frame(frames.data() + i * fbytes) != AQZ_STATUS_SUCCESS) {
+            if (h.write_frame(frames.data() + (i % R) * fbytes) != AQZ_STATUS_SUCCESS) {
                 fprintf(stderr, "write_frame %llu: %s\n", (unsigned long long)i,
                         aqz_last_error());
                 return 1;
@@ -147,35 +348,50 @@ main(int argc, char** argv)
             fprintf(stderr, "close: %s\n", aqz_last_error());
             return 1;
         }
+        pool.drain(); // the writer jobs (Array::close_ waits on write_counter_)
+        seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
     for (uint32_t l = 0; l < nl; ++l)
-        if (sink.lv[l].committed != aqz_stage_frames_written(st, l)) {
+        if (sink.lv[l]->committed != aqz_stage_frames_written(st, l)) {
             fprintf(stderr, "level %u: committed %llu of %llu frames\n", l,
-                    (unsigned long long)sink.lv[l].committed,
+                    (unsigned long long)sink.lv[l]->committed,
                     (unsigned long long)aqz_stage_frames_written(st, l));
             rc = 1;
         }
     if (!sink.ok)
         rc = 1;
-    printf("{\"summary\": true, \"ok\": %s, \"installs\": %llu, \"tickets\": %llu}\n",
-           rc == 0 ? "true" : "false", (unsigned long long)sink.installs,
-           (unsigned long long)aqz_stage_last_ticket(st));
+    const double in = double(n_frames) * double(fbytes);
+    printf("{\"summary\": true, \"ok\": %s, \"units\": %llu, \"tickets\": %llu, "
+           "\"frames\": %llu, \"seconds\": %.4f, \"input_gbs\": %.3f, "
+           "\"sink_bytes_per_input_byte\": %.4f, \"codec\": %d, \"clevel\": %d, "
+           "\"shuffle\": %d, \"device\": %d, \"batch\": %u, \"copy_threads\": %u, "
+           "\"pool_threads\": %u}\n",
+           rc == 0 ? "true" : "false", (unsigned long long)sink.units.load(),
+           (unsigned long long)aqz_stage_last_ticket(st), (unsigned long long)n_frames,
+           seconds, in / seconds / 1e9, double(sink.chunk_bytes.load()) / in, codec, clevel,
+           shuffle, device, batch, copy_threads, pool_threads);
     aqz_stage_destroy(st);
+    for (auto& L : sink.lv)
+        aqz_dims_destroy(L->dims);
+    if (!record)
+        return rc;
 
     FILE* o = fopen(argv[2], "wb");
     if (!o)
         return 2;
-    fwrite("AQZO", 1, 4, o);
+    fwrite("AQZ3", 1, 4, o);
     fwrite(&nl, 4, 1, o);
-    for (const LevelStore& L : sink.lv) {
-        const uint64_t n = L.layers.size(), lb = L.bpc * L.n_chunks;
+    for (auto& L : sink.lv) {
+        const uint64_t n = L->rec.size();
         fwrite(&n, 8, 1, o);
-        fwrite(&lb, 8, 1, o);
-        fwrite(&L.n_chunks, 4, 1, o);
-        for (const auto& [layer, bh] : L.layers) {
-            fwrite(&layer, 8, 1, o);
-            fwrite(bh.first.data(), 1, bh.first.size(), o);
-            fwrite(bh.second.data(), 1, bh.second.size(), o);
+        for (const Record& r : L->rec) {
+            const uint64_t nb = r.bytes.size();
+            fwrite(&r.layer, 8, 1, o);
+            fwrite(&r.chunk, 4, 1, o);
+            fwrite(&r.shard, 4, 1, o);
+            fwrite(&r.internal, 4, 1, o);
+            fwrite(&nb, 8, 1, o);
+            fwrite(r.bytes.data(), 1, nb, o);
         }
     }
     fclose(o);

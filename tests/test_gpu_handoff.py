@@ -168,11 +168,17 @@ def test_stage_append_cuda_tensor_from_side_stream(gpu):
     st.close()
 
 
-def _run_replay(tmp_path, dims, dtype, method, frames, batch, slots):
+REPLAY = None
+
+
+def _run_replay(tmp_path, dims, dtype, method, frames, batch, slots, codec=(0, 0, 0),
+                copy_threads=4, pool_threads=4, device=0, synth=0, n_frames=None,
+                placement_tries=0, record=True):
     """tests/native/handoff_replay: the binding's hand-off
     (integration/aqz_handoff.hh, what GpuMultiscaleArray runs) over the C
-    ABI with a recording sink.  Returns (commit log, {(level, layer): (bytes,
-    has_data)})."""
+    ABI with a recording sink that does GpuArray::write_unit's per-chunk
+    copy on a thread pool.  Returns (unit log, summary, {(level, layer,
+    chunk): (shard, internal, bytes)})."""
     import json
     import os
     import struct
@@ -180,64 +186,135 @@ def _run_replay(tmp_path, dims, dtype, method, frames, batch, slots):
     exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "handoff_replay")
     assert os.path.exists(exe), "make -C tests/native (built by __graft_entry__.build)"
     job, out = tmp_path / "job.bin", tmp_path / "out.bin"
-    fb = frames[0].nbytes
+    fb = frames[0].nbytes if frames is not None else None
     with open(job, "wb") as f:
-        f.write(b"AQZJ" + struct.pack("<I", len(dims)))
+        f.write(b"AQZ2" + struct.pack("<I", len(dims)))
         for d in dims:
             f.write(struct.pack("<iIII", *d))
-        f.write(struct.pack("<iiIIQQ", dtype, method, batch, slots, len(frames), fb))
-        f.write(np.ascontiguousarray(frames).tobytes())
-    r = subprocess.run([exe, str(job), str(out)], capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        n = len(frames) if frames is not None else n_frames
+        if fb is None:
+            fb = dims[-1][1] * dims[-2][1] * {0: 1, 1: 2}[dtype]
+        f.write(struct.pack("<iiIIiiiiIIIIQQ", dtype, method, batch, slots, device, *codec,
+                            copy_threads, pool_threads, synth, placement_tries, n, fb))
+        if frames is not None:
+            f.write(np.ascontiguousarray(frames).tobytes())
+    r = subprocess.run([exe, str(job), str(out) if record else "-"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     log = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
-    assert log[-1]["summary"] and log[-1]["ok"]
+    summary = log[-1]
+    assert summary["summary"] and summary["ok"], summary
     got = {}
-    b = out.read_bytes()
-    assert b[:4] == b"AQZO"
-    (nl,), o = struct.unpack_from("<I", b, 4), 8
-    for l in range(nl):
-        n, lb, nc = struct.unpack_from("<QQI", b, o)
-        o += 20
-        for _ in range(n):
-            (layer,) = struct.unpack_from("<Q", b, o)
+    if record:
+        b = out.read_bytes()
+        assert b[:4] == b"AQZ3"
+        (nl,), o = struct.unpack_from("<I", b, 4), 8
+        for l in range(nl):
+            (nrec,) = struct.unpack_from("<Q", b, o)
             o += 8
-            got[(l, layer)] = (np.frombuffer(b, np.uint8, lb, o),
-                               np.frombuffer(b, np.uint8, nc, o + lb))
-            o += lb + nc
-    return log[:-1], got
+            for _ in range(nrec):
+                layer, chunk, shard, internal, nb = struct.unpack_from("<QIIIQ", b, o)
+                o += 28
+                key = (l, layer, chunk)
+                assert key not in got, f"chunk handed to its shard twice: {key}"
+                got[key] = (shard, internal, b[o:o + nb])
+                o += nb
+    return log[:-1], summary, got
 
 
-@pytest.mark.parametrize("case", ["banded-3d", "layers-2d-ragged"])
-def test_binding_handoff_replay(gpu, tmp_path, case):
-    """The reference-side binding's consumer path, replayed natively: frames
-    batched into pinned double buffers, asynchronous appends refilled after
-    aqz_stage_wait_consumed, every complete band / layer copied D2H into a
-    2-slot host ring and installed when its ticket completes.  Commits are
-    contiguous and in frame order per level (Array::write_frame's order,
-    array.cpp:196-219), only the partial last unit is unflushed, and every
-    installed layer equals the oracle's (MultiscaleArray::write_frame,
-    multiscale.array.cpp:57-74, 291-325)."""
-    if case == "banded-3d":
-        dims = [(TIME, 0, 1, 1), (SPACE, 64, 16, 1), (SPACE, 256, 64, 1), (SPACE, 256, 64, 1)]
-        frames = synthetic_frames(U16, 2 * 64 + 24, 256, 256, 61)  # 2 volumes + a partial
-        batch = 8
-    else:
-        dims = [(TIME, 0, 4, 1), (SPACE, 300, 64, 1), (SPACE, 260, 64, 1)]
-        frames = synthetic_frames(U16, 4 * 9 + 3, 300, 260, 62)  # ragged last layer
-        batch = 5
-    exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
-    log, got = _run_replay(tmp_path, dims, U16, MEAN, frames, batch, 2)
+def _decode(codec, frame, bpc):
+    from codec_helpers import blosc_zstd_decode, libblosc, libblosc_decode, oracle_decode, \
+        zstd_decode
+    if codec == 0:
+        return frame
+    if codec == 1:
+        out = oracle_decode(frame)
+        if libblosc():
+            assert libblosc_decode(frame) == out
+        return out
+    if codec == 2:
+        return libblosc_decode(frame) if libblosc() else blosc_zstd_decode(frame)
+    return zstd_decode(frame, bpc)
+
+
+def _check_replay(exp, fw, log, got, codec, bpc_of):
+    """Every chunk of every oracle layer reached its shard exactly once:
+    skipped iff the oracle's has_data is false, else bytes that decode to
+    the oracle's chunk; units contiguous and in frame order per level."""
     per = {}
     for e in log:
         prev = per.setdefault(e["level"], [])
         assert e["first"] == sum(x["frames"] for x in prev), e  # contiguous, in order
         prev.append(e)
-    for l, commits in per.items():
-        assert sum(c["frames"] for c in commits) == fw[l]
-        assert all(c["flush"] for c in commits[:-1])
-    if case == "banded-3d":
-        assert len(per[0]) > 2 * 4  # bands, not layers
-    assert set(got) == set(exp)
-    for key, (buf, flags) in exp.items():
-        assert_same_pixels(got[key][0].copy(), buf, U16, f"L{key[0]} layer {key[1]}")
-        assert np.array_equal(got[key][1], flags), key
+    for l, units in per.items():
+        assert sum(u["frames"] for u in units) == fw[l]
+        first_open = [i for i, u in enumerate(units) if not u["complete"]]
+        assert not first_open or all(not u["complete"] for u in units[first_open[0]:])
+    seen = set()
+    for (l, layer), (buf, flags) in exp.items():
+        bpc = bpc_of[l]
+        for c in range(len(flags)):
+            key = (l, layer, c)
+            assert key in got, f"chunk never reached its shard: {key}"
+            seen.add(key)
+            _, _, data = got[key]
+            if not flags[c]:
+                assert len(data) == 0, f"{key}: a chunk without data must be skipped"
+                continue
+            assert len(data) > 0, f"{key}: a chunk with data was skipped"
+            dec = _decode(codec[0], data, bpc)
+            assert dec == buf[c * bpc:(c + 1) * bpc].tobytes(), f"{key}: decoded bytes differ"
+    assert seen == set(got), sorted(set(got) - seen)[:5]
+
+
+REPLAY_CASES = {
+    # dim-1 bands: 3-D, chunk 1 on the append dim, z chunk 16 of 64
+    "banded-3d": ([(TIME, 0, 1, 1), (SPACE, 64, 16, 1), (SPACE, 256, 64, 1),
+                   (SPACE, 256, 64, 1)], 2 * 64 + 24, 8),
+    # ragged dim 1 (48 planes, 32-plane chunks): the trailing band holds 16
+    # frames and is complete with its layer (array.cpp:884-886)
+    "banded-ragged": ([(TIME, 0, 1, 1), (SPACE, 48, 32, 1), (SPACE, 256, 64, 2),
+                       (SPACE, 192, 64, 2)], 3 * 48 + 20, 7),
+    # 2-D, ragged tiles and a partial last layer; shards of 2 x 2 chunks
+    "layers-2d-ragged": ([(TIME, 0, 4, 2), (SPACE, 300, 64, 2), (SPACE, 260, 64, 2)],
+                         4 * 9 + 3, 5),
+}
+CODECS = {"raw": (0, 0, 0), "lz4-shuffle": (1, 5, 1), "blosc-zstd-bitshuffle": (2, 5, 2),
+          "zstd-1": (3, 1, 0), "zstd-3": (3, 3, 0)}
+
+
+@pytest.mark.parametrize("codec", sorted(CODECS))
+@pytest.mark.parametrize("case", sorted(REPLAY_CASES))
+def test_binding_handoff_replay(gpu, tmp_path, case, codec):
+    """The reference-side binding's consumer path, replayed natively: frames
+    batched into pinned double buffers by copy threads, asynchronous appends
+    refilled after aqz_stage_wait_consumed, every unit -- a raw band / layer,
+    or a layer compressed on the device and copied out once its compression
+    finished -- handed to the sink in frame order with a lease on its host
+    buffer, and every chunk copied into a vector on a pool thread as
+    GpuArray::write_unit does before Shard::write_chunk.  Every chunk of every
+    layer reaches its shard exactly once, at the shard and internal index
+    ArrayDimensions gives (checked in the replay), skipped iff it has no
+    data, and decodes to the oracle's chunk (MultiscaleArray::write_frame,
+    multiscale.array.cpp:57-74, 291-325; Array::dispatch_chunk_job_,
+    array.cpp:664-760)."""
+    from codec_helpers import libzstd
+    if CODECS[codec][0] in (2, 3) and libzstd() is None:
+        pytest.skip("no libzstd to decode with")
+    dims, n, batch = REPLAY_CASES[case]
+    h, w = dims[-2][1], dims[-1][1]
+    frames = synthetic_frames(U16, n, h, w, 61 + n)
+    if CODECS[codec][0]:
+        # compressible: keep the low bits only, with all-zero frames mixed in
+        frames &= 0x00ff
+        frames[5:9] = 0
+    exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
+    log, summary, got = _run_replay(tmp_path, dims, U16, MEAN, frames, batch, 2,
+                                    codec=CODECS[codec])
+    st = gpu.Stage(dims, U16, MEAN)
+    bpc = [st.layout(l)["bytes_per_chunk"] for l in range(st.n_levels())]
+    st.close()
+    if case.startswith("banded") and not CODECS[codec][0]:
+        assert len([e for e in log if e["level"] == 0]) > len(
+            {k[1] for k in exp if k[0] == 0})  # bands, not layers
+    _check_replay(exp, fw, log, got, CODECS[codec], bpc)
