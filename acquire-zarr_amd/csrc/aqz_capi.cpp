@@ -633,6 +633,14 @@ aqz_stage_set_tuning(aqz_stage* st, uint32_t knobs, uint32_t nt)
 }
 
 aqz_status
+aqz_stage_bind_host_thread(const aqz_stage* st)
+{
+    if (!st)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard([&] { st->st->bind_host_thread(); });
+}
+
+aqz_status
 aqz_stage_bench_replace_rings(aqz_stage* st, uint32_t level_mask)
 {
     return guard_sticky(st, [&] { st->st->replace_rings(level_mask); });

@@ -370,6 +370,8 @@ class Stage
     const char* dominant_kernel() const;
     int numa_node() const { return numa_node_; }
     size_t numa_cpus() const { return numa_cpus_.size(); }
+    // pin the calling thread to the CPUs of the device's NUMA node
+    void bind_host_thread() const { pin_current_thread(numa_cpus_); }
     // placement calibration: ms per candidate launch and the one kept
     const std::vector<double>& placement_ms() const { return placement_.ms; }
     size_t placement_best() const { return placement_.kept; }

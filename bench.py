@@ -217,7 +217,20 @@ def cpu_baseline(cfg, seconds):
         threads = 1
         how = f"C port: downsample ({L} levels) + tile split of every level, single thread"
     return {"value": round(gbs, 4), "unit": "GB/s", "cores": threads, "kind": kind,
+            "downsample_threads": 1, "split_threads": threads,
+            "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "cpu_model": cpu_model(),
             "sample": f"{n} frames of {h}x{w} {ob.DTYPE_NAMES[dt]} ({el:.1f} s): {how}"}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def reduce_dev(dist, dev):

@@ -379,6 +379,11 @@ aqz_status aqz_stage_memory_usage(const aqz_stage* st, aqz_memory_usage* out);
 aqz_status aqz_stage_estimate_memory(const aqz_array_desc* desc,
                                      const aqz_stage_options* opt,
                                      aqz_memory_usage* out);
+/* Pin the calling thread to the CPUs of the NUMA node of the stage's device
+ * (the CPUs the stage's own host threads run on; no-op when unknown): for a
+ * caller's threads that feed the stage or read its hand-off buffers.  The
+ * reference pins none of its threads (thread.pool.cpp:6-20). */
+aqz_status aqz_stage_bind_host_thread(const aqz_stage* st);
 /* Page-locked host memory for frames and hand-off buffers. */
 aqz_status aqz_host_alloc(size_t bytes, void** out);
 void aqz_host_free(void* p);

@@ -119,8 +119,8 @@ struct HandoffSink
 struct HandoffOptions
 {
     uint32_t batch_frames = 64; // frames per append
-    uint32_t host_slots = 2;    // host unit buffers per level (>= 1)
-    uint32_t copy_threads = 4;  // threads copying frames into the batch
+    uint32_t host_slots = 3;    // host unit buffers per level (>= 1)
+    uint32_t copy_threads = 8;  // threads copying frames into the batch
     aqz_compression comp{};     // codec 0: raw chunk units
 };
 
@@ -207,7 +207,10 @@ class Handoff
         }
         const uint32_t nt = std::max<uint32_t>(1, opt_.copy_threads);
         for (uint32_t t = 1; t < nt; ++t)
-            copiers_.emplace_back([this, t] { copier_(t); });
+            copiers_.emplace_back([this, t] {
+                (void)aqz_stage_bind_host_thread(st_); // next to the device
+                copier_(t);
+            });
     }
 
     ~Handoff()
@@ -502,8 +505,12 @@ class Handoff
                     return AQZ_STATUS_SUCCESS;
             }
             Slot& slot = *levels_[p.level].slots[p.slot];
-            aqz_status s =
-              aqz_stage_copy_compressed_async(st_, p.level, p.layer, slot.buf, slot.cap);
+            // the entries now: the device frame slot may take a newer layer
+            // once this copy is issued (the stage orders the device side)
+            aqz_status s = aqz_stage_compressed_entries(st_, p.level, p.layer,
+                                                        slot.ent.data(), slot.ent.size());
+            if (s == AQZ_STATUS_SUCCESS)
+                s = aqz_stage_copy_compressed_async(st_, p.level, p.layer, slot.buf, slot.cap);
             if (s != AQZ_STATUS_SUCCESS)
                 return s;
             p.ticket = aqz_stage_last_ticket(st_);
@@ -565,10 +572,6 @@ class Handoff
         u.last_in_layer = p.band + 1 == L.n_bands;
         u.bytes_per_chunk = L.lay.bytes_per_chunk;
         if (L.compressed) {
-            const aqz_status s = aqz_stage_compressed_entries(st_, p.level, p.layer,
-                                                              slot.ent.data(), slot.ent.size());
-            if (s != AQZ_STATUS_SUCCESS)
-                return s;
             u.data = slot.buf;
             u.entries = slot.ent.data();
         } else {

@@ -200,7 +200,7 @@ class GpuMultiscaleArray final
                        const ZarrArraySettings& settings,
                        int32_t device,
                        uint32_t batch_frames = 64,
-                       uint32_t host_slots = 2)
+                       uint32_t host_slots = 3)
       : MultiscaleArray(config, thread_pool, file_handle_pool, s3_connection_pool)
     {
         EXPECT(downsampler_ != nullptr, "GpuMultiscaleArray needs a downsampling method");

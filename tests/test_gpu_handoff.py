@@ -318,3 +318,25 @@ def test_binding_handoff_replay(gpu, tmp_path, case, codec):
         assert len([e for e in log if e["level"] == 0]) > len(
             {k[1] for k in exp if k[0] == 0})  # bands, not layers
     _check_replay(exp, fw, log, got, CODECS[codec], bpc)
+
+
+@pytest.mark.parametrize("codec", ["lz4-shuffle", "zstd-1", "raw"])
+@pytest.mark.parametrize("slots", [1, 3])
+def test_binding_handoff_replay_host_slots(gpu, tmp_path, codec, slots):
+    """More (or fewer) host unit buffers per level than the stage has device
+    layer slots: a compressed layer's device frame slot takes a newer layer
+    as soon as its copy is issued, so the hand-off reads the entries at
+    issue time; with one host buffer every unit waits for the previous
+    unit's writer jobs (the lease)."""
+    from codec_helpers import libzstd
+    if CODECS[codec][0] in (2, 3) and libzstd() is None:
+        pytest.skip("no libzstd to decode with")
+    dims, n, batch = REPLAY_CASES["layers-2d-ragged"]
+    frames = synthetic_frames(U16, n, dims[-2][1], dims[-1][1], 7 * slots) & 0x0fff
+    exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
+    log, summary, got = _run_replay(tmp_path, dims, U16, MEAN, frames, batch, slots,
+                                    codec=CODECS[codec], pool_threads=3)
+    st = gpu.Stage(dims, U16, MEAN)
+    bpc = [st.layout(l)["bytes_per_chunk"] for l in range(st.n_levels())]
+    st.close()
+    _check_replay(exp, fw, log, got, CODECS[codec], bpc)

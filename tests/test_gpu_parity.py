@@ -468,6 +468,26 @@ def test_stage_z_slab_rejects_misaligned(gpu):
         gpu.Stage(dims, U16, MEAN, z_slab=(16, 16))
 
 
+def test_stage_z_slab_bounded_extent(gpu):
+    """A bounded time dim (2 stacks of 64 planes) with the slab [0, 16): the
+    stage takes 2 x 16 of its own planes and refuses the next with status 12
+    (Array::write_frame's bounds check, array.cpp:171-175).  Frame ids jump
+    over the other slabs, so room is counted in this stage's own frames."""
+    dims = [(TIME, 2, 1, 1), (SPACE, 64, 16, 1), (SPACE, 256, 64, 1), (SPACE, 256, 64, 1)]
+    frames = synthetic_frames(U16, 48, 256, 256, 9)
+    st = gpu.Stage(dims, U16, MEAN, layer_slots=4, max_batch_frames=8, z_slab=(0, 16))
+    st.append(np.ascontiguousarray(frames[:16]))
+    assert st.frames_written(0) == 64  # jumped to the next stack's slab
+    with pytest.raises(gpu.AqzError) as e:
+        st.append(np.ascontiguousarray(frames[16:48]))  # only 16 fit
+    assert e.value.status == 12
+    assert st.frames_written(0) == 64 + 64  # the 16 that fit, then the jump
+    with pytest.raises(gpu.AqzError) as e:
+        st.append(np.ascontiguousarray(frames[:1]))
+    assert e.value.status == 12
+    st.close()
+
+
 @pytest.mark.parametrize("pad", [0, 4224])
 def test_stage_async_handoff_pinned_and_pageable(gpu, pad):
     """The ingestion / hand-off pipeline: pinned and pageable (multi-threaded

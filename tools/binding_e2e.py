@@ -28,9 +28,9 @@ def main():
     ap.add_argument("--frames", type=int, default=512)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--codecs", default="raw,lz4,lz4-bit,blosc-zstd,zstd-1")
-    ap.add_argument("--copy-threads", type=int, default=4)
+    ap.add_argument("--copy-threads", type=int, default=8)
     ap.add_argument("--pool-threads", type=int, default=16)
-    ap.add_argument("--host-slots", type=int, default=2)
+    ap.add_argument("--host-slots", type=int, default=3)
     ap.add_argument("--placement-tries", type=int, default=0)
     args = ap.parse_args()
     dims = [(2, 0, 64, 1), (0, 2048, 256, 1), (0, 2048, 256, 1)]
