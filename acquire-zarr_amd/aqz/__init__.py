@@ -258,6 +258,8 @@ def lib():
         "aqz_compressor_run": ([vp, vp, u64, u32, vp, sz, vp, vp], i32),
         "aqz_compressor_blocksize": ([vp], u32),
         "aqz_stage_bench_replace_rings": ([vp, u32], i32),
+        "aqz_stage_bind_host_thread": ([vp], i32),
+        "aqz_stage_import_frames": ([vp, vp, u32, u64, u32, u32], i32),
         "aqz_stage_compression_done": ([vp, u32, u64, C.POINTER(C.c_int32)], i32),
         "aqz_stage_compressed_entries": ([vp, u32, u64, C.POINTER(ChunkEntryC), sz], i32),
         "aqz_stage_shard_geometry": ([vp, u32, C.POINTER(u32), C.POINTER(u32),
@@ -588,6 +590,12 @@ class Stage:
 
     def set_stream(self, stream_ptr):
         _check(lib().aqz_stage_set_stream(self.h, stream_ptr), "set_stream")
+
+    def import_frames(self, src, level, layer, first, count):
+        """z-slab assembly: frames [first, first + count) of a chunk layer
+        copied from stage `src` (None: zero-filled), aqz_stage_import_frames."""
+        _check(lib().aqz_stage_import_frames(self.h, src.h if src is not None else None,
+                                             level, layer, first, count), "import_frames")
 
     def replace_rings(self, level_mask):
         """Bench: fresh chunk-layer rings for the levels in level_mask (the

@@ -74,6 +74,38 @@ guard_sticky(O* o, F&& f)
     return s;
 }
 
+// A stage's work (and its lazily allocated buffers) belongs to its device,
+// whichever device the calling thread had current: one consumer thread may
+// drive stages on several GPUs (AQZ_DEVICE round robin, z slabs).
+struct DeviceScope
+{
+    int prev = -1;
+    explicit DeviceScope(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess || prev == dev) {
+            prev = -1;
+            (void)hipGetLastError();
+            return;
+        }
+        (void)hipSetDevice(dev);
+    }
+    ~DeviceScope()
+    {
+        if (prev >= 0)
+            (void)hipSetDevice(prev);
+    }
+};
+
+template<typename F>
+aqz_status
+guard_sticky(aqz_stage* o, F&& f)
+{
+    if (!o || !o->st)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    DeviceScope ds(o->st->device());
+    return guard_sticky<aqz_stage>(o, std::forward<F>(f));
+}
+
 std::vector<Dim>
 to_dims(const aqz_dimension* d, size_t n)
 {
@@ -498,6 +530,7 @@ create_stage(const aqz_array_desc* desc, const aqz_stage_options* opt,
         StageOptions o;
         apply_options(opt, o);
         apply_bench(bench, o);
+        DeviceScope ds(a.device); // the caller's current device is kept
         auto* s = new aqz_stage;
         try {
             s->st = std::make_unique<Stage>(a, o);
@@ -589,7 +622,12 @@ void
 aqz_stage_destroy(aqz_stage* st)
 {
     try {
-        delete st;
+        if (st && st->st) {
+            DeviceScope ds(st->st->device());
+            delete st;
+        } else {
+            delete st;
+        }
     } catch (...) {
     }
 }
@@ -630,6 +668,17 @@ aqz_stage_set_tuning(aqz_stage* st, uint32_t knobs, uint32_t nt)
     if (!st)
         return AQZ_STATUS_INVALID_ARGUMENT;
     return guard([&] { st->st->set_tuning(knobs, nt); });
+}
+
+aqz_status
+aqz_stage_import_frames(aqz_stage* dst, aqz_stage* src, uint32_t level, uint64_t layer,
+                        uint32_t first, uint32_t count)
+{
+    if (!dst)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard_sticky(dst, [&] {
+        dst->st->import_frames(src ? src->st.get() : nullptr, level, layer, first, count);
+    });
 }
 
 aqz_status

@@ -2271,6 +2271,63 @@ Stage::copy_compressed_async(uint32_t level, uint64_t layer, void* dst, size_t c
 }
 
 void
+Stage::import_frames(Stage* src, uint32_t level, uint64_t layer, uint32_t first,
+                     uint32_t count)
+{
+    if (level >= lv_.size())
+        throw Error(3, "level out of range");
+    StageLevel& L = lv_[level];
+    if (!L.ring.p)
+        throw Error(1, "level 0 split disabled for this stage");
+    if (uint64_t(first) + count > L.F)
+        throw Error(3, "frames outside the chunk layer");
+    StageLevel* S = nullptr;
+    if (src) {
+        if (src->lv_.size() != lv_.size())
+            throw Error(1, "stages of different pyramids");
+        S = &src->lv_[level];
+        if (S->bpc != L.bpc || S->n_chunks != L.n_chunks || S->F != L.F ||
+            S->n_slots != L.n_slots || S->pitch != L.pitch || !S->ring.p)
+            throw Error(1, "stages of different chunk geometry");
+        if (S->slot_layer[layer % S->n_slots] != int64_t(layer))
+            throw Error(3, "source chunk layer not resident");
+        if (src->desc_.device != desc_.device) {
+            // peer reads over xGMI; enabled once per device pair
+            const hipError_t e = hipDeviceEnablePeerAccess(src->desc_.device, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+                hip_check(e, "hipDeviceEnablePeerAccess");
+            (void)hipGetLastError();
+        }
+    }
+    if (count == 0)
+        return;
+    const uint32_t slot = uint32_t(layer % L.n_slots);
+    if (L.slot_layer[slot] != int64_t(layer))
+        enter_layer(L, layer); // this stage wrote none of the layer's frames yet
+    if (src) {
+        // after every kernel src enqueued so far (the frames it wrote)
+        hip_check(hipEventRecord(S->ready_ev[slot], src->stream_), "hipEventRecord");
+        hip_check(hipStreamWaitEvent(stream_, S->ready_ev[slot], 0), "hipStreamWaitEvent");
+    }
+    const uint32_t tile_bytes = L.th * L.tw * uint32_t(bpp_);
+    hip_check(launch_import_frames(
+                L.ring.p + slot * L.slot_bytes, S ? S->ring.p + slot * S->slot_bytes : nullptr,
+                reinterpret_cast<const uint64_t*>(L.tab_off.p),
+                reinterpret_cast<const uint32_t*>(L.tab_grp.p), first, count, L.ntx * L.nty,
+                L.pitch, tile_bytes,
+                reinterpret_cast<uint32_t*>(L.flags.p) + size_t(slot) * L.n_chunks,
+                S ? reinterpret_cast<const uint32_t*>(S->flags.p) + size_t(slot) * S->n_chunks
+                  : nullptr,
+                uint32_t(layer / L.n_slots + 1), stream_),
+              "import launch");
+    if (src) {
+        // src's slot holds the layer until the copy has read it
+        hip_check(hipEventRecord(S->copy_ev[slot], stream_), "hipEventRecord");
+        S->copy_pending[slot] = 1;
+    }
+}
+
+void
 Stage::finalize()
 {
     for (auto& L : lv_) {

@@ -35,6 +35,11 @@ hipError_t launch_transpose_frames(const void* src, void* dst, uint32_t rows,
 hipError_t launch_flags_to_bytes(const uint32_t* flags, uint8_t* out, uint32_t n,
                                  uint32_t tag, hipStream_t stream);
 hipError_t launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t stream);
+hipError_t launch_import_frames(uint8_t* dst, const uint8_t* src, const uint64_t* tab_off,
+                                const uint32_t* tab_grp, uint32_t f0, uint32_t n_frames,
+                                uint32_t n_tiles, uint64_t pitch, uint32_t tile_bytes,
+                                uint32_t* dst_flags, const uint32_t* src_flags, uint32_t tag,
+                                hipStream_t stream);
 hipError_t launch_zero_frame_tiles(uint8_t* fb, uint64_t bpc,
                                    uint32_t n_tiles, uint32_t tile_bytes,
                                    hipStream_t stream);
@@ -362,6 +367,13 @@ class Stage
     void shard_geometry(uint32_t level, uint32_t* chunks_per_shard, uint32_t* n_shards,
                         uint32_t* layers_per_shard) const;
     void finalize();
+    // z-slab assembly: frames [first, first + count) of `layer` of `level`
+    // (layer-local frame ids) copied from src's resident layer -- or zeroed
+    // when src is null -- with their has_data, after the work enqueued so far
+    // on src; src's slot is not rewritten until the copy has run
+    void import_frames(Stage* src, uint32_t level, uint64_t layer, uint32_t first,
+                       uint32_t count);
+    int device() const { return desc_.device; }
     void enable_timing(bool on);
     void timing(double* total_ms, uint64_t* launches);
     // timing events on the stage's stream bracketing a region of appends

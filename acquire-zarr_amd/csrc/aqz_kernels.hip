@@ -1817,6 +1817,36 @@ zero_frame_tiles(uint8_t* fb, uint64_t bpc, uint32_t n_tiles,
         p[i] = 0;
 }
 
+// z-slab assembly (Stage::import_frames): the tiles of frames [f0, f0 +
+// gridDim.y) of one chunk layer copied from another stage's resident layer
+// (a peer device's HBM over xGMI, or the same device) -- or zeroed when src
+// is null -- at the same offsets (same geometry).  Block (x, f): tile
+// blockIdx.x of frame f0 + blockIdx.y; the first lane also carries the
+// chunk's has_data tag over.
+__global__ __launch_bounds__(256) void
+import_frame_tiles(uint8_t* dst, const uint8_t* src, const uint64_t* tab_off,
+                   const uint32_t* tab_grp, uint32_t f0, uint64_t pitch, uint32_t tile_bytes,
+                   uint32_t* dst_flags, const uint32_t* src_flags, uint32_t tag)
+{
+    const uint32_t f = f0 + blockIdx.y, t = blockIdx.x;
+    const uint64_t off = tab_off[f] + uint64_t(t) * pitch;
+    if ((tile_bytes & 15u) == 0 && (off & 15u) == 0) {
+        typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+        u32x4v* d = reinterpret_cast<u32x4v*>(dst + off);
+        const u32x4v* s = reinterpret_cast<const u32x4v*>(src + off);
+        for (uint32_t i = threadIdx.x; i < tile_bytes / 16u; i += 256)
+            d[i] = src ? __builtin_nontemporal_load(s + i) : u32x4v{ 0, 0, 0, 0 };
+    } else {
+        for (uint32_t i = threadIdx.x; i < tile_bytes; i += 256)
+            dst[off + i] = src ? src[off + i] : uint8_t(0);
+    }
+    if (src && threadIdx.x == 0) {
+        const uint32_t c = tab_grp[f] + t;
+        if (src_flags[c] == tag)
+            dst_flags[c] = tag;
+    }
+}
+
 // splitmix64 words (the tests' synthetic_frames stream, seed-offset): the
 // placement calibration times its candidates on random frames, as the
 // stage sees them, not on a constant fill.
@@ -2102,6 +2132,19 @@ launch_flags_to_bytes(const uint32_t* flags, uint8_t* out, uint32_t n, uint32_t 
         return hipSuccess;
     hipLaunchKernelGGL(flags_to_bytes, dim3((n + 255) / 256), dim3(256), 0, stream,
                        flags, out, n, tag);
+    return hipGetLastError();
+}
+
+hipError_t
+launch_import_frames(uint8_t* dst, const uint8_t* src, const uint64_t* tab_off,
+                     const uint32_t* tab_grp, uint32_t f0, uint32_t n_frames, uint32_t n_tiles,
+                     uint64_t pitch, uint32_t tile_bytes, uint32_t* dst_flags,
+                     const uint32_t* src_flags, uint32_t tag, hipStream_t stream)
+{
+    if (n_frames == 0 || n_tiles == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(import_frame_tiles, dim3(n_tiles, n_frames), dim3(256), 0, stream, dst,
+                       src, tab_off, tab_grp, f0, pitch, tile_bytes, dst_flags, src_flags, tag);
     return hipGetLastError();
 }
 

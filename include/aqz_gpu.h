@@ -518,6 +518,22 @@ aqz_status aqz_compressor_run(aqz_compressor* c, const void* chunks, uint64_t pi
  * plain zstd). */
 uint32_t aqz_compressor_blocksize(const aqz_compressor* c);
 
+/* z-slab assembly of one chunk layer (a volume stream sharded
+ * over GPUs by z slabs, aqz_stage_options.z_slab_*): copy the tiles of
+ * frames [first, first + count) of `layer` of `level` (frame ids inside the
+ * layer) from stage src's resident layer into dst's, with their has_data
+ * flags -- over xGMI when the stages' devices differ (peer access is
+ * enabled on first use), on dst's stream after all work enqueued so far on
+ * src's.  src = NULL zero-fills those frames in dst.  The two stages must
+ * have the same array description and options apart from the device and
+ * the slab.  The layer becomes resident in dst if it was not; src's ring
+ * slot is not rewritten until the copy has read it.  dst then holds the
+ * whole layer and hands it off (aqz_stage_copy_*_async,
+ * aqz_stage_compress_layer) as if it had written every frame -- the chunk
+ * buffers Array::write_frame_to_chunks_ fills (array.cpp:507-622). */
+aqz_status aqz_stage_import_frames(aqz_stage* dst, aqz_stage* src, uint32_t level,
+                                   uint64_t layer, uint32_t first, uint32_t count);
+
 /* Zero the not-yet-written frames of every level's last partial layer so
  * it can be flushed (the reference's lazily zeroed chunks, chunk.cpp:8-15).
  * The unpaired trailing z plane is dropped, as in the reference. */

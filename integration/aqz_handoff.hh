@@ -160,27 +160,80 @@ select_device(int32_t n_visible)
     return list[next.fetch_add(1) % list.size()];
 }
 
+// z slabs of a volume stream over several stages (BASELINE
+// configs[3]): level-0 planes [begin, end) of every z stack go to stage r.
+// The bounds are multiples of 2^(z-halving levels), so no z pair straddles
+// two stages (aqz_stage_options.z_slab_*).
+struct SlabPlan
+{
+    uint32_t planes = 0;                // level-0 z planes per stack (0: one stage)
+    std::vector<uint32_t> begin, end;   // level-0 slab of each stage
+};
+
+// AQZ_Z_SLABS = N: a multiscale array whose dimension before y is a z
+// (Space) dimension is split into N z slabs, one stage (GPU) each.  Returns
+// the plan (empty when N < 2 or the z extent cannot be split evenly
+// enough: every slab at least `align` planes).
+inline SlabPlan
+plan_z_slabs(uint32_t planes, uint32_t n, uint32_t align)
+{
+    SlabPlan p;
+    align = std::max<uint32_t>(1, align);
+    if (n < 2 || planes == 0 || planes % align != 0 || planes / align < n)
+        return p;
+    const uint32_t units = planes / align;
+    p.planes = planes;
+    for (uint32_t r = 0; r < n; ++r) {
+        p.begin.push_back(uint32_t(uint64_t(units) * r / n) * align);
+        p.end.push_back(uint32_t(uint64_t(units) * (r + 1) / n) * align);
+    }
+    return p;
+}
+
+inline uint32_t
+slabs_from_env()
+{
+    const char* e = std::getenv("AQZ_Z_SLABS");
+    const int n = e ? std::atoi(e) : 1;
+    return n > 1 ? uint32_t(n) : 1u;
+}
+
 class Handoff
 {
   public:
-    Handoff(aqz_stage* st, uint64_t frame_bytes, const HandoffOptions& o, HandoffSink& sink)
-      : st_(st)
+    // One stage: the whole stream.  Several stages: stage r receives z
+    // slab r of every stack (created with aqz_stage_options.z_slab_begin /
+    // z_slab_end = plan.begin[r] / plan.end[r]); every unit is assembled in
+    // one of them (aqz_stage_import_frames, over xGMI) and handed off from
+    // there.
+    Handoff(std::vector<aqz_stage*> stages, const SlabPlan& plan, uint64_t frame_bytes,
+            const HandoffOptions& o, HandoffSink& sink)
+      : st_(std::move(stages))
+      , plan_(plan)
       , frame_bytes_(frame_bytes)
       , opt_(o)
       , sink_(sink)
     {
         opt_.batch_frames = std::max<uint32_t>(1, opt_.batch_frames);
         opt_.host_slots = std::max<uint32_t>(1, opt_.host_slots);
-        for (int j = 0; j < 2; ++j)
-            status_ = worse(status_, aqz_host_alloc(size_t(opt_.batch_frames) * frame_bytes_,
-                                                    reinterpret_cast<void**>(&buf_[j])));
-        const uint32_t nl = aqz_stage_n_levels(st_);
+        if (st_.empty() || (st_.size() > 1 && plan_.begin.size() != st_.size())) {
+            status_ = AQZ_STATUS_INVALID_ARGUMENT;
+            return;
+        }
+        in_.resize(st_.size());
+        for (Input& in : in_)
+            for (int j = 0; j < 2; ++j)
+                status_ =
+                  worse(status_, aqz_host_alloc(size_t(opt_.batch_frames) * frame_bytes_,
+                                                reinterpret_cast<void**>(&in.buf[j])));
+        aqz_stage* st0 = st_[0];
+        const uint32_t nl = aqz_stage_n_levels(st0);
         levels_.resize(nl);
         for (uint32_t l = 0; l < nl && status_ == AQZ_STATUS_SUCCESS; ++l) {
             Level& L = levels_[l];
-            status_ = worse(status_, aqz_stage_level_layout(st_, l, &L.lay));
+            status_ = worse(status_, aqz_stage_level_layout(st0, l, &L.lay));
             int32_t banded = 0;
-            status_ = worse(status_, aqz_stage_band_geometry(st_, l, &banded, &L.n_bands,
+            status_ = worse(status_, aqz_stage_band_geometry(st0, l, &banded, &L.n_bands,
                                                              &L.frames_per_band,
                                                              &L.chunks_per_band));
             // a compressed unit is a whole layer (the device compresses
@@ -190,6 +243,15 @@ class Handoff
                 L.n_bands = 1;
                 L.frames_per_band = L.lay.frames_per_layer;
                 L.chunks_per_band = L.lay.chunks_per_layer;
+            }
+            if (st_.size() > 1) {
+                // z planes of this level (the dimension before y)
+                aqz_dimension d[16];
+                size_t nd = 0;
+                status_ = worse(status_, aqz_stage_level_dims(st0, l, d, 16, &nd));
+                L.planes = nd >= 3 ? d[nd - 3].array_size_px : 0;
+                if (L.planes == 0 || plan_.planes % L.planes != 0)
+                    status_ = worse(status_, AQZ_STATUS_INVALID_SETTINGS);
             }
             const size_t cap =
               L.compressed ? size_t(aqz_compressor_max_bytes(L.lay.bytes_per_chunk,
@@ -208,9 +270,14 @@ class Handoff
         const uint32_t nt = std::max<uint32_t>(1, opt_.copy_threads);
         for (uint32_t t = 1; t < nt; ++t)
             copiers_.emplace_back([this, t] {
-                (void)aqz_stage_bind_host_thread(st_); // next to the device
+                (void)aqz_stage_bind_host_thread(st_[0]); // next to the device
                 copier_(t);
             });
+    }
+
+    Handoff(aqz_stage* st, uint64_t frame_bytes, const HandoffOptions& o, HandoffSink& sink)
+      : Handoff(std::vector<aqz_stage*>{ st }, SlabPlan{}, frame_bytes, o, sink)
+    {
     }
 
     ~Handoff()
@@ -224,15 +291,17 @@ class Handoff
             t.join();
         // units still in flight must land, and every lease end, before the
         // buffers are freed
-        (void)aqz_stage_wait_copies(st_);
+        for (aqz_stage* s : st_)
+            (void)aqz_stage_wait_copies(s);
         for (Level& L : levels_)
             for (auto& s : L.slots) {
                 wait_pins_(*s);
                 aqz_host_free(s->buf);
                 aqz_host_free(s->has);
             }
-        for (uint8_t* b : buf_)
-            aqz_host_free(b);
+        for (Input& in : in_)
+            for (uint8_t* b : in.buf)
+                aqz_host_free(b);
     }
 
     Handoff(const Handoff&) = delete;
@@ -244,48 +313,63 @@ class Handoff
     // pinned host bytes held (batch buffers + unit buffers)
     size_t host_bytes() const
     {
-        size_t n = 2 * size_t(opt_.batch_frames) * frame_bytes_;
+        size_t n = in_.size() * 2 * size_t(opt_.batch_frames) * frame_bytes_;
         for (const Level& L : levels_)
             for (const auto& s : L.slots)
                 n += s->cap + L.chunks_per_band;
         return n;
     }
 
-    // One level-0 frame (frame_bytes bytes).  Appends a full batch.
+    // One level-0 frame (frame_bytes bytes), to the stage that owns its z
+    // plane.  Appends a full batch, or a slab run's last frames.
     aqz_status write_frame(const void* frame)
     {
         if (status_ != AQZ_STATUS_SUCCESS)
             return status_;
-        if (n_batched_ == 0) {
+        uint32_t r = 0;
+        bool run_end = false;
+        if (st_.size() > 1) {
+            const uint32_t z = uint32_t(accepted_ % plan_.planes);
+            while (z >= plan_.end[r])
+                ++r;
+            run_end = z + 1 == plan_.end[r];
+        }
+        Input& in = in_[r];
+        if (in.n == 0) {
             // refill only once the stage has read this buffer's last batch
-            const aqz_status s = aqz_stage_wait_consumed(st_, end_[cur_]);
+            const aqz_status s = aqz_stage_wait_consumed(st_[r], in.end[in.cur]);
             if (s != AQZ_STATUS_SUCCESS)
                 return status_ = s;
         }
-        copy_frame_(buf_[cur_] + size_t(n_batched_) * frame_bytes_, frame);
-        ++n_batched_;
+        copy_frame_(in.buf[in.cur] + size_t(in.n) * frame_bytes_, frame);
+        ++in.n;
+        ++in.appended;
         ++accepted_;
-        if (n_batched_ == opt_.batch_frames)
-            return append_batch_();
+        if (in.n == opt_.batch_frames || run_end)
+            return append_batch_(r);
         // units whose copies landed meanwhile go to the sink now
         return retire_(false);
     }
 
     // MultiscaleArray::close_ (multiscale.array.cpp:112-135): the partial
-    // batch, the zero-filled remainder of every level's last layer (chunk.cpp:
-    // 8-15) and every remaining unit (Array::close_ flushes them, array.cpp:
-    // 374-424).
+    // batches, the zero-filled remainder of every level's last layer (chunk.
+    // cpp:8-15) and every remaining unit (Array::close_ flushes them,
+    // array.cpp:374-424).
     aqz_status close()
     {
         if (status_ != AQZ_STATUS_SUCCESS)
             return status_;
-        aqz_status s = append_batch_();
-        if (s != AQZ_STATUS_SUCCESS)
-            return s;
-        s = aqz_stage_finalize(st_);
-        if (s != AQZ_STATUS_SUCCESS)
-            return status_ = s;
-        s = issue_(true);
+        for (uint32_t r = 0; r < st_.size(); ++r) {
+            const aqz_status s = append_batch_(r, false);
+            if (s != AQZ_STATUS_SUCCESS)
+                return s;
+        }
+        for (aqz_stage* st : st_) {
+            const aqz_status s = aqz_stage_finalize(st);
+            if (s != AQZ_STATUS_SUCCESS)
+                return status_ = s;
+        }
+        aqz_status s = issue_(true);
         if (s == AQZ_STATUS_SUCCESS)
             s = drain_();
         if (s != AQZ_STATUS_SUCCESS)
@@ -297,6 +381,14 @@ class Handoff
     }
 
   private:
+    struct Input // a stage's pinned double buffer of frames
+    {
+        uint8_t* buf[2] = { nullptr, nullptr };
+        uint64_t end[2] = { 0, 0 }; // frames appended to the stage with each buffer
+        int cur = 0;
+        uint32_t n = 0;             // frames in buf[cur]
+        uint64_t appended = 0;      // frames given to this stage (batched or not)
+    };
     struct Slot
     {
         uint8_t* buf = nullptr;
@@ -312,14 +404,15 @@ class Handoff
         bool compressed = false;
         uint32_t n_bands = 1, chunks_per_band = 0;
         uint64_t frames_per_band = 0;
-        uint64_t layer = 0; // next unit to hand off: (layer, band)
+        uint32_t planes = 0; // z planes of the level (slab mode)
+        uint64_t layer = 0;  // next unit to hand off: (layer, band)
         uint32_t band = 0;
         std::vector<std::unique_ptr<Slot>> slots;
         uint32_t next = 0;
     };
     struct Pending
     {
-        uint32_t level, slot;
+        uint32_t level, slot, owner;
         uint64_t layer;
         uint32_t band;
         uint64_t frames;
@@ -385,21 +478,87 @@ class Handoff
     }
 
     // ---- batches and units ------------------------------------------------------
-    aqz_status append_batch_()
+    aqz_status append_batch_(uint32_t r, bool hand_off = true)
     {
-        if (n_batched_ == 0)
+        Input& in = in_[r];
+        if (in.n == 0)
             return AQZ_STATUS_SUCCESS;
-        const aqz_status s =
-          aqz_stage_append(st_, buf_[cur_], n_batched_, AQZ_MEM_HOST_PINNED);
+        const aqz_status s = aqz_stage_append(st_[r], in.buf[in.cur], in.n, AQZ_MEM_HOST_PINNED);
         if (s != AQZ_STATUS_SUCCESS)
             return status_ = s;
-        end_[cur_] = accepted_;
-        cur_ ^= 1;
-        n_batched_ = 0;
+        in.end[in.cur] = in.appended;
+        in.cur ^= 1;
+        in.n = 0;
+        if (!hand_off)
+            return AQZ_STATUS_SUCCESS;
         aqz_status h = issue_(false);
         if (h == AQZ_STATUS_SUCCESS)
             h = retire_(false);
         return h == AQZ_STATUS_SUCCESS ? h : (status_ = h);
+    }
+
+    // Frames of level l written so far by the whole stream.  One stage: its
+    // own count (any cascade, odd z included).  z slabs (a regular z
+    // schedule): every level-0 plane appended, stack by stack.
+    uint64_t written_(uint32_t l) const
+    {
+        if (st_.size() == 1)
+            return aqz_stage_frames_written(st_[0], l);
+        uint64_t n0 = 0;
+        for (const Input& in : in_)
+            n0 += in.appended - in.n; // given to its stage (a batch not yet appended is not)
+        const uint64_t Z = plan_.planes, Zk = levels_[l].planes;
+        const uint64_t shift = ctz_(uint32_t(Z / Zk));
+        return (n0 / Z) * Zk + ((n0 % Z) >> shift);
+    }
+    static uint32_t ctz_(uint32_t v)
+    {
+        uint32_t n = 0;
+        while (v > 1) {
+            v >>= 1;
+            ++n;
+        }
+        return n;
+    }
+
+    // The stage that assembles and hands off a unit, after the others'
+    // frames of it were imported (z slabs; round robin over layers so the
+    // assembly traffic and the codec work spread over the GPUs).  Frames of
+    // the unit not yet appended (close) are zeroed there.
+    aqz_status assemble_(uint32_t l, uint64_t layer, uint64_t lo, uint64_t hi,
+                         uint64_t written, uint32_t& owner)
+    {
+        owner = 0;
+        if (st_.size() == 1)
+            return AQZ_STATUS_SUCCESS;
+        const Level& L = levels_[l];
+        const uint64_t F = L.lay.frames_per_layer;
+        const uint32_t shift = ctz_(plan_.planes / L.planes);
+        owner = uint32_t(layer % st_.size());
+        for (uint64_t f = lo; f < hi;) {
+            const uint32_t z = uint32_t(f % L.planes);
+            uint32_t r = 0;
+            while (z >= (plan_.end[r] >> shift))
+                ++r;
+            const uint64_t run_end = std::min<uint64_t>(hi, f - z + (plan_.end[r] >> shift));
+            const uint64_t have = std::min(std::max(written, f), run_end); // [f, have) written
+            if (r != owner && have > f) {
+                const aqz_status s =
+                  aqz_stage_import_frames(st_[owner], st_[r], l, layer, uint32_t(f - layer * F),
+                                          uint32_t(have - f));
+                if (s != AQZ_STATUS_SUCCESS)
+                    return s;
+            }
+            if (run_end > have) {
+                const aqz_status s =
+                  aqz_stage_import_frames(st_[owner], nullptr, l, layer,
+                                          uint32_t(have - layer * F), uint32_t(run_end - have));
+                if (s != AQZ_STATUS_SUCCESS)
+                    return s;
+            }
+            f = run_end;
+        }
+        return AQZ_STATUS_SUCCESS;
     }
 
     // Hand off every unit of every level whose frames are all written (final:
@@ -413,7 +572,7 @@ class Handoff
             Level& L = levels_[l];
             const uint64_t F = L.lay.frames_per_layer;
             for (;;) {
-                const uint64_t written = aqz_stage_frames_written(st_, l);
+                const uint64_t written = written_(l);
                 const uint64_t lo = L.layer * F + uint64_t(L.band) * L.frames_per_band;
                 const uint64_t hi =
                   L.layer * F + std::min<uint64_t>((uint64_t(L.band) + 1) * L.frames_per_band, F);
@@ -421,31 +580,39 @@ class Handoff
                 if (!complete && !(final && written > L.layer * F))
                     break;
                 const uint32_t si = L.next;
-                aqz_status s = take_slot_(L, *L.slots[si]);
+                aqz_status s = take_slot_(*L.slots[si]);
                 if (s != AQZ_STATUS_SUCCESS)
                     return s;
                 Slot& slot = *L.slots[si];
-                Pending p{ l, si, L.layer, L.band,
+                uint32_t owner = 0;
+                // a compressed unit is the whole layer
+                s = L.compressed ? assemble_(l, L.layer, L.layer * F, (L.layer + 1) * F, written,
+                                             owner)
+                                 : assemble_(l, L.layer, lo, hi, written, owner);
+                if (s != AQZ_STATUS_SUCCESS)
+                    return s;
+                aqz_stage* st = st_[owner];
+                Pending p{ l, si, owner, L.layer, L.band,
                            std::min(written, hi) - std::min(written, lo), complete, 0 };
                 if (L.compressed) {
                     // the previous occupant of this layer's device frame slot
                     // must be on its way out before the slot is rewritten
-                    s = flush_compressions_(l, L.layer);
+                    s = flush_compressions_(l, L.layer, owner);
                     if (s == AQZ_STATUS_SUCCESS)
-                        s = aqz_stage_compress_layer(st_, l, L.layer, &opt_.comp);
+                        s = aqz_stage_compress_layer(st, l, L.layer, &opt_.comp);
                     if (s != AQZ_STATUS_SUCCESS)
                         return s;
                     compressing_.push_back(p);
                 } else {
                     const size_t cap = size_t(L.lay.bytes_per_chunk) * L.chunks_per_band;
                     s = L.n_bands > 1
-                          ? aqz_stage_copy_band_async(st_, l, L.layer, L.band, slot.buf, cap,
+                          ? aqz_stage_copy_band_async(st, l, L.layer, L.band, slot.buf, cap,
                                                       slot.has, L.chunks_per_band)
-                          : aqz_stage_copy_layer_async(st_, l, L.layer, slot.buf, cap, slot.has,
+                          : aqz_stage_copy_layer_async(st, l, L.layer, slot.buf, cap, slot.has,
                                                        L.chunks_per_band);
                     if (s != AQZ_STATUS_SUCCESS)
                         return s;
-                    p.ticket = aqz_stage_last_ticket(st_);
+                    p.ticket = aqz_stage_last_ticket(st);
                     inflight_.push_back(p);
                 }
                 slot.busy = true;
@@ -461,9 +628,8 @@ class Handoff
 
     // Wait until a host slot is free: neither compressing nor in flight, and
     // no lease on it.
-    aqz_status take_slot_(Level& L, Slot& slot)
+    aqz_status take_slot_(Slot& slot)
     {
-        (void)L;
         while (slot.busy) {
             const aqz_status s = progress_(true);
             if (s != AQZ_STATUS_SUCCESS)
@@ -473,15 +639,16 @@ class Handoff
         return AQZ_STATUS_SUCCESS;
     }
 
-    // Compressed layers of level l that share the device frame slot of
-    // `layer` (layer - layer_slots and earlier) get their D2H issued.
-    aqz_status flush_compressions_(uint32_t l, uint64_t layer)
+    // Compressed layers of level l on stage `owner` that share the device
+    // frame slot of `layer` (layer - layer_slots and earlier) get their D2H
+    // issued.
+    aqz_status flush_compressions_(uint32_t l, uint64_t layer, uint32_t owner)
     {
         const uint64_t ns = std::max<uint32_t>(1, levels_[l].lay.layer_slots);
         for (;;) {
             bool found = false;
             for (const Pending& p : compressing_)
-                found |= p.level == l && p.layer + ns <= layer;
+                found |= p.level == l && p.owner == owner && p.layer + ns <= layer;
             if (!found)
                 return AQZ_STATUS_SUCCESS;
             const aqz_status s = advance_compressions_(true);
@@ -496,9 +663,10 @@ class Handoff
     {
         while (!compressing_.empty()) {
             Pending p = compressing_.front();
+            aqz_stage* st = st_[p.owner];
             if (!block) {
                 int32_t done = 0;
-                const aqz_status s = aqz_stage_compression_done(st_, p.level, p.layer, &done);
+                const aqz_status s = aqz_stage_compression_done(st, p.level, p.layer, &done);
                 if (s != AQZ_STATUS_SUCCESS)
                     return s;
                 if (!done)
@@ -507,13 +675,13 @@ class Handoff
             Slot& slot = *levels_[p.level].slots[p.slot];
             // the entries now: the device frame slot may take a newer layer
             // once this copy is issued (the stage orders the device side)
-            aqz_status s = aqz_stage_compressed_entries(st_, p.level, p.layer,
-                                                        slot.ent.data(), slot.ent.size());
+            aqz_status s = aqz_stage_compressed_entries(st, p.level, p.layer, slot.ent.data(),
+                                                        slot.ent.size());
             if (s == AQZ_STATUS_SUCCESS)
-                s = aqz_stage_copy_compressed_async(st_, p.level, p.layer, slot.buf, slot.cap);
+                s = aqz_stage_copy_compressed_async(st, p.level, p.layer, slot.buf, slot.cap);
             if (s != AQZ_STATUS_SUCCESS)
                 return s;
-            p.ticket = aqz_stage_last_ticket(st_);
+            p.ticket = aqz_stage_last_ticket(st);
             compressing_.pop_front();
             inflight_.push_back(p);
             block = false;
@@ -542,18 +710,19 @@ class Handoff
     }
 
     // Deliver the oldest in-flight unit (wait: block until its copy landed;
-    // else only if it has).  Tickets complete in issue order, and per level
-    // they are issued in frame order.
+    // else only if it has).  A stage's tickets complete in issue order, and
+    // per level units are issued in frame order.
     aqz_status retire_one_(bool wait)
     {
         if (inflight_.empty())
             return AQZ_STATUS_SUCCESS;
         const Pending p = inflight_.front();
+        aqz_stage* st = st_[p.owner];
         if (wait) {
-            const aqz_status s = aqz_stage_wait_ticket(st_, p.ticket);
+            const aqz_status s = aqz_stage_wait_ticket(st, p.ticket);
             if (s != AQZ_STATUS_SUCCESS)
                 return s;
-        } else if (aqz_stage_copies_completed(st_) < p.ticket) {
+        } else if (aqz_stage_copies_completed(st) < p.ticket) {
             return AQZ_STATUS_SUCCESS;
         }
         inflight_.pop_front();
@@ -608,19 +777,17 @@ class Handoff
         return AQZ_STATUS_SUCCESS;
     }
 
-    aqz_stage* st_;
+    std::vector<aqz_stage*> st_;
+    SlabPlan plan_;
     const uint64_t frame_bytes_;
     HandoffOptions opt_;
     HandoffSink& sink_;
     aqz_status status_ = AQZ_STATUS_SUCCESS;
-    uint8_t* buf_[2] = { nullptr, nullptr };
-    uint64_t end_[2] = { 0, 0 }; // frames accepted when each buffer was appended
-    int cur_ = 0;
-    uint32_t n_batched_ = 0;
+    std::vector<Input> in_;
     uint64_t accepted_ = 0;
     std::vector<Level> levels_;
     std::deque<Pending> compressing_; // compression issued, in issue order
-    std::deque<Pending> inflight_;    // copies issued, in ticket order
+    std::deque<Pending> inflight_;    // copies issued, in issue order
     // frame copy threads
     std::vector<std::thread> copiers_;
     std::mutex cmu_;

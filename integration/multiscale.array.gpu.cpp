@@ -192,13 +192,15 @@ class GpuMultiscaleArray final
   public:
     // settings: the ZarrArraySettings the stream was configured with
     // (acquisition-order dims + storage order, zarr.types.h:157-169);
-    // device: a HIP device ordinal (aqz_binding::select_device).
+    // devices: HIP device ordinals (aqz_binding::select_device), one per
+    // z slab of `plan` (one device: no slabs).
     GpuMultiscaleArray(std::shared_ptr<ArrayConfig> config,
                        std::shared_ptr<ThreadPool> thread_pool,
                        std::shared_ptr<FileHandlePool> file_handle_pool,
                        std::shared_ptr<S3ConnectionPool> s3_connection_pool,
                        const ZarrArraySettings& settings,
-                       int32_t device,
+                       std::vector<int32_t> devices,
+                       const aqz_binding::SlabPlan& plan = {},
                        uint32_t batch_frames = 64,
                        uint32_t host_slots = 3)
       : MultiscaleArray(config, thread_pool, file_handle_pool, s3_connection_pool)
@@ -229,24 +231,37 @@ class GpuMultiscaleArray final
                              int32_t(*config_->downsampling_method),
                              settings.max_levels,
                              settings.storage_dimension_order,
-                             device };
-        aqz_stage_options opt{};
-        opt.max_batch_frames = batch_frames;
-        opt.layer_slots = 2;
-        // the fused kernels' rate depends on where the chunk-layer rings
-        // land; the search's transient peak is in
-        // aqz_stage_estimate_memory
-        opt.placement_tries = 16;
-        EXPECT(aqz_stage_create(&desc, &opt, &stage_) == AQZ_STATUS_SUCCESS,
-               "aqz_stage_create failed: ", aqz_last_error());
-        EXPECT(aqz_stage_n_levels(stage_) == arrays_.size(),
-               "level count differs from the Downsampler's");
+                             0 };
+        EXPECT(!devices.empty() && (devices.size() == 1 || plan.begin.size() == devices.size()),
+               "one device per z slab");
+        for (size_t r = 0; r < devices.size(); ++r) {
+            desc.device = devices[r];
+            aqz_stage_options opt{};
+            opt.max_batch_frames = batch_frames;
+            opt.layer_slots = 2;
+            // the fused kernels' rate depends on where the chunk-layer rings
+            // land; the search's transient peak is in
+            // aqz_stage_estimate_memory
+            opt.placement_tries = 16;
+            if (devices.size() > 1) {
+                opt.z_slab_begin = plan.begin[r];
+                opt.z_slab_end = plan.end[r];
+            }
+            aqz_stage* st = nullptr;
+            EXPECT(aqz_stage_create(&desc, &opt, &st) == AQZ_STATUS_SUCCESS,
+                   "aqz_stage_create failed: ", aqz_last_error());
+            stages_.push_back(st);
+            EXPECT(aqz_stage_n_levels(st) == arrays_.size(),
+                   "level count differs from the Downsampler's");
+        }
         aqz_binding::HandoffOptions ho;
         ho.batch_frames = batch_frames;
         ho.host_slots = host_slots;
         ho.comp = aqz_codec_for(config_->compression_params);
         aqz_binding::HandoffSink& sink = *this;
-        handoff_ = std::make_unique<aqz_binding::Handoff>(stage_, bytes_per_frame_, ho, sink);
+        handoff_ = std::make_unique<aqz_binding::Handoff>(
+          stages_, devices.size() > 1 ? plan : aqz_binding::SlabPlan{}, bytes_per_frame_, ho,
+          sink);
         EXPECT(handoff_->status() == AQZ_STATUS_SUCCESS, "aqz hand-off buffers: ",
                aqz_status_message(handoff_->status()));
     }
@@ -254,14 +269,19 @@ class GpuMultiscaleArray final
     ~GpuMultiscaleArray() override
     {
         handoff_.reset();
-        aqz_stage_destroy(stage_);
+        for (aqz_stage* st : stages_)
+            aqz_stage_destroy(st);
     }
 
     size_t memory_usage() const noexcept override
     {
-        aqz_memory_usage m{};
-        (void)aqz_stage_memory_usage(stage_, &m);
-        return MultiscaleArray::memory_usage() + m.pinned_bytes + handoff_->host_bytes();
+        size_t pinned = 0;
+        for (aqz_stage* st : stages_) {
+            aqz_memory_usage m{};
+            (void)aqz_stage_memory_usage(st, &m);
+            pinned += m.pinned_bytes;
+        }
+        return MultiscaleArray::memory_usage() + pinned + handoff_->host_bytes();
     }
 
     // MultiscaleArray::write_frame (multiscale.array.cpp:57-74) with the
@@ -318,7 +338,7 @@ class GpuMultiscaleArray final
         }
     }
 
-    aqz_stage* stage_ = nullptr;
+    std::vector<aqz_stage*> stages_;
     std::vector<aqz_dimension> dims_;
     std::vector<GpuArray*> gpu_arrays_;
     std::unique_ptr<aqz_binding::Handoff> handoff_;
@@ -336,7 +356,9 @@ class GpuMultiscaleArray final
 // A multiscale array gets the GPU stage on the device AQZ_DEVICE selects
 // (aqz_handoff.hh: round robin over the visible devices by default, one
 // stream per GPU); nullptr -- no device, AQZ_DEVICE=off, not multiscale --
-// keeps the reference's CPU path.
+// keeps the reference's CPU path.  AQZ_Z_SLABS=N splits a volume stream
+// (a z Space dimension before y, acquisition storage order) into N z slabs
+// on the next N selected devices (BASELINE configs[3]: 4 GPUs).
 inline std::unique_ptr<ArrayBase>
 make_gpu_multiscale_array(std::shared_ptr<ArrayConfig> config,
                           std::shared_ptr<ThreadPool> thread_pool,
@@ -349,11 +371,42 @@ make_gpu_multiscale_array(std::shared_ptr<ArrayConfig> config,
     int32_t n = 0;
     if (aqz_device_count(&n) != AQZ_STATUS_SUCCESS)
         return nullptr;
-    const int32_t device = aqz_binding::select_device(n);
-    if (device < 0)
-        return nullptr;
+    aqz_binding::SlabPlan plan;
+    const uint32_t slabs = aqz_binding::slabs_from_env();
+    const size_t nd = settings.dimension_count;
+    bool identity = true;
+    for (size_t i = 0; settings.storage_dimension_order && i < nd; ++i)
+        identity &= settings.storage_dimension_order[i] == i;
+    if (slabs > 1 && nd >= 4 && identity &&
+        settings.dimensions[nd - 3].type == ZarrDimensionType_Space) {
+        // level z extents: slab bounds must be multiples of 2^(z halvings)
+        std::vector<aqz_dimension> d(nd);
+        for (size_t i = 0; i < nd; ++i)
+            d[i] = aqz_dimension{ int32_t(settings.dimensions[i].type),
+                                  settings.dimensions[i].array_size_px,
+                                  settings.dimensions[i].chunk_size_px,
+                                  settings.dimensions[i].shard_size_chunks };
+        uint32_t nl = 0;
+        if (aqz_pyramid_levels(d.data(), nd, settings.max_levels, &nl, nullptr, 0) ==
+            AQZ_STATUS_SUCCESS) {
+            std::vector<aqz_dimension> lv(size_t(nl) * nd);
+            if (aqz_pyramid_levels(d.data(), nd, settings.max_levels, &nl, lv.data(),
+                                   lv.size()) == AQZ_STATUS_SUCCESS) {
+                const uint32_t z0 = lv[nd - 3].array_size_px;
+                const uint32_t zl = lv[(nl - 1) * nd + nd - 3].array_size_px;
+                plan = aqz_binding::plan_z_slabs(z0, slabs, zl ? z0 / zl : 0);
+            }
+        }
+    }
+    std::vector<int32_t> devices;
+    for (size_t r = 0; r < std::max<size_t>(1, plan.begin.size()); ++r) {
+        const int32_t device = aqz_binding::select_device(n);
+        if (device < 0)
+            return nullptr;
+        devices.push_back(device);
+    }
     return std::make_unique<GpuMultiscaleArray>(config, thread_pool, file_handle_pool,
-                                                s3_connection_pool, settings, device);
+                                                s3_connection_pool, settings, devices, plan);
 }
 
 } // namespace zarr

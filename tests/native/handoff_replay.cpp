@@ -15,7 +15,9 @@
 //   i32 dtype, i32 method, u32 batch, u32 host_slots, i32 device,
 //   i32 codec, i32 clevel, i32 shuffle, u32 copy_threads, u32 pool_threads,
 //   u32 synth (0: frames follow; 1: camera-like u16/u8 frames made here;
-//   2: random bytes made here), u32 placement_tries, u64 n_frames,
+//   2: random bytes made here), u32 placement_tries, u32 z_slabs (>= 2: that
+//   many stages, z slab r of every stack each, assembled by
+//   aqz_stage_import_frames), u64 n_frames,
 //   u64 frame_bytes, [n_frames frames].
 // OUT: "AQZ3", u32 n_levels, then per level {u64 n, n x {u64 layer,
 //   u32 chunk, u32 shard, u32 internal, u64 nbytes, nbytes bytes}}: every
@@ -272,12 +274,12 @@ main(int argc, char** argv)
             !rd(f, &d.shard_size_chunks))
             return 2;
     int32_t dtype, method, device, codec, clevel, shuffle;
-    uint32_t batch, slots, copy_threads, pool_threads, synth, tries;
+    uint32_t batch, slots, copy_threads, pool_threads, synth, tries, n_slabs;
     uint64_t n_frames, fbytes;
     if (!rd(f, &dtype) || !rd(f, &method) || !rd(f, &batch) || !rd(f, &slots) ||
         !rd(f, &device) || !rd(f, &codec) || !rd(f, &clevel) || !rd(f, &shuffle) ||
         !rd(f, &copy_threads) || !rd(f, &pool_threads) || !rd(f, &synth) || !rd(f, &tries) ||
-        !rd(f, &n_frames) || !rd(f, &fbytes))
+        !rd(f, &n_slabs) || !rd(f, &n_frames) || !rd(f, &fbytes))
         return 2;
     std::vector<uint8_t> frames;
     uint32_t R = 0;
@@ -302,6 +304,37 @@ main(int argc, char** argv)
     if (aqz_stage_create(&desc, &opt, &st) != AQZ_STATUS_SUCCESS) {
         fprintf(stderr, "aqz_stage_create: %s\n", aqz_last_error());
         return 1;
+    }
+    // z slabs: stage r owns planes [begin_r, end_r) of every stack
+    // (GpuMultiscaleArray with AQZ_Z_SLABS, here all on `device`)
+    std::vector<aqz_stage*> stages{ st };
+    aqz_binding::SlabPlan plan;
+    if (n_slabs > 1) {
+        const uint32_t nl0 = aqz_stage_n_levels(st);
+        aqz_dimension d0[16], dl[16];
+        size_t n0 = 0, n1 = 0;
+        aqz_stage_level_dims(st, 0, d0, 16, &n0);
+        aqz_stage_level_dims(st, nl0 - 1, dl, 16, &n1);
+        const uint32_t Z = d0[n0 - 3].array_size_px;
+        plan = aqz_binding::plan_z_slabs(Z, n_slabs, Z / dl[n1 - 3].array_size_px);
+        if (plan.begin.size() != n_slabs) {
+            fprintf(stderr, "no z-slab plan for %u planes over %u stages\n", Z, n_slabs);
+            return 1;
+        }
+        aqz_stage_destroy(st);
+        stages.clear();
+        for (uint32_t r = 0; r < n_slabs; ++r) {
+            aqz_stage_options o = opt;
+            o.z_slab_begin = plan.begin[r];
+            o.z_slab_end = plan.end[r];
+            aqz_stage* s = nullptr;
+            if (aqz_stage_create(&desc, &o, &s) != AQZ_STATUS_SUCCESS) {
+                fprintf(stderr, "aqz_stage_create (slab %u): %s\n", r, aqz_last_error());
+                return 1;
+            }
+            stages.push_back(s);
+        }
+        st = stages[0];
     }
     const uint32_t nl = aqz_stage_n_levels(st);
     RecordingSink sink;
@@ -332,7 +365,7 @@ main(int argc, char** argv)
         ho.host_slots = slots;
         ho.copy_threads = copy_threads;
         ho.comp = aqz_compression{ codec, clevel, shuffle };
-        aqz_binding::Handoff h(st, fbytes, ho, sink);
+        aqz_binding::Handoff h(stages, plan, fbytes, ho, sink);
         if (h.status() != AQZ_STATUS_SUCCESS) {
             fprintf(stderr, "handoff: %s\n", aqz_last_error());
             return 1;
@@ -351,7 +384,7 @@ main(int argc, char** argv)
         pool.drain(); // the writer jobs (Array::close_ waits on write_counter_)
         seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
-    for (uint32_t l = 0; l < nl; ++l)
+    for (uint32_t l = 0; l < nl && n_slabs <= 1; ++l)
         if (sink.lv[l]->committed != aqz_stage_frames_written(st, l)) {
             fprintf(stderr, "level %u: committed %llu of %llu frames\n", l,
                     (unsigned long long)sink.lv[l]->committed,
@@ -367,10 +400,11 @@ main(int argc, char** argv)
            "\"shuffle\": %d, \"device\": %d, \"batch\": %u, \"copy_threads\": %u, "
            "\"pool_threads\": %u}\n",
            rc == 0 ? "true" : "false", (unsigned long long)sink.units.load(),
-           (unsigned long long)aqz_stage_last_ticket(st), (unsigned long long)n_frames,
+           (unsigned long long)aqz_stage_last_ticket(stages.back()), (unsigned long long)n_frames,
            seconds, in / seconds / 1e9, double(sink.chunk_bytes.load()) / in, codec, clevel,
            shuffle, device, batch, copy_threads, pool_threads);
-    aqz_stage_destroy(st);
+    for (aqz_stage* s : stages)
+        aqz_stage_destroy(s);
     for (auto& L : sink.lv)
         aqz_dims_destroy(L->dims);
     if (!record)

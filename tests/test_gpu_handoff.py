@@ -173,7 +173,7 @@ REPLAY = None
 
 def _run_replay(tmp_path, dims, dtype, method, frames, batch, slots, codec=(0, 0, 0),
                 copy_threads=4, pool_threads=4, device=0, synth=0, n_frames=None,
-                placement_tries=0, record=True):
+                placement_tries=0, record=True, z_slabs=1):
     """tests/native/handoff_replay: the binding's hand-off
     (integration/aqz_handoff.hh, what GpuMultiscaleArray runs) over the C
     ABI with a recording sink that does GpuArray::write_unit's per-chunk
@@ -194,8 +194,8 @@ def _run_replay(tmp_path, dims, dtype, method, frames, batch, slots, codec=(0, 0
         n = len(frames) if frames is not None else n_frames
         if fb is None:
             fb = dims[-1][1] * dims[-2][1] * {0: 1, 1: 2}[dtype]
-        f.write(struct.pack("<iiIIiiiiIIIIQQ", dtype, method, batch, slots, device, *codec,
-                            copy_threads, pool_threads, synth, placement_tries, n, fb))
+        f.write(struct.pack("<iiIIiiiiIIIIIQQ", dtype, method, batch, slots, device, *codec,
+                            copy_threads, pool_threads, synth, placement_tries, z_slabs, n, fb))
         if frames is not None:
             f.write(np.ascontiguousarray(frames).tobytes())
     r = subprocess.run([exe, str(job), str(out) if record else "-"], capture_output=True,
@@ -336,6 +336,34 @@ def test_binding_handoff_replay_host_slots(gpu, tmp_path, codec, slots):
     exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
     log, summary, got = _run_replay(tmp_path, dims, U16, MEAN, frames, batch, slots,
                                     codec=CODECS[codec], pool_threads=3)
+    st = gpu.Stage(dims, U16, MEAN)
+    bpc = [st.layout(l)["bytes_per_chunk"] for l in range(st.n_levels())]
+    st.close()
+    _check_replay(exp, fw, log, got, CODECS[codec], bpc)
+
+
+@pytest.mark.parametrize("codec", ["raw", "lz4-shuffle", "zstd-1"])
+@pytest.mark.parametrize("slabs,tail", [(2, 0), (2, 37), (4, 0), (4, 21), (3, 50)])
+def test_binding_z_slabs(gpu, tmp_path, codec, slabs, tail):
+    """AQZ_Z_SLABS: one multiscale volume stream over N stages (here all on
+    device 0; on a node, one GPU each), stage r receiving z slab r of every
+    stack.  Each unit is assembled in one stage (round robin over layers)
+    from the others' frames by aqz_stage_import_frames (peer reads over
+    xGMI between GPUs) and handed off from there -- raw or compressed on
+    that device.  A partial last stack (tail planes) leaves the unwritten
+    frames zero.  Every chunk reaches its shard once and decodes to the
+    single-stream oracle's chunk."""
+    from codec_helpers import libzstd
+    if CODECS[codec][0] in (2, 3) and libzstd() is None:
+        pytest.skip("no libzstd to decode with")
+    # z 64 -> 32 -> 16 -> 16 (xy 256 -> 32), z chunk 16: slabs align to 4
+    dims = [(TIME, 0, 1, 1), (SPACE, 64, 16, 1), (SPACE, 256, 64, 2), (SPACE, 256, 64, 2)]
+    n = 2 * 64 + tail
+    frames = synthetic_frames(U16, n, 256, 256, 71 + slabs + tail) & 0x0fff
+    frames[70:75] = 0
+    exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
+    log, summary, got = _run_replay(tmp_path, dims, U16, MEAN, frames, 8, 3,
+                                    codec=CODECS[codec], z_slabs=slabs)
     st = gpu.Stage(dims, U16, MEAN)
     bpc = [st.layout(l)["bytes_per_chunk"] for l in range(st.n_levels())]
     st.close()

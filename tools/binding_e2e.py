@@ -41,9 +41,9 @@ def main():
                 f.write(b"AQZ2" + struct.pack("<I", len(dims)))
                 for x in dims:
                     f.write(struct.pack("<iIII", *x))
-                f.write(struct.pack("<iiIIiiiiIIIIQQ", 1, 1, args.batch, args.host_slots, 0,
+                f.write(struct.pack("<iiIIiiiiIIIIIQQ", 1, 1, args.batch, args.host_slots, 0,
                                     *CODECS[name], args.copy_threads, args.pool_threads, 1,
-                                    args.placement_tries, args.frames, 2048 * 2048 * 2))
+                                    args.placement_tries, 1, args.frames, 2048 * 2048 * 2))
             r = subprocess.run([EXE, job, "-"], capture_output=True, text=True, timeout=600)
             if r.returncode != 0:
                 sys.exit(r.stdout[-2000:] + r.stderr[-2000:])
