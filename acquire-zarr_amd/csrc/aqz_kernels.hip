@@ -1921,6 +1921,15 @@ launch_interior(uint32_t blocks, const FusedParams& p, hipStream_t stream)
         }
         if (p.rh_log2 == 6 && p.n_fused >= 3 && !(p.knobs & 128u) &&
             (p.scratch_level == 0 || p.scratch_level >= 5)) {
+            // tuning knob bits 13-15 = v: unused LDS that caps the strip
+            // kernel at v workgroups per CU (an occupancy A/B)
+            const uint32_t v = (p.knobs >> 13) & 7u;
+            const uint32_t cap_lds = v ? (163840u / v - 512u) & ~255u : 0u;
+            if (cap_lds && p.nt == 7) {
+                hipLaunchKernelGGL((fused_pyramid_strip<T, M, 7>), dim3(blocks), dim3(256),
+                                   cap_lds, stream, p);
+                return;
+            }
             switch (p.nt) {
                 case 1:
                     hipLaunchKernelGGL((fused_pyramid_strip<T, M, 1>), dim3(blocks),

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--knobs", default="0,512,256")
     ap.add_argument("--nt", type=int, default=7)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--placement-tries", type=int, default=0)
     args = ap.parse_args()
     c = bench.CONFIGS[args.config]
     B = c["batch"]
@@ -33,8 +34,9 @@ def main():
     src.view(torch.int16).random_(-32768, 32767)
     knobs = [int(x) for x in args.knobs.split(",")]
     for inst in range(args.instances):
-        st = aqz.Stage(c["dims"], c["dtype"], c["method"], max_batch_frames=B, layer_slots=2,
-                       force_levels=c["force_levels"])
+        st = aqz.Stage(c["dims"], c["dtype"], c["method"], max_batch_frames=B,
+                       layer_slots=bench.layer_slots_for(c, B), force_levels=c["force_levels"],
+                       placement_tries=args.placement_tries)
         row = []
         for rnd in range(2):
             for j, k in enumerate(knobs):
