@@ -184,7 +184,7 @@ struct ZstdParams
     uint32_t far_tb;        // tag bits of a far table entry (32 - position bits)
     uint32_t far_slices;    // hash slices (workgroups) per segment: 1, 2, 4 or 8
     uint32_t far_log;       // log2 of a slice's table entries (<= kFarLog)
-    uint32_t dbg;           // A/B switches (AQZ_ZSTD_DBG; 0 = shipped)
+    uint32_t dbg;           // parse A/B switches (bench option zstd_flags; 0 = shipped)
     const uint32_t* flags;  // has_data words (nullptr: every chunk has data)
     uint32_t tag;
     const zstd::SeqTables* seqt; // predefined sequence tables (device)

@@ -392,7 +392,7 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
     // stream: compression waited for every queued D2H piece (e2e trace: 41 ->
     // 51 GB/s with 8 queues).  The PCIe streams take high priority, a queue
     // pool of their own; their work is DMA and small blits, so priority costs
-    // the kernels nothing.  AQZ_COPY_PRIORITY=0 keeps them at normal priority (2: lowest).
+    // the kernels nothing.
     {
         int least = 0, greatest = 0;
         hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest),
