@@ -483,8 +483,8 @@ apply_bench(const aqz_stage_bench_options* bench, StageOptions& o)
     if (bench->placement_tries)
         o.placement_tries = bench->placement_tries;
     o.placement_mode = bench->placement_mode;
-    if (o.placement_mode > 1)
-        throw Error(AQZ_STATUS_INVALID_ARGUMENT, "placement_mode must be 0 or 1");
+    if (o.placement_mode > 2)
+        throw Error(AQZ_STATUS_INVALID_ARGUMENT, "placement_mode must be 0, 1 or 2");
     if (bench->placement_spacer_bytes)
         o.placement_spacer = bench->placement_spacer_bytes;
     if (bench->placement_reps)

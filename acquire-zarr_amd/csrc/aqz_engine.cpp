@@ -471,10 +471,13 @@ Stage::place_level(StageLevel& L)
 // space, so it is searched, not predicted.  Each candidate is timed on
 // random frames over `reps` launches; a loser is freed and a spacer
 // allocation (held until the search ends) pushes the next candidate
-// elsewhere, so the peak is two ring sets plus the spacers (mode 0), or
-// every candidate is held (mode 1, the round-2 search).  The kept
-// placement is re-timed alone at the end (kept_ms_final).  Only for rings
-// >= 256 MiB on the fused paths.
+// elsewhere, so the peak is two ring sets plus the spacers.  Mode 0 (the
+// default) doubles the spacer after every loser, up to 4 GiB: the fast band
+// comes with earlier allocations held (round 4, profiles/
+// r04_placement_localize.txt), and on some boxes only after several GB of
+// them.  Mode 2 keeps the spacer fixed (round 3); mode 1 holds every
+// candidate (round 2).  The kept placement is re-timed alone at the end
+// (kept_ms_final).  Only for rings >= 256 MiB on the fused paths.
 void
 Stage::calibrate_placement()
 {
@@ -575,10 +578,12 @@ Stage::calibrate_placement()
             const double worst = *std::max_element(rep.ms.begin(), rep.ms.end());
             if (best_ms < 0.92 * worst || t + 1 == tries)
                 break;
-            if (mode == 0 && spacer > 0) {
+            if (mode != 1 && spacer > 0) {
                 spacers.emplace_back(spacer); // the next candidate lands elsewhere
                 live += spacer;
                 peak = std::max(peak, live);
+                if (mode == 0)
+                    spacer = std::min<uint64_t>(spacer * 2, kMaxPlacementSpacer);
             }
         }
     } catch (const Error& e) {
@@ -1594,8 +1599,17 @@ Stage::estimate_memory(const ArrayDesc& desc, const StageOptions& opt_in)
     if (opt.placement_tries > 1 && ring_bytes >= (uint64_t(256) << 20)) {
         const uint64_t extra = opt.placement_tries - 1;
         f.device += B * fb0;
-        f.device += opt.placement_mode == 1 ? extra * set_bytes
-                                            : set_bytes + extra * opt.placement_spacer;
+        if (opt.placement_mode == 1) {
+            f.device += extra * set_bytes;
+        } else {
+            f.device += set_bytes;
+            uint64_t sp = opt.placement_spacer;
+            for (uint64_t t = 0; t < extra; ++t) {
+                f.device += sp;
+                if (opt.placement_mode == 0)
+                    sp = std::min<uint64_t>(sp * 2, kMaxPlacementSpacer);
+            }
+        }
     }
     return f;
 }

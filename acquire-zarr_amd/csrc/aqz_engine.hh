@@ -183,6 +183,9 @@ struct ArrayDesc
     int32_t device = 0;
 };
 
+// the placement search's spacers grow up to this (mode 0)
+constexpr uint64_t kMaxPlacementSpacer = uint64_t(4) << 30;
+
 struct StageOptions
 {
     uint32_t layer_slots = 2;
@@ -191,12 +194,12 @@ struct StageOptions
     bool skip_level0_split = false;
     uint64_t first_frame = 0;
     uint32_t z_slab_begin = 0, z_slab_end = 0; // aqz_stage_options
-    // creation-time placement search (bench-only; 0/1 = off): up to
-    // placement_tries placements of the chunk-layer rings are timed and the
-    // fastest kept.  mode 0: a losing placement is freed and a spacer of
-    // placement_spacer bytes is held until the search ends (peak: two ring
-    // sets + the spacers); mode 1: every candidate is held (peak: tries ring
-    // sets).
+    // creation-time placement search (aqz_stage_options.placement_tries;
+    // 0/1 = off): up to placement_tries placements of the chunk-layer rings
+    // are timed and the fastest kept.  mode 0: a losing placement is freed
+    // and a spacer is held until the search ends, starting at
+    // placement_spacer bytes and doubling up to kMaxPlacementSpacer; mode 2:
+    // the same with a fixed spacer; mode 1: every candidate is held.
     uint32_t placement_tries = 0;
     uint32_t placement_mode = 0;
     uint64_t placement_spacer = uint64_t(128) << 20;

@@ -248,7 +248,8 @@ typedef struct
                                   (up to ~10% on 2-D
                                   stages); only rings >= 256 MiB search.  The
                                   transient peak (two ring sets, one batch of
-                                  random frames and 128 MiB spacers) is in
+                                  random frames and spacers from 128 MiB
+                                  doubling to 4 GiB) is in
                                   aqz_stage_estimate_memory. */
     uint32_t reserved;
 } aqz_stage_options;

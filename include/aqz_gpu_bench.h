@@ -33,10 +33,12 @@ typedef struct
                                   launch time depends on the physical memory
                                   the rings land in) */
     uint32_t placement_mode;   /* 0: a losing placement is freed and a spacer
-                                  allocation held until the search ends
+                                  allocation held until the search ends,
+                                  doubling after every loser up to 4 GiB
                                   (peak: 2 ring sets + the spacers);
-                                  1: every candidate is held (peak: n sets) */
-    uint64_t placement_spacer_bytes; /* mode 0 spacer (0 = 128 MiB) */
+                                  1: every candidate is held (peak: n sets);
+                                  2: as 0 with a fixed spacer (round 3) */
+    uint64_t placement_spacer_bytes; /* first spacer (0 = 128 MiB) */
     uint32_t placement_reps;   /* timed launches per candidate (0 = 10) */
     /* Kernel tuning for A/B runs.  The library reads none of these from the
      * environment: a stage made by aqz_stage_create always runs the shipped
