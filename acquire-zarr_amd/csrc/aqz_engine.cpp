@@ -342,6 +342,13 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         xy_direct_ = bpp_ <= 4 && rh_log2_ == 6 && n_fused_ >= 3 && !(knobs_ & 128u) &&
                      (!tail || n_fused_ >= 5) && !(knobs_ & 4096u) &&
                      (uint64_t(acq_cols_) * bpp_) % 16 == 0;
+    } else if (xy_ && fused_3d_) {
+        // the 2x2x2 strip kernel reads acquisition-order planes itself
+        // (launch_fused_pyramid_3d); batches that also need the generic
+        // cascade take the transpose pass (run_batch)
+        xy_direct_ = bpp_ <= 4 && rh_log2_ == 6 && n_levels() - 1 <= 4 &&
+                     !(knobs_ & 256u) && !(knobs_ & 4096u) &&
+                     (uint64_t(acq_cols_) * bpp_) % 16 == 0;
     }
 
     const Dim& d0 = lv_[0].dims[0];
@@ -948,7 +955,20 @@ Stage::append(const void* frames, uint64_t n_frames, int mem)
 void
 Stage::run_batch(const uint8_t* dsrc, uint32_t n)
 {
-    if (xy_ && !(xy_direct_ && reinterpret_cast<uintptr_t>(dsrc) % 16 == 0)) {
+    // 2x2x2 pyramids: how many frames the fused kernel takes (whole z
+    // groups, no carried partial plane), the rest go to the generic cascade
+    uint32_t n3 = 0;
+    if (!fused_2d_ && fused_3d_) {
+        bool idle = lv_[0].frames_written % g3d_ == 0 &&
+                    reinterpret_cast<uintptr_t>(dsrc) % 16 == 0;
+        for (const auto& pd : pend_)
+            idle &= !pd.has;
+        if (idle)
+            n3 = n / g3d_ * g3d_;
+    }
+    const bool direct = xy_direct_ && reinterpret_cast<uintptr_t>(dsrc) % 16 == 0 &&
+                        (fused_2d_ || n3 == n);
+    if (xy_ && !direct) {
         xbuf_.alloc(size_t(opt_.max_batch_frames) * acq_rows_ * acq_cols_ * bpp_);
         hip_check(launch_transpose_frames(dsrc, xbuf_.p, acq_rows_, acq_cols_, n,
                                           uint32_t(bpp_), stream_),
@@ -972,15 +992,6 @@ Stage::run_batch(const uint8_t* dsrc, uint32_t n)
     if (fused_2d_) {
         run_fused(dsrc, n);
     } else {
-        uint32_t n3 = 0;
-        if (fused_3d_) {
-            bool idle = lv_[0].frames_written % g3d_ == 0 &&
-                        reinterpret_cast<uintptr_t>(dsrc) % 16 == 0;
-            for (const auto& pd : pend_)
-                idle &= !pd.has;
-            if (idle)
-                n3 = n / g3d_ * g3d_;
-        }
         if (n3 > 0)
             run_fused3d(dsrc, n3);
         if (n3 < n)
@@ -2434,10 +2445,14 @@ Stage::dominant_kernel() const
                                        : "transpose_frames + fused_pyramid");
         return strip ? "fused_pyramid_strip" : "fused_pyramid";
     }
-    if (fused_3d_) // launch_fused_pyramid_3d's choice
-        return rh_log2_ == 6 && n_levels() - 1 <= 4 && !(knobs_ & 256u)
-                 ? "fused_pyramid_strip3d"
-                 : "fused_pyramid_3d";
+    if (fused_3d_) { // launch_fused_pyramid_3d's choice
+        const bool strip = rh_log2_ == 6 && n_levels() - 1 <= 4 && !(knobs_ & 256u);
+        if (xy_)
+            return xy_direct_ ? "fused_pyramid_strip3d (XY load)"
+                   : strip    ? "transpose_frames + fused_pyramid_strip3d"
+                              : "transpose_frames + fused_pyramid_3d";
+        return strip ? "fused_pyramid_strip3d" : "fused_pyramid_3d";
+    }
     return "level_kernel";
 }
 

@@ -1487,8 +1487,11 @@ fused_pyramid_3d(const FusedParams p)
 // (downsampler.cpp:366-385, average_two_frames :208-246), so the cascade
 // needs no LDS and no barrier.  NTM as fused_pyramid_strip.  Host
 // guarantees as fused_pyramid_3d, plus rh_log2 == 6 and n_fused <= 4.
+// XY: the planes are in acquisition order (XY-transposed storage order,
+// array.cpp:488-534): each plane's region comes through load_region_xy, the
+// strip kernel's LDS transpose (a barrier per plane; no prefetch).
 // ---------------------------------------------------------------------------
-template<typename T, int M, int NTM, int PF>
+template<typename T, int M, int NTM, int PF, bool XY = false>
 __global__ __launch_bounds__(256) void
 fused_pyramid_strip3d(const FusedParams p)
 {
@@ -1521,8 +1524,9 @@ fused_pyramid_strip3d(const FusedParams p)
     const uint32_t zm = p.zmask;
     const uint32_t ry = 16 * w + 2 * hw;
     const uint64_t row = uint64_t(p.W[0]) * sizeof(T);
-    const uint8_t* src0 = p.src + uint64_t(grp * G) * p.src_stride +
-                          uint64_t(y0 + ry) * row + uint64_t(x0 + cv * VEC) * sizeof(T);
+    const uint8_t* src0 = XY ? p.src
+                             : p.src + uint64_t(grp * G) * p.src_stride +
+                                 uint64_t(y0 + ry) * row + uint64_t(x0 + cv * VEC) * sizeof(T);
     const bool v3ok = lane < 32 && (cv % S3) == 0;
     const bool v4ok = lane < 32 && (cv % S4) == 0;
 
@@ -1540,6 +1544,12 @@ fused_pyramid_strip3d(const FusedParams p)
     // they are in flight while levels 1-4 are formed and stored
     uint4 ra[4], rb[4];
     auto load_plane = [&](uint32_t pl) {
+        if constexpr (XY) {
+            if (pl > 0)
+                __syncthreads(); // every wave has gathered the previous plane
+            load_region_xy<T, NTM>(p, grp * G + pl, y0, x0, ry, cv, ra, rb);
+            return;
+        }
         const uint8_t* s = src0 + uint64_t(pl) * p.src_stride;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -2003,11 +2013,20 @@ launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
         return hipSuccess;
     // the register-cascade kernel takes 64-row regions down to 4 fused levels
     const bool strip = p.rh_log2 == 6 && p.n_fused <= 4 && !(p.knobs & 256u);
+    // acquisition-order planes: only through the strip kernel's XY load
+    if (p.xy && !(strip && dtype != 3 && dtype != 7 && dtype != 9))
+        return hipErrorInvalidValue;
     const FusedParams pr = with_xcd_rotation(p, blocks);
 #define CALL(T, MM)                                                            \
     do {                                                                       \
         const dim3 gd{ uint32_t(blocks), 1, 1 };                              \
-        if (strip && p.nt && (p.knobs & 512u))                                \
+        if (p.xy && p.nt)                                                     \
+            hipLaunchKernelGGL((fused_pyramid_strip3d<T, MM, 7, 0, true>), gd, dim3(256), \
+                               0, stream, pr);                                 \
+        else if (p.xy)                                                        \
+            hipLaunchKernelGGL((fused_pyramid_strip3d<T, MM, 0, 0, true>), gd, dim3(256), \
+                               0, stream, pr);                                 \
+        else if (strip && p.nt && (p.knobs & 512u))                           \
             hipLaunchKernelGGL((fused_pyramid_strip3d<T, MM, 7, 0>), gd, dim3(256), 0, \
                                stream, pr);                                    \
         else if (strip && p.nt)                                               \
