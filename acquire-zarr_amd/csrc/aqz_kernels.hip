@@ -964,7 +964,7 @@ fused_pyramid(const FusedParams p)
 template<typename T, int NTM>
 __device__ __forceinline__ void
 load_region_xy(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0, uint32_t ry,
-               uint32_t cv, uint4 (&ra)[4], uint4 (&rb)[4])
+               uint32_t cv, uint4 (&ra)[4], uint4 (&rb)[4], uint32_t tid = threadIdx.x)
 {
     typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
     typedef typename std::conditional<
@@ -981,13 +981,13 @@ load_region_xy(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0, uint3
     u32x4v v[8];
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j) {
-        const uint32_t idx = threadIdx.x + 256u * j;
+        const uint32_t idx = tid + 256u * j;
         const uint32_t r = idx / VR, c16 = idx % VR;
         v[j] = gload<(NTM & 1) != 0, u32x4v>(s + uint64_t(r) * pitch + c16 * 16u);
     }
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j) {
-        const uint32_t idx = threadIdx.x + 256u * j;
+        const uint32_t idx = tid + 256u * j;
         const uint32_t r = idx / VR, c16 = idx % VR;
         PT e[PV];
         __builtin_memcpy(e, &v[j], 16);
@@ -1547,7 +1547,12 @@ fused_pyramid_strip3d(const FusedParams p)
         if constexpr (XY) {
             if (pl > 0)
                 __syncthreads(); // every wave has gathered the previous plane
-            load_region_xy<T, NTM>(p, grp * G + pl, y0, x0, ry, cv, ra, rb);
+            // opaque per plane: the loop-invariant LDS / global addresses of
+            // the transpose are recomputed, not hoisted (and held) across
+            // the plane loop
+            uint32_t tid = threadIdx.x, ryo = ry, cvo = cv;
+            asm volatile("" : "+v"(tid), "+v"(ryo), "+v"(cvo));
+            load_region_xy<T, NTM>(p, grp * G + pl, y0, x0, ryo, cvo, ra, rb, tid);
             return;
         }
         const uint8_t* s = src0 + uint64_t(pl) * p.src_stride;
@@ -1750,6 +1755,269 @@ fused_pyramid_strip3d(const FusedParams p)
 #pragma unroll
             for (int j = 0; j < N4; ++j)
                 v4[j] = reduce2<M, T>(h4[j], v4[j]);
+        }
+        {
+            FastTile t4{};
+            if (v4ok)
+                t4 = fast_tile<T>(p, 4, grp * g4 + i4, (y0 >> 4) + w,
+                                  (x0 >> 4) + (cv / S4) * N4);
+            if (t4.p) {
+                gstore_px<T, N4, false>(t4.p, v4);
+                t4.nz |= any_nonzero<T, N4>(v4);
+            }
+            flush_tile_flag(t4);
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// 2x2x2 pyramids whose level 1 halves z, two planes at a time: 512 threads,
+// the first 256 on plane 2j, the second 256 on plane 2j+1 of the same
+// region (twice the loads in flight per workgroup, at the 2-D strip
+// kernel's register count).  Both halves store their level-0 tile rows and
+// form level 1 in registers; the first half hands its level-1 rows to the
+// second through LDS (double-buffered by j, one barrier per pair), and the
+// second half emits mean2(earlier, later) (average_two_frames,
+// downsampler.cpp:208-246) and carries levels 2-4 exactly as
+// fused_pyramid_strip3d does (later z pairs in registers across j).
+// The default where it applies; tuning knob 2 selects fused_pyramid_strip3d.
+// ---------------------------------------------------------------------------
+template<typename T, int M, int NTM>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void
+fused_pyramid_strip3d_pair(const FusedParams p)
+{
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+    constexpr int VEC = 16 / sizeof(T);
+    constexpr int HV = VEC / 2;
+    constexpr int QV = VEC / 4;
+    constexpr uint32_t RW = 32 * VEC;
+    static_assert(QV >= 1, "strip 3-D kernel needs <= 4-byte pixels");
+    constexpr int N3 = QV >= 2 ? QV / 2 : 1;
+    constexpr int S3 = QV >= 2 ? 1 : 2;
+    constexpr int N4 = N3 >= 2 ? N3 / 2 : 1;
+    constexpr int S4 = N3 >= 2 ? S3 : 2 * S3;
+    __shared__ uint2 xch[2][4][256]; // level-1 rows of plane 2j, by j parity
+
+    const uint32_t nreg = p.nbx_in * p.nby_in;
+    const uint32_t blk = region_of_block(p);
+    const uint32_t grp = fdiv(blk, p.d_nreg_in);
+    const uint32_t r = blk - grp * nreg;
+    uint32_t by, bx;
+    region_xy(p, r, by, bx, true);
+    const uint32_t y0 = by << 6;
+    const uint32_t x0 = bx * RW;
+    const uint32_t half = threadIdx.x >> 8;
+    const uint32_t t = threadIdx.x & 255u;
+    const uint32_t w = t >> 6;
+    const uint32_t hw = (t >> 5) & 1u;
+    const uint32_t lane = t & 63u;
+    const uint32_t cv = t & 31u;
+    const uint32_t trow = p.tw * uint32_t(sizeof(T));
+    const uint32_t nf = p.n_fused;
+    const uint32_t G = p.G;
+    const uint32_t zm = p.zmask; // bit 1 set (host)
+    const uint32_t ry = 16 * w + 2 * hw;
+    const uint64_t row = uint64_t(p.W[0]) * sizeof(T);
+    const uint8_t* src0 = p.src + uint64_t(grp * G + half) * p.src_stride +
+                          uint64_t(y0 + ry) * row + uint64_t(x0 + cv * VEC) * sizeof(T);
+    const bool v3ok = lane < 32 && (cv % S3) == 0;
+    const bool v4ok = lane < 32 && (cv % S4) == 0;
+    uint32_t h2[4];
+    T h3[2][N3], h4[N4];
+    const uint32_t g1 = G >> 1;
+    const uint32_t g2 = g1 >> ((zm >> 2) & 1u);
+    const uint32_t g3 = g2 >> ((zm >> 3) & 1u);
+    const uint32_t g4 = g3 >> ((zm >> 4) & 1u);
+
+    for (uint32_t j = 0; 2 * j < G; ++j) {
+        const uint32_t pl = 2 * j + half;
+        uint4 ra[4], rb[4];
+        {
+            const uint8_t* s = src0 + uint64_t(2 * j) * p.src_stride;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const u32x4v a = gload<(NTM & 1) != 0, u32x4v>(s + uint64_t(4 * i) * row);
+                const u32x4v b = gload<(NTM & 1) != 0, u32x4v>(s + uint64_t(4 * i + 1) * row);
+                ra[i] = uint4{ a.x, a.y, a.z, a.w };
+                rb[i] = uint4{ b.x, b.y, b.z, b.w };
+            }
+        }
+        // level 0: both halves
+        {
+            FastTile t0 = fast_tile<T>(p, 0, grp * G + pl, y0 + ry, x0 + cv * VEC);
+            if (t0.p) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    gstore<(NTM & 2) != 0>(t0.p + uint64_t(4 * i) * trow,
+                                           u32x4v{ ra[i].x, ra[i].y, ra[i].z, ra[i].w });
+                    gstore<(NTM & 2) != 0>(t0.p + uint64_t(4 * i + 1) * trow,
+                                           u32x4v{ rb[i].x, rb[i].y, rb[i].z, rb[i].w });
+                    t0.nz |= ((ra[i].x | ra[i].y | ra[i].z | ra[i].w) |
+                              (rb[i].x | rb[i].y | rb[i].z | rb[i].w)) != 0u;
+                }
+            }
+            flush_tile_flag(t0);
+        }
+        if (nf < 1)
+            continue;
+        // level-1 2x2 sums of this half's plane
+        uint2 o1[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            T r0[VEC], r1[VEC], o[HV];
+            __builtin_memcpy(r0, &ra[i], 16);
+            __builtin_memcpy(r1, &rb[i], 16);
+#pragma unroll
+            for (int q = 0; q < HV; ++q)
+                o[q] = reduce4<M, T>(r0[2 * q], r0[2 * q + 1], r1[2 * q], r1[2 * q + 1]);
+            __builtin_memcpy(&o1[i], o, 8);
+        }
+        if (half == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                xch[j & 1][i][t] = o1[i];
+        }
+        __syncthreads();
+        if (half == 0)
+            continue;
+        // second half: the pair's level 1, then levels 2-4 as strip3d with
+        // the level-1 frame index j (the odd plane of the pair emits)
+        uint32_t i2 = j, i3, i4;
+        bool e2 = nf >= 2, e3, e4;
+        if (zm & 4u) {
+            e2 = e2 && (i2 & 1u);
+            i2 >>= 1;
+        }
+        i3 = i2;
+        e3 = e2 && nf >= 3;
+        if (zm & 8u) {
+            e3 = e3 && (i3 & 1u);
+            i3 >>= 1;
+        }
+        i4 = i3;
+        e4 = e3 && nf >= 4;
+        if (zm & 16u) {
+            e4 = e4 && (i4 & 1u);
+            i4 >>= 1;
+        }
+        FastTile t1 = fast_tile<T>(p, 1, grp * g1 + j, (y0 >> 1) + 8 * w + hw,
+                                   (x0 >> 1) + cv * HV);
+        FastTile t2{};
+        if (e2 && lane < 32)
+            t2 = fast_tile<T>(p, 2, grp * g2 + i2, (y0 >> 2) + 4 * w, (x0 >> 2) + cv * QV);
+        uint32_t q2w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            T o[HV], a[HV];
+            __builtin_memcpy(o, &o1[i], 8);
+            const uint2 e = xch[j & 1][i][t];
+            __builtin_memcpy(a, &e, 8);
+#pragma unroll
+            for (int q = 0; q < HV; ++q)
+                o[q] = reduce2<M, T>(a[q], o[q]);
+            if (t1.p) {
+                gstore_px<T, HV, (NTM & 4) != 0>(t1.p + uint64_t(2 * i) * trow, o);
+                t1.nz |= any_nonzero<T, HV>(o);
+            }
+            if (nf < 2)
+                continue;
+            uint2 mine, below;
+            __builtin_memcpy(&mine, o, 8);
+            below.x = __shfl_xor(mine.x, 32);
+            below.y = __shfl_xor(mine.y, 32);
+            T b[HV], q[QV];
+            __builtin_memcpy(b, &below, 8);
+#pragma unroll
+            for (int k = 0; k < QV; ++k)
+                q[k] = reduce4<M, T>(o[2 * k], o[2 * k + 1], b[2 * k], b[2 * k + 1]);
+            if (zm & 4u) {
+                if (!e2) {
+                    __builtin_memcpy(&h2[i], q, 4);
+                    continue;
+                }
+                T hq[QV];
+                __builtin_memcpy(hq, &h2[i], 4);
+#pragma unroll
+                for (int k = 0; k < QV; ++k)
+                    q[k] = reduce2<M, T>(hq[k], q[k]);
+            }
+            if (t2.p) {
+                gstore_px<T, QV, (NTM & 4) != 0>(t2.p + uint64_t(i) * trow, q);
+                t2.nz |= any_nonzero<T, QV>(q);
+            }
+            __builtin_memcpy(&q2w[i], q, 4);
+        }
+        flush_tile_flag(t1);
+        flush_tile_flag(t2);
+        if (!e2 || nf < 3)
+            continue;
+        T v3[2][N3];
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+            T a[QV], c[QV];
+            __builtin_memcpy(a, &q2w[2 * rr], 4);
+            __builtin_memcpy(c, &q2w[2 * rr + 1], 4);
+            if constexpr (QV >= 2) {
+#pragma unroll
+                for (int k = 0; k < N3; ++k)
+                    v3[rr][k] = reduce4<M, T>(a[2 * k], a[2 * k + 1], c[2 * k], c[2 * k + 1]);
+            } else {
+                const T ar = shfl_down_t(a[0], 1), cr = shfl_down_t(c[0], 1);
+                v3[rr][0] = reduce4<M, T>(a[0], ar, c[0], cr);
+            }
+        }
+        if (zm & 8u) {
+            if (!e3) {
+#pragma unroll
+                for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+                    for (int k = 0; k < N3; ++k)
+                        h3[rr][k] = v3[rr][k];
+                continue;
+            }
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+                for (int k = 0; k < N3; ++k)
+                    v3[rr][k] = reduce2<M, T>(h3[rr][k], v3[rr][k]);
+        }
+        {
+            FastTile t3{};
+            if (v3ok)
+                t3 = fast_tile<T>(p, 3, grp * g3 + i3, (y0 >> 3) + 2 * w,
+                                  (x0 >> 3) + (cv / S3) * N3);
+            if (t3.p) {
+#pragma unroll
+                for (int rr = 0; rr < 2; ++rr) {
+                    gstore_px<T, N3, false>(t3.p + uint64_t(rr) * trow, v3[rr]);
+                    t3.nz |= any_nonzero<T, N3>(v3[rr]);
+                }
+            }
+            flush_tile_flag(t3);
+        }
+        if (nf < 4)
+            continue;
+        T v4[N4];
+        if constexpr (N3 >= 2) {
+#pragma unroll
+            for (int k = 0; k < N4; ++k)
+                v4[k] = reduce4<M, T>(v3[0][2 * k], v3[0][2 * k + 1], v3[1][2 * k],
+                                      v3[1][2 * k + 1]);
+        } else {
+            const T ar = shfl_down_t(v3[0][0], S3), cr = shfl_down_t(v3[1][0], S3);
+            v4[0] = reduce4<M, T>(v3[0][0], ar, v3[1][0], cr);
+        }
+        if (zm & 16u) {
+            if (!e4) {
+#pragma unroll
+                for (int k = 0; k < N4; ++k)
+                    h4[k] = v4[k];
+                continue;
+            }
+#pragma unroll
+            for (int k = 0; k < N4; ++k)
+                v4[k] = reduce2<M, T>(h4[k], v4[k]);
         }
         {
             FastTile t4{};
@@ -2013,6 +2281,11 @@ launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
         return hipSuccess;
     // the register-cascade kernel takes 64-row regions down to 4 fused levels
     const bool strip = p.rh_log2 == 6 && p.n_fused <= 4 && !(p.knobs & 256u);
+    // two planes at a time (fused_pyramid_strip3d_pair) when level 1 halves
+    // z and the group holds whole pairs: 0.8-1.3% faster than one plane at a
+    // time on C4, same stage (profiles/r04_c4_pair_ab.txt); knob 2 keeps
+    // fused_pyramid_strip3d
+    const bool pair = strip && !(p.knobs & 2u) && (p.zmask & 2u) && p.G % 2 == 0;
     // acquisition-order planes: only through the strip kernel's XY load
     if (p.xy && !(strip && dtype != 3 && dtype != 7 && dtype != 9))
         return hipErrorInvalidValue;
@@ -2023,6 +2296,9 @@ launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
         if (p.xy && p.nt)                                                     \
             hipLaunchKernelGGL((fused_pyramid_strip3d<T, MM, 7, 0, true>), gd, dim3(256), \
                                0, stream, pr);                                 \
+        else if (pair && p.nt)                                                \
+            hipLaunchKernelGGL((fused_pyramid_strip3d_pair<T, MM, 7>), gd, dim3(512), 0, \
+                               stream, pr);                                    \
         else if (p.xy)                                                        \
             hipLaunchKernelGGL((fused_pyramid_strip3d<T, MM, 0, 0, true>), gd, dim3(256), \
                                0, stream, pr);                                 \

@@ -120,7 +120,7 @@ def test_c4_volume_exact(gpu, c4_volume):
     c, frames, exp, fw, ldims = c4_volume
     dims, B = c["dims"], c["batch"]
     st = gpu.Stage(dims, U16, MEAN, max_batch_frames=B, layer_slots=2)
-    assert st.dominant_kernel() == "fused_pyramid_strip3d"
+    assert st.dominant_kernel() == "fused_pyramid_strip3d_pair"
     assert st.n_levels() == 4 == len(ldims)
     assert [st.level_dims(l)[1][1] for l in range(4)] == [256, 128, 64, 64]
     ring = _device_ring(frames)

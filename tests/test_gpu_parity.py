@@ -312,8 +312,9 @@ def test_stage_timing_marks(gpu):
 # the register-cascade kernel (fused_pyramid_strip3d; tuning knob 512: its
 # variant without the next-plane prefetch) and, with knob 256, the
 # LDS-cascade kernel it replaced (fused_pyramid_3d)
-KERNELS_3D = {"strip3d": (0, "fused_pyramid_strip3d"),
-              "strip3d_nopf": (512, "fused_pyramid_strip3d"),
+KERNELS_3D = {"strip3d_pair": (0, "fused_pyramid_strip3d_pair"),
+              "strip3d": (2, "fused_pyramid_strip3d"),
+              "strip3d_nopf": (2 | 512, "fused_pyramid_strip3d"),
               "lds3d": (256, "fused_pyramid_3d")}
 
 
@@ -378,7 +379,7 @@ def test_stage_3d_five_levels(gpu, dtype):
     but not z after three that halve both."""
     dims = [(TIME, 0, 1, 1), (SPACE, 64, 8, 1), (SPACE, 1024, 64, 1), (SPACE, 1024, 64, 1)]
     st = gpu.Stage(dims, dtype, MEAN)
-    assert st.dominant_kernel() == "fused_pyramid_strip3d"
+    assert st.dominant_kernel() == "fused_pyramid_strip3d_pair"
     assert st.n_levels() == 5
     assert [st.level_dims(l)[1][1] for l in range(5)] == [64, 32, 16, 8, 8]
     st.close()
@@ -693,7 +694,7 @@ def test_stage_xy_fused_strip3d(gpu, dtype, path):
         st = gpu.Stage(acq, dtype, m, storage_order=[0, 1, 3, 2], max_batch_frames=16,
                        layer_slots=4, knobs=knobs)
         want = "fused_pyramid_strip3d (XY load)" if path == "fused" else \
-            "transpose_frames + fused_pyramid_strip3d"
+            "transpose_frames + fused_pyramid_strip3d_pair"
         assert st.dominant_kernel() == want
         assert st.n_levels() == len(ldims) == 4
         i = 0
