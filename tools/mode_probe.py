@@ -1,4 +1,8 @@
 #!/usr/bin/env python3
+# HISTORICAL (rounds 2-3): the AQZ_* environment switches this probe sets were
+# removed in round 4 (kernel tuning is only in aqz_stage_bench_options, e.g.
+# aqz.Stage(..., knobs=..., chunk_pad_bytes=...)); kept for the provenance of
+# the profiles/ files it produced.
 """Dev probe (not product): is the fast/slow mode of the C2 stage kernel a
 property of the stage's own allocations, of the source ring, or of the
 pair?  Creates S stages (bench C2 geometry, 128-frame launches) and R source

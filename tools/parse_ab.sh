@@ -1,3 +1,6 @@
+# HISTORICAL (rounds 2-3): the environment switch this script sets was removed in
+# round 4 (tuning is only in aqz_stage_bench_options); kept for the provenance of
+# the profiles/ files it produced.
 # dev: zstd L3 parse cost split (AQZ_ZSTD_DBG: 1 no far verification, 2 no far reads)
 set -o pipefail
 cd $GRAFT_REPO_ROOT

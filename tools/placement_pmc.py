@@ -1,4 +1,8 @@
 #!/usr/bin/env python3
+# HISTORICAL (rounds 2-3): the AQZ_* environment switches this probe sets were
+# removed in round 4 (kernel tuning is only in aqz_stage_bench_options, e.g.
+# aqz.Stage(..., knobs=..., chunk_pad_bytes=...)); kept for the provenance of
+# the profiles/ files it produced.
 """Dev probe (not product): what separates a fast chunk-ring placement from a
 slow one?  Creates S stages of the bench C2 geometry in ONE process with the
 creation-time search off (AQZ_PLACEMENT_TRIES=1), so each lands its rings

@@ -1,3 +1,6 @@
+# HISTORICAL (rounds 2-3): the environment switch this script sets was removed in
+# round 4 (tuning is only in aqz_stage_bench_options); kept for the provenance of
+# the profiles/ files it produced.
 # A/B of the PCIe stream priority (AQZ_COPY_PRIORITY) on the e2e path.
 set -o pipefail
 cd $GRAFT_REPO_ROOT

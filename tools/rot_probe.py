@@ -1,4 +1,8 @@
 #!/usr/bin/env python3
+# HISTORICAL (rounds 2-3): the AQZ_* environment switches this probe sets were
+# removed in round 4 (kernel tuning is only in aqz_stage_bench_options, e.g.
+# aqz.Stage(..., knobs=..., chunk_pad_bytes=...)); kept for the provenance of
+# the profiles/ files it produced.
 """Dev probe (not product): the XCD walk rotation (FusedParams.xcd_rot,
 tuning knob bits 16-31) against placement bands.  S stages held together
 (S placements, creation-time search off); every stage is timed under every

@@ -22,7 +22,7 @@ for a in "--config c3 --batch 32" "--config c3 --batch 64" "--config c2 --pyrami
 done
 for i in 1 2; do
   ab - "--config c2 --xy --steps 400 --warmup 10" || exit 6
-  ab AQZ_KNOBS=4096 "--config c2 --xy --steps 400 --warmup 10" || exit 6
+  ab - "--config c2 --xy --tune knobs=4096 --steps 400 --warmup 10" || exit 6
 done
 bash tools/profile.sh c2 r03 || exit 2
 bash tools/profile.sh c2 r03 pyr || exit 3

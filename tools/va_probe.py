@@ -1,4 +1,8 @@
 #!/usr/bin/env python3
+# HISTORICAL (rounds 2-3): the AQZ_* environment switches this probe sets were
+# removed in round 4 (kernel tuning is only in aqz_stage_bench_options, e.g.
+# aqz.Stage(..., knobs=..., chunk_pad_bytes=...)); kept for the provenance of
+# the profiles/ files it produced.
 """Dev probe (not product): does the stage's slow/fast mode follow the
 virtual addresses of its chunk-layer rings?  Creates stages one after the
 other with placement calibration off (AQZ_PLACEMENT_TRIES=1), shifting the
