@@ -7,217 +7,217 @@ export TMPDIR=/tmp
 
 # knob tests + placement localisation (one process)
 step_g1() {
-  mkdir -p gpurun_out/r4a
-  timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider -k "environment or 3d_shallow or xy_fused or async_handoff" > gpurun_out/r4a/pytest.log 2>&1 || { tail -30 gpurun_out/r4a/pytest.log; exit 1; }
-  tail -3 gpurun_out/r4a/pytest.log
-  timeout -k 10 300 python3 -u tools/placement_localize.py --trials 5 > gpurun_out/r4a/localize.jsonl 2> gpurun_out/r4a/localize.err || { tail gpurun_out/r4a/localize.err; exit 1; }
-  tail -2 gpurun_out/r4a/localize.jsonl
+mkdir -p gpurun_out/r4a
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider -k "environment or 3d_shallow or xy_fused or async_handoff" > gpurun_out/r4a/pytest.log 2>&1 || { tail -30 gpurun_out/r4a/pytest.log; exit 1; }
+tail -3 gpurun_out/r4a/pytest.log
+timeout -k 10 300 python3 -u tools/placement_localize.py --trials 5 > gpurun_out/r4a/localize.jsonl 2> gpurun_out/r4a/localize.err || { tail gpurun_out/r4a/localize.err; exit 1; }
+tail -2 gpurun_out/r4a/localize.jsonl
 }
 
 # placement localisation, one process per plan
 step_g2() {
-  O=gpurun_out/r4b
-  mkdir -p $O
-  for plan in "start,src,src" "start,L=0x1e" "start,L=0x2,L=0x4,L=0x8,L=0x10" \
-              "start,L=0x10,L=0x8,L=0x4,L=0x2" "pre=4096,start" "pre=16384,start" \
-              "start,L=1,L=1,L=1" "start,all,all" "start,src,L=0x1e,L=1"; do
-    timeout -k 10 120 python3 -u tools/placement_localize.py --plan "$plan" >> $O/plans.jsonl 2>> $O/plans.err || { tail $O/plans.err; exit 1; }
-  done
-  cat $O/plans.jsonl
+O=gpurun_out/r4b
+mkdir -p $O
+for plan in "start,src,src" "start,L=0x1e" "start,L=0x2,L=0x4,L=0x8,L=0x10" \
+            "start,L=0x10,L=0x8,L=0x4,L=0x2" "pre=4096,start" "pre=16384,start" \
+            "start,L=1,L=1,L=1" "start,all,all" "start,src,L=0x1e,L=1"; do
+  timeout -k 10 120 python3 -u tools/placement_localize.py --plan "$plan" >> $O/plans.jsonl 2>> $O/plans.err || { tail $O/plans.err; exit 1; }
+done
+cat $O/plans.jsonl
 }
 
 # contiguous vs hipMalloc ring sets
 step_g3() {
-  O=gpurun_out/r4c
-  mkdir -p $O
-  for i in 1 2 3; do
-  for fl in 4 0; do
-    timeout -k 10 120 python3 -u tools/placement_localize.py --ring-flags $fl --plan "start,all,all,all,all" >> $O/plans.jsonl 2>> $O/plans.err || { tail $O/plans.err; exit 1; }
-  done
-  done
-  cat $O/plans.jsonl
+O=gpurun_out/r4c
+mkdir -p $O
+for i in 1 2 3; do
+for fl in 4 0; do
+  timeout -k 10 120 python3 -u tools/placement_localize.py --ring-flags $fl --plan "start,all,all,all,all" >> $O/plans.jsonl 2>> $O/plans.err || { tail $O/plans.err; exit 1; }
+done
+done
+cat $O/plans.jsonl
 }
 
 # contiguous spacer sweep
 step_g4() {
-  O=gpurun_out/r4d
-  mkdir -p $O
-  for S in 0 4 7 9 10.5 12 16 24 48 96 160; do
-    timeout -k 10 120 python3 -u tools/placement_localize.py --ring-flags 4 --spacer-gib $S --plan "start,all" >> $O/plans.jsonl 2>> $O/plans.err || { tail $O/plans.err; exit 1; }
-  done
-  for S in 12 48; do
-    timeout -k 10 120 python3 -u tools/placement_localize.py --ring-flags 0 --spacer-gib $S --plan "start,all" >> $O/plans.jsonl 2>> $O/plans.err || { tail $O/plans.err; exit 1; }
-  done
-  cat $O/plans.jsonl
+O=gpurun_out/r4d
+mkdir -p $O
+for S in 0 4 7 9 10.5 12 16 24 48 96 160; do
+  timeout -k 10 120 python3 -u tools/placement_localize.py --ring-flags 4 --spacer-gib $S --plan "start,all" >> $O/plans.jsonl 2>> $O/plans.err || { tail $O/plans.err; exit 1; }
+done
+for S in 12 48; do
+  timeout -k 10 120 python3 -u tools/placement_localize.py --ring-flags 0 --spacer-gib $S --plan "start,all" >> $O/plans.jsonl 2>> $O/plans.err || { tail $O/plans.err; exit 1; }
+done
+cat $O/plans.jsonl
 }
 
 # placement search variants through bench.py
 step_g5() {
-  O=gpurun_out/r4e
-  mkdir -p $O
-  run() { timeout -k 10 180 python3 bench.py --steps 200 --warmup 5 --no-cpu-baseline --no-pyramid-only-line --no-hbm-probe "$@" > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
-    python3 -c "import json,sys; d=json.load(open('$O/tmp.json')); r=d['roofline']; p=r['placement']; print(json.dumps({'args': sys.argv[1:], 'frac': r['frac'], 'ms': r['kernel_avg_ms'], 'cand': p['candidates_ms'], 'kept': p['kept'], 'peak_gb': round(p['peak_device_bytes']/1e9,2)}))" "$@" >> $O/runs.jsonl; }
-  run --placement-tries 16
-  run --placement-tries 16 --tune ring_malloc_flags=4
-  run --placement-tries 8 --tune placement_mode=1
-  run --placement-tries 8 --tune placement_mode=1 --tune ring_malloc_flags=4
-  run --placement-tries 16 --tune placement_spacer_bytes=1073741824
-  run --placement-tries 16 --tune placement_spacer_bytes=4294967296 --tune ring_malloc_flags=4
-  cat $O/runs.jsonl
+O=gpurun_out/r4e
+mkdir -p $O
+run() { timeout -k 10 180 python3 bench.py --steps 200 --warmup 5 --no-cpu-baseline --no-pyramid-only-line --no-hbm-probe "$@" > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open('$O/tmp.json')); r=d['roofline']; p=r['placement']; print(json.dumps({'args': sys.argv[1:], 'frac': r['frac'], 'ms': r['kernel_avg_ms'], 'cand': p['candidates_ms'], 'kept': p['kept'], 'peak_gb': round(p['peak_device_bytes']/1e9,2)}))" "$@" >> $O/runs.jsonl; }
+run --placement-tries 16
+run --placement-tries 16 --tune ring_malloc_flags=4
+run --placement-tries 8 --tune placement_mode=1
+run --placement-tries 8 --tune placement_mode=1 --tune ring_malloc_flags=4
+run --placement-tries 16 --tune placement_spacer_bytes=1073741824
+run --placement-tries 16 --tune placement_spacer_bytes=4294967296 --tune ring_malloc_flags=4
+cat $O/runs.jsonl
 }
 
 # binding replay + golden tests, first binding timing
 step_g6() {
-  O=gpurun_out/r4f
-  mkdir -p $O
-  timeout -k 10 500 python3 -u -m pytest tests/test_gpu_handoff.py tests/test_gpu_golden.py -m gpu -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1; rc=$?
-  tail -40 $O/pytest.log
-  [ $rc -le 1 ] || exit 1
-  timeout -k 10 300 python3 -u tools/binding_e2e.py > $O/binding_e2e.jsonl 2> $O/binding_e2e.err || { tail $O/binding_e2e.err; exit 1; }
-  cat $O/binding_e2e.jsonl
+O=gpurun_out/r4f
+mkdir -p $O
+timeout -k 10 500 python3 -u -m pytest tests/test_gpu_handoff.py tests/test_gpu_golden.py -m gpu -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1; rc=$?
+tail -40 $O/pytest.log
+[ $rc -le 1 ] || exit 1
+timeout -k 10 300 python3 -u tools/binding_e2e.py > $O/binding_e2e.jsonl 2> $O/binding_e2e.err || { tail $O/binding_e2e.err; exit 1; }
+cat $O/binding_e2e.jsonl
 }
 
 # binding sweep (copy threads, slots, batch) vs bench e2e
 step_g7() {
-  O=gpurun_out/r4g
-  mkdir -p $O
-  rm -f $O/sweep.jsonl
-  timeout -k 10 300 python3 -u -m pytest tests/test_gpu_handoff.py tests/test_gpu_parity.py -m gpu -q --timeout 200 --timeout-method thread -p no:cacheprovider -k "replay or slab" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
-  tail -2 $O/pytest.log
-  for args in "--copy-threads 8 --host-slots 3" "--copy-threads 8 --batch 128" "--copy-threads 6" "--copy-threads 8 --pool-threads 8"; do
-    echo "# $args" >> $O/sweep.jsonl
-    timeout -k 10 200 python3 -u tools/binding_e2e.py --frames 2048 --codecs raw,lz4,zstd-1 $args >> $O/sweep.jsonl 2> $O/sweep.err || { tail $O/sweep.err; exit 1; }
-  done
-  for src in pageable pinned; do for c in none lz4; do
-    timeout -k 10 200 python3 bench.py --config c2-ref4 --e2e $src --codec $c --compress 1 --steps 16 --warmup 2 >> $O/bench_e2e.jsonl 2> $O/bench.err || { tail $O/bench.err; exit 1; }
-  done; done
-  cat $O/sweep.jsonl | python3 -c "
-  import sys, json
-  for l in sys.stdin:
-      if l.startswith('#'): print(l.strip()); continue
-      d=json.loads(l); print(d['codec_name'], d['input_gbs'], d['seconds'])"
-  python3 -c "
-  import json
-  for l in open('$O/bench_e2e.jsonl'):
-      d=json.loads(l); print(d['config']['workload'][-30:], d['metric'][-60:], d['value'])"
+O=gpurun_out/r4g
+mkdir -p $O
+rm -f $O/sweep.jsonl
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_handoff.py tests/test_gpu_parity.py -m gpu -q --timeout 200 --timeout-method thread -p no:cacheprovider -k "replay or slab" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+for args in "--copy-threads 8 --host-slots 3" "--copy-threads 8 --batch 128" "--copy-threads 6" "--copy-threads 8 --pool-threads 8"; do
+  echo "# $args" >> $O/sweep.jsonl
+  timeout -k 10 200 python3 -u tools/binding_e2e.py --frames 2048 --codecs raw,lz4,zstd-1 $args >> $O/sweep.jsonl 2> $O/sweep.err || { tail $O/sweep.err; exit 1; }
+done
+for src in pageable pinned; do for c in none lz4; do
+  timeout -k 10 200 python3 bench.py --config c2-ref4 --e2e $src --codec $c --compress 1 --steps 16 --warmup 2 >> $O/bench_e2e.jsonl 2> $O/bench.err || { tail $O/bench.err; exit 1; }
+done; done
+cat $O/sweep.jsonl | python3 -c "
+import sys, json
+for l in sys.stdin:
+    if l.startswith('#'): print(l.strip()); continue
+    d=json.loads(l); print(d['codec_name'], d['input_gbs'], d['seconds'])"
+python3 -c "
+import json
+for l in open('$O/bench_e2e.jsonl'):
+    d=json.loads(l); print(d['config']['workload'][-30:], d['metric'][-60:], d['value'])"
 }
 
 # binding rate vs bench.py e2e, same box
 step_g8() {
-  O=gpurun_out/r4h
-  mkdir -p $O
-  rm -f $O/*.jsonl
-  for rep in 1 2 3; do
-    timeout -k 10 300 python3 -u tools/binding_e2e.py --frames 4096 --codecs raw,lz4,lz4-bit,blosc-zstd,zstd-1 >> $O/binding.jsonl 2> $O/b.err || { tail $O/b.err; exit 1; }
+O=gpurun_out/r4h
+mkdir -p $O
+rm -f $O/*.jsonl
+for rep in 1 2 3; do
+  timeout -k 10 300 python3 -u tools/binding_e2e.py --frames 4096 --codecs raw,lz4,lz4-bit,blosc-zstd,zstd-1 >> $O/binding.jsonl 2> $O/b.err || { tail $O/b.err; exit 1; }
+done
+for src in pageable pinned; do
+  timeout -k 10 200 python3 bench.py --config c2-ref4 --e2e $src --steps 32 --warmup 2 >> $O/bench_e2e.jsonl 2> $O/bench.err || { tail $O/bench.err; exit 1; }
+  for c in lz4 zstd; do
+  timeout -k 10 200 python3 bench.py --config c2-ref4 --e2e $src --codec $c --compress 1 --steps 32 --warmup 2 >> $O/bench_e2e.jsonl 2> $O/bench.err || { tail $O/bench.err; exit 1; }
   done
-  for src in pageable pinned; do
-    timeout -k 10 200 python3 bench.py --config c2-ref4 --e2e $src --steps 32 --warmup 2 >> $O/bench_e2e.jsonl 2> $O/bench.err || { tail $O/bench.err; exit 1; }
-    for c in lz4 zstd; do
-    timeout -k 10 200 python3 bench.py --config c2-ref4 --e2e $src --codec $c --compress 1 --steps 32 --warmup 2 >> $O/bench_e2e.jsonl 2> $O/bench.err || { tail $O/bench.err; exit 1; }
-    done
-  done
-  python3 -c "
-  import json
-  for l in open('$O/binding.jsonl'):
-      d=json.loads(l); print('binding', d['codec_name'], d['input_gbs'])
-  for l in open('$O/bench_e2e.jsonl'):
-      d=json.loads(l); print('bench', d['config']['workload'][-20:], d['metric'][-45:], d['value'])"
+done
+python3 -c "
+import json
+for l in open('$O/binding.jsonl'):
+    d=json.loads(l); print('binding', d['codec_name'], d['input_gbs'])
+for l in open('$O/bench_e2e.jsonl'):
+    d=json.loads(l); print('bench', d['config']['workload'][-20:], d['metric'][-45:], d['value'])"
 }
 
 # binding replay tests incl. z slabs
 step_g9() {
-  O=gpurun_out/r4i
-  mkdir -p $O
-  timeout -k 10 500 python3 -u -m pytest tests/test_gpu_handoff.py -m gpu -q -x --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1; rc=$?
-  tail -30 $O/pytest.log
-  exit $rc
+O=gpurun_out/r4i
+mkdir -p $O
+timeout -k 10 500 python3 -u -m pytest tests/test_gpu_handoff.py -m gpu -q -x --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1; rc=$?
+tail -30 $O/pytest.log
+exit $rc
 }
 
 # placement search strategies, twice
 step_g10() {
-  O=gpurun_out/r4j
-  mkdir -p $O
-  rm -f $O/runs.jsonl
-  run() { timeout -k 10 240 python3 bench.py --steps 200 --warmup 5 --no-cpu-baseline --no-pyramid-only-line --no-hbm-probe "$@" > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
-    python3 -c "import json,sys; d=json.load(open('$O/tmp.json')); r=d['roofline']; p=r['placement']; print(json.dumps({'args': sys.argv[1:], 'frac': r['frac'], 'ms': r['kernel_avg_ms'], 'c0': r.get('candidate0_ms'), 'kept': p['kept'], 'n': len(p['candidates_ms']), 'peak_gb': round(p['peak_device_bytes']/1e9,2)}))" "$@" >> $O/runs.jsonl; }
-  for rep in 1 2; do
-  run --placement-tries 16
-  run --placement-tries 16 --tune placement_spacer_bytes=2147483648
-  run --placement-tries 16 --tune placement_spacer_bytes=4294967296 --tune ring_malloc_flags=4
-  run --placement-tries 16 --tune placement_spacer_bytes=4294967296
-  run --placement-tries 12 --tune placement_mode=1 --tune ring_malloc_flags=4
-  done
-  cat $O/runs.jsonl
+O=gpurun_out/r4j
+mkdir -p $O
+rm -f $O/runs.jsonl
+run() { timeout -k 10 240 python3 bench.py --steps 200 --warmup 5 --no-cpu-baseline --no-pyramid-only-line --no-hbm-probe "$@" > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open('$O/tmp.json')); r=d['roofline']; p=r['placement']; print(json.dumps({'args': sys.argv[1:], 'frac': r['frac'], 'ms': r['kernel_avg_ms'], 'c0': r.get('candidate0_ms'), 'kept': p['kept'], 'n': len(p['candidates_ms']), 'peak_gb': round(p['peak_device_bytes']/1e9,2)}))" "$@" >> $O/runs.jsonl; }
+for rep in 1 2; do
+run --placement-tries 16
+run --placement-tries 16 --tune placement_spacer_bytes=2147483648
+run --placement-tries 16 --tune placement_spacer_bytes=4294967296 --tune ring_malloc_flags=4
+run --placement-tries 16 --tune placement_spacer_bytes=4294967296
+run --placement-tries 12 --tune placement_mode=1 --tune ring_malloc_flags=4
+done
+cat $O/runs.jsonl
 }
 
 # strip kernel occupancy A/B
 step_g11() {
-  O=gpurun_out/r4k
-  mkdir -p $O
-  K=0,$((2<<13)),$((3<<13)),$((4<<13)),$((5<<13)),$((6<<13))
-  timeout -k 10 300 python3 -u tools/knob_ab.py --config c2 --knobs $K --instances 2 > $O/occ_ab2.txt 2>&1 || { tail $O/occ_ab2.txt; exit 1; }
-  timeout -k 10 300 python3 -u tools/knob_ab.py --config c2 --knobs $K --instances 2 --placement-tries 16 >> $O/occ_ab2.txt 2>&1 || { tail $O/occ_ab2.txt; exit 1; }
-  cat $O/occ_ab2.txt
+O=gpurun_out/r4k
+mkdir -p $O
+K=0,$((2<<13)),$((3<<13)),$((4<<13)),$((5<<13)),$((6<<13))
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c2 --knobs $K --instances 2 > $O/occ_ab2.txt 2>&1 || { tail $O/occ_ab2.txt; exit 1; }
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c2 --knobs $K --instances 2 --placement-tries 16 >> $O/occ_ab2.txt 2>&1 || { tail $O/occ_ab2.txt; exit 1; }
+cat $O/occ_ab2.txt
 }
 
 # 3-D parity incl. XY and pair kernels, C4 A/B
 step_g12() {
-  O=gpurun_out/r4l
-  mkdir -p $O
-  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider -k "3d or c4 or xy" > $O/pytest.log 2>&1; rc=$?
-  tail -15 $O/pytest.log
-  [ $rc -eq 0 ] || exit 1
-  timeout -k 10 300 python3 -u tools/knob_ab.py --config c4 --knobs 0,2,512 --instances 3 > $O/c4_ab.txt 2>&1 || { tail $O/c4_ab.txt; exit 1; }
-  cat $O/c4_ab.txt
-  timeout -k 10 300 python3 bench.py --config c4 --xy --steps 100 --warmup 5 --no-cpu-baseline --no-pyramid-only-line > $O/c4xy.json 2> $O/c4xy.err || { tail $O/c4xy.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$O/c4xy.json')); r=d['roofline']; print('c4 xy', r['kernel'], r['kernel_avg_ms'], r['frac'], r.get('frac_of_probed_ceiling'))"
+O=gpurun_out/r4l
+mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider -k "3d or c4 or xy" > $O/pytest.log 2>&1; rc=$?
+tail -15 $O/pytest.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c4 --knobs 0,2,512 --instances 3 > $O/c4_ab.txt 2>&1 || { tail $O/c4_ab.txt; exit 1; }
+cat $O/c4_ab.txt
+timeout -k 10 300 python3 bench.py --config c4 --xy --steps 100 --warmup 5 --no-cpu-baseline --no-pyramid-only-line > $O/c4xy.json 2> $O/c4xy.err || { tail $O/c4xy.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/c4xy.json')); r=d['roofline']; print('c4 xy', r['kernel'], r['kernel_avg_ms'], r['frac'], r.get('frac_of_probed_ceiling'))"
 }
 
 # C4 pair kernel A/B on searched placements
 step_g13() {
-  O=gpurun_out/r4m
-  mkdir -p $O
-  timeout -k 10 300 python3 -u tools/knob_ab.py --config c4 --knobs 0,2,0,2 --instances 3 --placement-tries 16 > $O/c4_ab_search.txt 2>&1 || { tail $O/c4_ab_search.txt; exit 1; }
-  cat $O/c4_ab_search.txt
+O=gpurun_out/r4m
+mkdir -p $O
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c4 --knobs 0,2,0,2 --instances 3 --placement-tries 16 > $O/c4_ab_search.txt 2>&1 || { tail $O/c4_ab_search.txt; exit 1; }
+cat $O/c4_ab_search.txt
 }
 
 # full GPU suite + smoke + default bench
 step_full() {
-  O=gpurun_out/r4full
-  mkdir -p $O
-  timeout -k 10 1200 python3 -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1; rc=$?
-  tail -15 $O/pytest.log
-  [ $rc -eq 0 ] || exit 1
-  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
-  tail -1 $O/smoke.log
-  timeout -k 10 600 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
-  python3 -c "
-  import json; d=json.load(open('$O/bench.json')); r=d['roofline']; p=r['placement']
-  print(d['value'], d['ms_per_step'], r['frac'], r.get('candidate0_ms'), r.get('kept_ms'), p['candidates_ms'], round(p['peak_device_bytes']/1e9,2))"
+O=gpurun_out/r4full
+mkdir -p $O
+timeout -k 10 1200 python3 -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1; rc=$?
+tail -15 $O/pytest.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 600 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
+python3 -c "
+import json; d=json.load(open('$O/bench.json')); r=d['roofline']; p=r['placement']
+print(d['value'], d['ms_per_step'], r['frac'], r.get('candidate0_ms'), r.get('kept_ms'), p['candidates_ms'], round(p['peak_device_bytes']/1e9,2))"
 }
 
 # round-4 rocprofv3 profiles + default bench
 step_prof() {
-  # then the default bench line
-  NO_SQ=1 bash tools/profile.sh c2 r04 || exit 1
-  NO_SQ=1 bash tools/profile.sh c2 r04 pyr || exit 1
-  NO_SQ=1 bash tools/profile.sh c4 r04 || exit 1
-  mkdir -p gpurun_out/r4bench
-  timeout -k 10 600 python3 bench.py > gpurun_out/r4bench/bench_default.json 2> gpurun_out/r4bench/bench_default.err || { tail gpurun_out/r4bench/bench_default.err; exit 1; }
-  cat gpurun_out/r4bench/bench_default.json
+# then the default bench line
+NO_SQ=1 bash tools/profile.sh c2 r04 || exit 1
+NO_SQ=1 bash tools/profile.sh c2 r04 pyr || exit 1
+NO_SQ=1 bash tools/profile.sh c4 r04 || exit 1
+mkdir -p gpurun_out/r4bench
+timeout -k 10 600 python3 bench.py > gpurun_out/r4bench/bench_default.json 2> gpurun_out/r4bench/bench_default.err || { tail gpurun_out/r4bench/bench_default.err; exit 1; }
+cat gpurun_out/r4bench/bench_default.json
 }
 
 # C4 pair profile and XY lines
 step_prof2() {
-  # XY-transposed C2 / C4 bench lines against their live probes
-  NO_SQ=1 bash tools/profile.sh c4 r04b || exit 1
-  mkdir -p gpurun_out/r4xy
-  for c in c2 c4; do
-    timeout -k 10 300 python3 bench.py --config $c --xy --steps 200 --warmup 5 --no-cpu-baseline --no-pyramid-only-line > gpurun_out/r4xy/$c.json 2> gpurun_out/r4xy/$c.err || { tail gpurun_out/r4xy/$c.err; exit 1; }
-  done
-  timeout -k 10 300 python3 bench.py --config c4 --steps 200 --warmup 5 --no-cpu-baseline --no-pyramid-only-line > gpurun_out/r4xy/c4_plain.json 2> gpurun_out/r4xy/c4p.err || { tail gpurun_out/r4xy/c4p.err; exit 1; }
-  for f in gpurun_out/r4xy/*.json; do python3 -c "
-  import json,sys; d=json.load(open('$f')); r=d['roofline']; print('$f', r['kernel'], r['kernel_avg_ms'], r['frac'], r.get('frac_of_probed_ceiling'), r.get('candidate0_ms'))"; done
+# XY-transposed C2 / C4 bench lines against their live probes
+NO_SQ=1 bash tools/profile.sh c4 r04b || exit 1
+mkdir -p gpurun_out/r4xy
+for c in c2 c4; do
+  timeout -k 10 300 python3 bench.py --config $c --xy --steps 200 --warmup 5 --no-cpu-baseline --no-pyramid-only-line > gpurun_out/r4xy/$c.json 2> gpurun_out/r4xy/$c.err || { tail gpurun_out/r4xy/$c.err; exit 1; }
+done
+timeout -k 10 300 python3 bench.py --config c4 --steps 200 --warmup 5 --no-cpu-baseline --no-pyramid-only-line > gpurun_out/r4xy/c4_plain.json 2> gpurun_out/r4xy/c4p.err || { tail gpurun_out/r4xy/c4p.err; exit 1; }
+for f in gpurun_out/r4xy/*.json; do python3 -c "
+import json,sys; d=json.load(open('$f')); r=d['roofline']; print('$f', r['kernel'], r['kernel_avg_ms'], r['frac'], r.get('frac_of_probed_ceiling'), r.get('candidate0_ms'))"; done
 }
 
 "step_$1"
