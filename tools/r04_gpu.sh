@@ -220,4 +220,22 @@ for f in gpurun_out/r4xy/*.json; do python3 -c "
 import json,sys; d=json.load(open('$f')); r=d['roofline']; print('$f', r['kernel'], r['kernel_avg_ms'], r['frac'], r.get('frac_of_probed_ceiling'), r.get('candidate0_ms'))"; done
 }
 
+# C4 pair kernel: region walk order A/B (knob 1024 flips column-major)
+step_g14() {
+O=gpurun_out/r4n
+mkdir -p $O
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c4 --knobs 0,1024,2,0,1024 --instances 3 --placement-tries 16 > $O/c4_walk_ab.txt 2>&1 || { tail $O/c4_walk_ab.txt; exit 1; }
+cat $O/c4_walk_ab.txt
+}
+
+# C2 strip kernel: chunk-major region walk (an experimental knob bit 31, since
+# removed: 13-17% slower, profiles/r04_c2_walk_order_ab.txt) vs frame by frame
+step_g15() {
+O=gpurun_out/r4o
+mkdir -p $O
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c2 --knobs 0,2147483648,0,2147483648 --instances 2 > $O/c2_walk_ab.txt 2>&1 || { tail $O/c2_walk_ab.txt; exit 1; }
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c2 --knobs 0,2147483648,0,2147483648 --instances 2 --placement-tries 16 >> $O/c2_walk_ab.txt 2>&1 || { tail $O/c2_walk_ab.txt; exit 1; }
+cat $O/c2_walk_ab.txt
+}
+
 "step_$1"
