@@ -502,7 +502,9 @@ Stage::calibrate_placement()
     uint32_t n = opt_.max_batch_frames;
     if (fused_3d_ && !fused_2d_)
         n = n / g3d_ * g3d_;
-    if (tries <= 1 || n == 0 || !(fused_2d_ || fused_3d_) || xy_ ||
+    // XY stages search too when the strip kernels read acquisition order
+    // themselves; with the separate transpose pass they keep the first
+    if (tries <= 1 || n == 0 || !(fused_2d_ || fused_3d_) || (xy_ && !xy_direct_) ||
         ring_bytes < (uint64_t(256) << 20))
         return;
     const uint64_t fb0 = uint64_t(lv_[0].W) * lv_[0].H * bpp_;

@@ -15,6 +15,7 @@ import argparse
 import ctypes as C
 import json
 import os
+import resource
 import sys
 import time
 
@@ -596,7 +597,12 @@ def main():
             nd = len(cfg["dims"])
             kw["storage_order"] = list(range(nd - 2)) + [nd - 1, nd - 2]
         est = aqz.estimate_memory(cfg["dims"], dt, cfg["method"], **kw)
+        tc = time.perf_counter()
         st = aqz.Stage(cfg["dims"], dt, cfg["method"], device=dev.index, z_slab=slab, **kw)
+        # what creation costs a rank: wall time (with the placement search)
+        # and the process's peak host RSS so far
+        create_s = time.perf_counter() - tc
+        rss_mib = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0
         # the stage runs on its own HIP stream; the timing marks below are
         # recorded by the library on that same stream
         sizes = level_sizes(st)
@@ -643,6 +649,8 @@ def main():
         kernel = st.dominant_kernel()
         placement = st.placement()
         placement["estimate_device_bytes"] = est["device_bytes"]
+        placement["stage_create_s"] = round(create_s, 3)
+        placement["host_peak_rss_mib"] = round(rss_mib, 1)
         placement["rings_bytes"] = sum(
             x["chunk_pitch"] * x["chunks_per_layer"] * x["layer_slots"]
             for x in (st.layout(l) for l in range(len(sizes))))

@@ -50,18 +50,25 @@ def _check_layer(st, l, layer, exp):
     assert np.array_equal(gflags, flags), f"has_data L{l} layer{layer}"
 
 
-@pytest.mark.parametrize("cfg", ["c2", "c2-ref4"])
+@pytest.mark.parametrize("cfg", ["c2", "c2-ref4", "c2-xy"])
 def test_bench_c2_configuration_exact(gpu, cfg):
-    c = bench.CONFIGS[cfg]
+    """The bench's C2 stages, placement search included, oracle-exact;
+    c2-xy is `bench.py --xy` (XY-transposed storage order, the transpose
+    fused into the strip kernel's loads)."""
+    xy = cfg == "c2-xy"
+    c = bench.CONFIGS["c2" if xy else cfg]
     dims, B = c["dims"], c["batch"]
     h, w = dims[-2][1], dims[-1][1]
     slots = bench.layer_slots_for(c, B)
     kw = dict(force_levels=c["force_levels"], max_batch_frames=B, layer_slots=slots,
               **bench.PLACEMENT)
+    if xy:
+        assert h == w  # storage dims equal acquisition dims
+        kw["storage_order"] = [0, 2, 1]
     est = gpu.estimate_memory(dims, U16, MEAN, **kw)
     st = gpu.Stage(dims, U16, MEAN, **kw)
     L = st.n_levels()
-    assert L == (5 if cfg == "c2" else 4)
+    assert L == (4 if cfg == "c2-ref4" else 5)
     # the bench's placement search ran; its creation peak is within the
     # bench estimate, and the stage keeps one ring set afterwards
     pl = st.placement()
@@ -71,21 +78,25 @@ def test_bench_c2_configuration_exact(gpu, cfg):
     assert pl["peak_device_bytes"] <= est["device_bytes"]
     assert st.memory_usage()["device_bytes"] <= gpu.estimate_memory(
         dims, U16, MEAN, force_levels=c["force_levels"], max_batch_frames=B,
-        layer_slots=slots)["device_bytes"]
+        layer_slots=slots, storage_order=kw.get("storage_order"))["device_bytes"]
     ldims = [st.level_dims(l) for l in range(L)]
     assert [d[-1][1] for d in ldims] == [2048, 1024, 512, 256, 128][:L]
     assert all(d[-1][2] == 256 and d[-2][2] == 256 for d in ldims)
     if cfg == "c2":
         assert st.dominant_kernel() == "fused_pyramid_strip"
+    if xy:
+        assert st.dominant_kernel() == "fused_pyramid_strip (XY load)"
     # oracle pixels: the reference rule at 128-px chunks gives the same
     # 5 levels (c2); c2-ref4 is the reference configuration itself
     odims = list(dims)
-    if c["force_levels"]:
+    if c["force_levels"]:  # c2, c2-xy
         odims[-1] = (SPACE, w, 128, 1)
         odims[-2] = (SPACE, h, 128, 1)
     n = 2 * max(B, 128)
     frames = distinct_frames(n, h, w, 7 + L)
-    exp, fw, _ = expected_stage_layers(odims, U16, MEAN, frames, level_dims=ldims)
+    stored = np.ascontiguousarray(frames.transpose(0, 2, 1)) if xy else frames
+    exp, fw, _ = expected_stage_layers(odims, U16, MEAN, stored, level_dims=ldims)
+    del stored
     assert len(fw) == L
     ring = _device_ring(frames)
     F = [st.layout(l)["frames_per_layer"] for l in range(L)]

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--nt", type=int, default=7)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--placement-tries", type=int, default=0)
+    ap.add_argument("--xy", action="store_true", help="XY-transposed storage order")
     args = ap.parse_args()
     c = bench.CONFIGS[args.config]
     B = c["batch"]
@@ -33,10 +34,12 @@ def main():
     src = torch.empty(2 * B * fbytes, dtype=torch.uint8, device="cuda")
     src.view(torch.int16).random_(-32768, 32767)
     knobs = [int(x) for x in args.knobs.split(",")]
+    nd = len(c["dims"])
+    xy = dict(storage_order=list(range(nd - 2)) + [nd - 1, nd - 2]) if args.xy else {}
     for inst in range(args.instances):
         st = aqz.Stage(c["dims"], c["dtype"], c["method"], max_batch_frames=B,
                        layer_slots=bench.layer_slots_for(c, B), force_levels=c["force_levels"],
-                       placement_tries=args.placement_tries)
+                       placement_tries=args.placement_tries, **xy)
         row = []
         for rnd in range(2):
             for j, k in enumerate(knobs):

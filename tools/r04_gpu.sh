@@ -238,4 +238,27 @@ timeout -k 10 300 python3 -u tools/knob_ab.py --config c2 --knobs 0,2147483648,0
 cat $O/c2_walk_ab.txt
 }
 
+# XY-transposed storage order: row-major vs column-major region walk (knob
+# 1024) on the fused XY loads
+step_g16() {
+O=gpurun_out/r4p
+mkdir -p $O
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c2 --xy --knobs 0,1024,0,1024 --instances 2 --placement-tries 16 > $O/xy_walk_ab.txt 2>&1 || { tail $O/xy_walk_ab.txt; exit 1; }
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c4 --xy --knobs 0,1024,0,1024 --instances 2 --placement-tries 16 >> $O/xy_walk_ab.txt 2>&1 || { tail $O/xy_walk_ab.txt; exit 1; }
+cat $O/xy_walk_ab.txt
+}
+
+# XY stages now run the placement search: exactness at the bench layout,
+# then the XY bench lines (C2, C4) at the default search
+step_g17() {
+O=gpurun_out/r4q
+mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_headline.py -k "c2_configuration" > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
+tail -5 $O/pytest.txt
+for c in c2 c4; do
+timeout -k 10 240 python3 bench.py --config $c --xy --steps 200 --warmup 5 --no-cpu-baseline --no-pyramid-only-line > $O/xy_$c.json 2> $O/xy_$c.err || { tail $O/xy_$c.err; exit 1; }
+tail -1 $O/xy_$c.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$c', d['value'], r['frac'], r.get('frac_of_probed_ceiling'), r['placement'].get('candidates_ms'), r['placement'].get('stage_create_s'), r['placement'].get('host_peak_rss_mib'))"
+done
+}
+
 "step_$1"
