@@ -2449,13 +2449,16 @@ Stage::dominant_kernel() const
     }
     if (fused_3d_) { // launch_fused_pyramid_3d's choice
         const bool strip = rh_log2_ == 6 && n_levels() - 1 <= 4 && !(knobs_ & 256u);
-        const bool pair = strip && !(knobs_ & 2u) && (zmask3d_ & 2u) && g3d_ % 2 == 0;
+        const bool pair = strip && !(knobs_ & 2u) && (zmask3d_ & 2u) && g3d_ % 2 == 0 &&
+                          nt_mode_ != 0;
         const char* k = pair    ? "fused_pyramid_strip3d_pair"
                         : strip ? "fused_pyramid_strip3d"
                                 : "fused_pyramid_3d";
+        if (xy_ && xy_direct_)
+            return pair ? "fused_pyramid_strip3d_pair (XY load)"
+                        : "fused_pyramid_strip3d (XY load)";
         if (xy_)
-            return xy_direct_ ? "fused_pyramid_strip3d (XY load)"
-                   : pair     ? "transpose_frames + fused_pyramid_strip3d_pair"
+            return pair       ? "transpose_frames + fused_pyramid_strip3d_pair"
                    : strip    ? "transpose_frames + fused_pyramid_strip3d"
                               : "transpose_frames + fused_pyramid_3d";
         return k;

@@ -888,13 +888,19 @@ with_xcd_rotation(const FusedParams& p, uint64_t blocks)
 __device__ __forceinline__ void
 region_xy(const FusedParams& p, uint32_t q, uint32_t& by, uint32_t& bx, bool colmajor)
 {
-    if (colmajor != ((p.knobs & 1024u) != 0)) {
-        bx = q / p.nby_in;
-        by = q - bx * p.nby_in;
+    // values, then selects: assigning by / bx inside the branches made the
+    // compiler pick the store address per branch and keep both in scratch
+    const bool cm = colmajor != ((p.knobs & 1024u) != 0);
+    uint32_t a, b;
+    if (cm) {
+        a = q / p.nby_in; // column
+        b = q - a * p.nby_in;
     } else {
-        by = fdiv(q, p.d_nbx_in);
-        bx = q - by * p.nbx_in;
+        a = fdiv(q, p.d_nbx_in); // row
+        b = q - a * p.nbx_in;
     }
+    by = cm ? b : a;
+    bx = cm ? a : b;
 }
 
 // Interior regions, one per workgroup (region r of n_frames * nby_in * nbx_in).
@@ -961,10 +967,13 @@ fused_pyramid(const FusedParams p)
 // = the row below, both from one LDS read per pixel pair.  Pair index pc of
 // row r sits at (pc + r + r / VEC) mod 32, so the 32 lanes of a gather
 // (rows cv * VEC + k) hit distinct banks.
-template<typename T, int NTM>
+// SLOTS tiles of LDS, one per group of 256 threads loading its own region
+// (slot = the group; fused_pyramid_strip3d_pair loads two planes at once).
+template<typename T, int NTM, int SLOTS = 1>
 __device__ __forceinline__ void
 load_region_xy(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0, uint32_t ry,
-               uint32_t cv, uint4 (&ra)[4], uint4 (&rb)[4], uint32_t tid = threadIdx.x)
+               uint32_t cv, uint4 (&ra)[4], uint4 (&rb)[4], uint32_t tid = threadIdx.x,
+               uint32_t slot = 0)
 {
     typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
     typedef typename std::conditional<
@@ -974,7 +983,8 @@ load_region_xy(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0, uint3
     constexpr uint32_t RW = 32 * VEC;      // acquisition rows of the region
     constexpr uint32_t VR = 4 * sizeof(T); // 16-B vectors per 64-pixel row segment
     constexpr uint32_t PV = 8 / sizeof(T); // column pairs per 16-B vector
-    __shared__ PT xt[RW * 32];             // 32 KiB
+    __shared__ PT xt_slots[SLOTS * RW * 32]; // 32 KiB per slot
+    PT* const xt = xt_slots + slot * (RW * 32);
     const uint64_t pitch = uint64_t(p.H[0]) * sizeof(T); // acquisition row bytes
     const uint8_t* s =
       p.src + uint64_t(f) * p.src_stride + uint64_t(x0) * pitch + uint64_t(y0) * sizeof(T);
@@ -1782,9 +1792,11 @@ fused_pyramid_strip3d(const FusedParams p)
 // downsampler.cpp:208-246) and carries levels 2-4 exactly as
 // fused_pyramid_strip3d does (later z pairs in registers across j).
 // The default where it applies; tuning knob 2 selects fused_pyramid_strip3d.
+// XY: acquisition-order planes, each half through load_region_xy with its
+// own 32 KiB LDS tile (72 KiB per workgroup).
 // ---------------------------------------------------------------------------
-template<typename T, int M, int NTM>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void
+template<typename T, int M, int NTM, bool XY = false>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(XY ? 4 : 6))) void
 fused_pyramid_strip3d_pair(const FusedParams p)
 {
     typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
@@ -1819,8 +1831,9 @@ fused_pyramid_strip3d_pair(const FusedParams p)
     const uint32_t zm = p.zmask; // bit 1 set (host)
     const uint32_t ry = 16 * w + 2 * hw;
     const uint64_t row = uint64_t(p.W[0]) * sizeof(T);
-    const uint8_t* src0 = p.src + uint64_t(grp * G + half) * p.src_stride +
-                          uint64_t(y0 + ry) * row + uint64_t(x0 + cv * VEC) * sizeof(T);
+    const uint8_t* src0 = XY ? p.src
+                             : p.src + uint64_t(grp * G + half) * p.src_stride +
+                                 uint64_t(y0 + ry) * row + uint64_t(x0 + cv * VEC) * sizeof(T);
     const bool v3ok = lane < 32 && (cv % S3) == 0;
     const bool v4ok = lane < 32 && (cv % S4) == 0;
     uint32_t h2[4];
@@ -1833,7 +1846,13 @@ fused_pyramid_strip3d_pair(const FusedParams p)
     for (uint32_t j = 0; 2 * j < G; ++j) {
         const uint32_t pl = 2 * j + half;
         uint4 ra[4], rb[4];
-        {
+        if constexpr (XY) {
+            // the previous pair's gathers are behind the level-1 exchange's
+            // barrier; the transpose addresses are recomputed per pair
+            uint32_t tid = t, ryo = ry, cvo = cv;
+            asm volatile("" : "+v"(tid), "+v"(ryo), "+v"(cvo));
+            load_region_xy<T, NTM, 2>(p, grp * G + pl, y0, x0, ryo, cvo, ra, rb, tid, half);
+        } else {
             const uint8_t* s = src0 + uint64_t(2 * j) * p.src_stride;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -2293,7 +2312,10 @@ launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
 #define CALL(T, MM)                                                            \
     do {                                                                       \
         const dim3 gd{ uint32_t(blocks), 1, 1 };                              \
-        if (p.xy && p.nt)                                                     \
+        if (p.xy && pair && p.nt)                                             \
+            hipLaunchKernelGGL((fused_pyramid_strip3d_pair<T, MM, 7, true>), gd, dim3(512), \
+                               0, stream, pr);                                 \
+        else if (p.xy && p.nt)                                                \
             hipLaunchKernelGGL((fused_pyramid_strip3d<T, MM, 7, 0, true>), gd, dim3(256), \
                                0, stream, pr);                                 \
         else if (pair && p.nt)                                                \

@@ -672,17 +672,24 @@ def test_environment_cannot_change_drop_in_output(gpu, monkeypatch, env):
     st.close()
 
 
-@pytest.mark.parametrize("path", ["fused", "pass"])
+XY_KERNELS_3D = {"pair": (0, "fused_pyramid_strip3d_pair (XY load)"),
+                 "single": (2, "fused_pyramid_strip3d (XY load)"),
+                 "pass": (4096, "transpose_frames + fused_pyramid_strip3d_pair")}
+
+
+@pytest.mark.parametrize("path", sorted(XY_KERNELS_3D))
 @pytest.mark.parametrize("dtype", [U8, U16, I16, U32, F32], ids=lambda d: DTYPE_NAMES[d])
 def test_stage_xy_fused_strip3d(gpu, dtype, path):
     """XY-transposed storage order on a 2x2x2 pyramid (transpose_frame,
     array.cpp:488-534): the 3-D strip kernel reads the acquisition-order
     planes itself (load_region_xy, one LDS transpose per plane), knob 4096
     the separate transpose pass.  Batches of whole z groups take the fused
-    load; a batch that also needs the generic cascade (6 planes: one z group
-    and a carried pair) is transposed first.  Either way every level equals
-    the oracle's on the transposed frames."""
-    knobs = 0 if path == "fused" else 4096
+    load -- two planes at a time by default (fused_pyramid_strip3d_pair, each
+    half of the workgroup its own LDS tile), one at a time with knob 2; a
+    batch that also needs the generic cascade (6 planes: one z group and a
+    carried pair) is transposed first.  Either way every level equals the
+    oracle's on the transposed frames."""
+    knobs, want = XY_KERNELS_3D[path]
     # acquisition (t, z, y, x) = (*, 16, 1024, 768) -> storage x = 1024 (a
     # multiple of the 512-B region), storage y = 768 (64-row regions)
     acq = [(TIME, 0, 1, 1), (SPACE, 16, 4, 1), (SPACE, 1024, 128, 1), (SPACE, 768, 128, 1)]
@@ -693,8 +700,6 @@ def test_stage_xy_fused_strip3d(gpu, dtype, path):
         exp, fw, ldims = expected_stage_layers(store, dtype, m, stored)
         st = gpu.Stage(acq, dtype, m, storage_order=[0, 1, 3, 2], max_batch_frames=16,
                        layer_slots=4, knobs=knobs)
-        want = "fused_pyramid_strip3d (XY load)" if path == "fused" else \
-            "transpose_frames + fused_pyramid_strip3d_pair"
         assert st.dominant_kernel() == want
         assert st.n_levels() == len(ldims) == 4
         i = 0

@@ -261,4 +261,37 @@ tail -1 $O/xy_$c.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read
 done
 }
 
+# XY on 2x2x2 pyramids, two planes at a time: parity, then the same-stage
+# A/B against one plane at a time (knob 2), then the C4 --xy bench line
+step_g18() {
+O=gpurun_out/r4r
+mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "xy_fused_strip3d" > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
+tail -3 $O/pytest.txt
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c4 --xy --knobs 0,2,0,2 --instances 3 --placement-tries 16 > $O/xy_pair_ab.txt 2>&1 || { tail $O/xy_pair_ab.txt; exit 1; }
+cat $O/xy_pair_ab.txt
+timeout -k 10 240 python3 bench.py --config c4 --xy --steps 200 --warmup 5 --no-cpu-baseline --no-pyramid-only-line > $O/xy_c4.json 2> $O/xy_c4.err || { tail $O/xy_c4.err; exit 1; }
+tail -1 $O/xy_c4.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('c4', d['value'], r['kernel'], r['frac'], r.get('frac_of_probed_ceiling'), r['placement'].get('candidates_ms'))"
+}
+
+# build A/B: the previous library (acquire-zarr_amd/abx/libaqz_gpu_prev.so,
+# region_xy through scratch) against the current one, alternating, each with
+# its own placement search
+step_g19() {
+O=gpurun_out/r4s
+mkdir -p $O
+: > $O/lib_ab.txt
+for c in c2 c4 c3; do
+for rep in 1 2; do
+for lib in prev cur; do
+if [ $lib = prev ]; then export AQZ_LIB=$PWD/acquire-zarr_amd/abx/libaqz_gpu_prev.so; else unset AQZ_LIB; fi
+timeout -k 10 240 python3 bench.py --config $c --steps 200 --warmup 5 --no-cpu-baseline --no-pyramid-only-line --no-hbm-probe > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+tail -1 $O/tmp.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; p=r['placement']; print('$c', '$lib', '$rep', round(r['achieved']/1e3*0+d['ms_per_step'],4), r['frac'], p.get('kept_ms_final'), min(p.get('candidates_ms') or [0]))" >> $O/lib_ab.txt
+done
+done
+done
+unset AQZ_LIB
+cat $O/lib_ab.txt
+}
+
 "step_$1"
