@@ -339,7 +339,7 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
     // writes the storage-order frames first.  Knob 4096: always transpose.
     if (xy_ && fused_2d_) {
         const bool tail = n_levels() - 1 > n_fused_;
-        xy_direct_ = bpp_ <= 4 && rh_log2_ == 6 && n_fused_ >= 3 && !(knobs_ & 128u) &&
+        xy_direct_ = bpp_ <= 4 && rh_log2_ == 6 && !(knobs_ & 128u) &&
                      (!tail || n_fused_ >= 5) && !(knobs_ & 4096u) &&
                      (uint64_t(acq_cols_) * bpp_) % 16 == 0;
     } else if (xy_ && fused_3d_) {
@@ -2439,8 +2439,8 @@ Stage::dominant_kernel() const
     if (fused_2d_) {
         // launch_interior's choice (aqz_kernels.hip) for this stage's launches
         const bool tail = n_levels() - 1 > n_fused_;
-        const bool strip = bpp_ <= 4 && rh_log2_ == 6 && n_fused_ >= 3 &&
-                           !(knobs_ & 128u) && (!tail || n_fused_ >= 5);
+        const bool strip = bpp_ <= 4 && rh_log2_ == 6 && !(knobs_ & 128u) &&
+                           (!tail || n_fused_ >= 5);
         if (xy_)
             return xy_direct_ ? "fused_pyramid_strip (XY load)"
                               : (strip ? "transpose_frames + fused_pyramid_strip"

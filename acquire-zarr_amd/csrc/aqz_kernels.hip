@@ -2216,7 +2216,7 @@ launch_interior(uint32_t blocks, const FusedParams& p, hipStream_t stream)
                                    dim3(256), 0, stream, p);
             return;
         }
-        if (p.rh_log2 == 6 && p.n_fused >= 3 && !(p.knobs & 128u) &&
+        if (p.rh_log2 == 6 && !(p.knobs & 128u) &&
             (p.scratch_level == 0 || p.scratch_level >= 5)) {
             // tuning knob bits 13-15 = v: unused LDS that caps the strip
             // kernel at v workgroups per CU (an occupancy A/B)
@@ -2270,7 +2270,7 @@ launch_fused_pyramid(int dtype, int method, const FusedParams& p,
     if (p.xy && interior &&
         !((dtype == 0 || dtype == 1 || dtype == 2 || dtype == 4 || dtype == 5 ||
            dtype == 6 || dtype == 8) &&
-          p.rh_log2 == 6 && p.n_fused >= 3 &&
+          p.rh_log2 == 6 &&
           !(p.knobs & 128u) && (p.scratch_level == 0 || p.scratch_level >= 5)))
         return hipErrorInvalidValue;
     const FusedParams pr = with_xcd_rotation(p, interior);

@@ -266,6 +266,43 @@ def test_stage_baseline_configs(gpu, cfg):
     _check_stage(gpu, dims, dt, m, frames, batch=2)
 
 
+@pytest.mark.parametrize("nf", [1, 2])
+@pytest.mark.parametrize("dtype", [U8, U16, I16, U32, F32], ids=lambda d: DTYPE_NAMES[d])
+def test_stage_shallow_pyramid_strip(gpu, dtype, nf):
+    """Pyramids of 2-3 levels (1-2 fused levels, e.g. C1's 3) on the strip
+    kernel's 64-row interior regions, every method; the same stages forced
+    onto fused_pyramid (knob 128); and XY-transposed storage order through
+    the strip kernel's XY load.  300 x 1100 frames at 128-px chunks: interior
+    regions plus ragged right and bottom edges."""
+    dims = [(TIME, 0, 4, 1), (SPACE, 300, 128, 1), (SPACE, 1100, 128, 1)]
+    for m in ALL_METHODS:
+        frames = _frames(dtype, 5, 300, 1100, 31 * nf + 7 * m + dtype)
+        for knobs, name in ((0, "fused_pyramid_strip"), (128, "fused_pyramid")):
+            st = gpu.Stage(dims, dtype, m, max_levels=nf, knobs=knobs)
+            assert st.n_levels() == nf + 1 and st.dominant_kernel() == name
+            st.close()
+            _check_stage(gpu, dims, dtype, m, frames, max_levels=nf, batch=3,
+                         knobs=knobs)
+    # XY: acquisition 1100 x 1088 -> storage 1088 rows x 1100 columns
+    acq = [(TIME, 0, 4, 1), (SPACE, 1100, 128, 1), (SPACE, 1088, 128, 1)]
+    frames = _frames(dtype, 5, 1100, 1088, 5 * nf + dtype)
+    stored = np.ascontiguousarray(frames.transpose(0, 2, 1))
+    exp, fw, ldims = expected_stage_layers([acq[0], acq[2], acq[1]], dtype, MEAN, stored,
+                                           nf)
+    st = gpu.Stage(acq, dtype, MEAN, storage_order=[0, 2, 1], max_levels=nf,
+                   max_batch_frames=3, layer_slots=4)
+    assert st.n_levels() == nf + 1
+    assert st.dominant_kernel() == "fused_pyramid_strip (XY load)"
+    st.append(frames[:3])
+    st.append(frames[3:])
+    st.finalize()
+    for (l, layer), (buf, flags) in sorted(exp.items()):
+        got, gflags = st.copy_layer(l, layer)
+        assert_same_pixels(got, buf, dtype, f"xy L{l} layer{layer}")
+        assert (gflags == flags).all(), (l, layer)
+    st.close()
+
+
 def test_stage_device_resident_input(gpu):
     import torch
     dims = [(TIME, 0, 2, 1), (SPACE, 256, 64, 1), (SPACE, 256, 64, 1)]

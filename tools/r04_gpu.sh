@@ -294,4 +294,32 @@ unset AQZ_LIB
 cat $O/lib_ab.txt
 }
 
+# BASELINE configs[0] (C1, u16 512^2, 3 levels, decimate): the device-resident
+# bench line with its CPU baseline, then the example end to end (raw and lz4,
+# to shard files on the box's /tmp and without the sink)
+step_g20() {
+O=gpurun_out/r4t
+mkdir -p $O
+timeout -k 10 300 python3 bench.py --config c1 --steps 100 --warmup 5 > $O/c1.json 2> $O/c1.err || { tail $O/c1.err; exit 1; }
+tail -2 $O/c1.json
+for codec in raw lz4; do
+for w in "--no-write" ""; do
+rm -rf /tmp/aqz_c1
+timeout -k 10 240 acquire-zarr_amd/examples/stream_to_filesystem /tmp/aqz_c1 --config c1 --frames 16384 --codec $codec --pattern camera $w >> $O/c1_e2e.jsonl 2> $O/c1_e2e.err || { tail $O/c1_e2e.err; exit 1; }
+done
+done
+rm -rf /tmp/aqz_c1
+cat $O/c1_e2e.jsonl
+}
+
+# the strip kernel for 0-2 fused levels (C1): parity, then the C1 bench line
+step_g21() {
+O=gpurun_out/r4u
+mkdir -p $O
+timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "shallow_pyramid_strip or baseline_configs or xy_fused_strip or tile_split_and_pyramid or max_levels" > $O/pytest.txt 2>&1 || { tail -40 $O/pytest.txt; exit 1; }
+tail -3 $O/pytest.txt
+timeout -k 10 300 python3 bench.py --config c1 --steps 100 --warmup 5 > $O/c1.json 2> $O/c1.err || { tail $O/c1.err; exit 1; }
+tail -1 $O/c1.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('c1', d['value'], r['kernel'], r['kernel_avg_ms'], r['frac'], r.get('frac_of_probed_ceiling'), d['pyramid_only']['kernel_input_frac_of_probed_ceiling'], d['cpu_baseline']['value'])"
+}
+
 "step_$1"
