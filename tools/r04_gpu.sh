@@ -322,4 +322,9 @@ timeout -k 10 300 python3 bench.py --config c1 --steps 100 --warmup 5 > $O/c1.js
 tail -1 $O/c1.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('c1', d['value'], r['kernel'], r['kernel_avg_ms'], r['frac'], r.get('frac_of_probed_ceiling'), d['pyramid_only']['kernel_input_frac_of_probed_ceiling'], d['cpu_baseline']['value'])"
 }
 
+# C1 on the strip kernel: kernel trace + PMC (traffic, SQ)
+step_prof3() {
+bash tools/profile.sh c1 r04 || exit 1
+}
+
 "step_$1"
