@@ -75,7 +75,8 @@ class StageBenchOptionsC(C.Structure):
                 ("nt_policy", C.c_uint32), ("xcd_rot", C.c_uint32),
                 ("region_rows_log2", C.c_uint32), ("zstd_flags", C.c_uint32),
                 ("ring_malloc_flags", C.c_uint32), ("chunk_pad_bytes", C.c_uint64),
-                ("ring_spacer_bytes", C.c_uint64)]
+                ("ring_spacer_bytes", C.c_uint64),
+                ("ring_arena_bytes", C.c_uint64)]
 
 
 # zstd_flags bits of aqz_stage_bench_options
@@ -258,6 +259,7 @@ def lib():
         "aqz_compressor_run": ([vp, vp, u64, u32, vp, sz, vp, vp], i32),
         "aqz_compressor_blocksize": ([vp], u32),
         "aqz_stage_bench_replace_rings": ([vp, u32], i32),
+        "aqz_stage_bench_set_ring_offset": ([vp, u64], i32),
         "aqz_stage_bind_host_thread": ([vp], i32),
         "aqz_stage_import_frames": ([vp, vp, u32, u64, u32, u32], i32),
         "aqz_stage_compression_done": ([vp, u32, u64, C.POINTER(C.c_int32)], i32),
@@ -601,6 +603,11 @@ class Stage:
         """Bench: fresh chunk-layer rings for the levels in level_mask (the
         old ones stay allocated); placement experiments only."""
         _check(lib().aqz_stage_bench_replace_rings(self.h, level_mask), "replace_rings")
+
+    def set_ring_offset(self, offset):
+        """Bench (ring_arena_bytes stages): every ring moved to arena +
+        offset; the stage restarts at frame 0."""
+        _check(lib().aqz_stage_bench_set_ring_offset(self.h, offset), "set_ring_offset")
 
     def set_tuning(self, knobs=0, nt=0):
         _check(lib().aqz_stage_set_tuning(self.h, knobs, nt), "set_tuning")

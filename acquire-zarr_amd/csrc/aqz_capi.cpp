@@ -497,6 +497,7 @@ apply_bench(const aqz_stage_bench_options* bench, StageOptions& o)
     o.chunk_pad = bench->chunk_pad_bytes;
     o.ring_malloc_flags = bench->ring_malloc_flags;
     o.ring_spacer = bench->ring_spacer_bytes;
+    o.ring_arena = bench->ring_arena_bytes;
     const uint32_t z = bench->zstd_flags;
     o.codec.match = (z & 1u) ? 0 : 1;
     o.codec.far = (z & 2u) ? 0 : 1;
@@ -693,6 +694,12 @@ aqz_status
 aqz_stage_bench_replace_rings(aqz_stage* st, uint32_t level_mask)
 {
     return guard_sticky(st, [&] { st->st->replace_rings(level_mask); });
+}
+
+aqz_status
+aqz_stage_bench_set_ring_offset(aqz_stage* st, uint64_t offset)
+{
+    return guard_sticky(st, [&] { st->st->set_ring_offset(offset); });
 }
 
 aqz_status

@@ -27,41 +27,56 @@ hip_check(hipError_t e, const char* what)
 
 DevBuf::~DevBuf()
 {
-    if (p)
+    if (p && !view)
         (void)hipFree(p);
 }
 
 DevBuf::DevBuf(DevBuf&& o) noexcept
   : p(o.p)
   , n(o.n)
+  , view(o.view)
 {
     o.p = nullptr;
     o.n = 0;
+    o.view = false;
 }
 
 DevBuf&
 DevBuf::operator=(DevBuf&& o) noexcept
 {
     if (this != &o) {
-        if (p)
+        if (p && !view)
             (void)hipFree(p);
         p = o.p;
         n = o.n;
+        view = o.view;
         o.p = nullptr;
         o.n = 0;
+        o.view = false;
     }
     return *this;
 }
 
 void
+DevBuf::set_view(uint8_t* q, size_t bytes)
+{
+    if (p && !view)
+        (void)hipFree(p);
+    p = q;
+    n = bytes;
+    view = true;
+}
+
+void
 DevBuf::alloc(size_t bytes, unsigned flags)
 {
-    if (p && n >= bytes)
+    if (p && !view && n >= bytes)
         return;
-    if (p)
+    if (p && !view)
         (void)hipFree(p);
     p = nullptr;
     n = 0;
+    view = false;
     if (bytes == 0)
         return;
     void* q = nullptr;
@@ -260,8 +275,12 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         if (P > 0x7fffffffull)
             throw Error(9, "chunk-layer ring period too large");
         L.period = uint32_t(P);
-        if (!(k == 0 && opt_.skip_level0_split))
-            place_level(L);
+        if (!(k == 0 && opt_.skip_level0_split)) {
+            if (opt_.ring_arena)
+                arena_rings_ += (L.slot_bytes * L.n_slots + 0xffffull) & ~0xffffull;
+            else
+                place_level(L);
+        }
         build_shard_order(L);
         L.tab_off.alloc(size_t(L.F) * 8);
         L.tab_grp.alloc(size_t(L.F) * 4);
@@ -273,6 +292,10 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
                   "hipMemcpy");
     }
 
+    if (opt_.ring_arena) {
+        arena_.alloc(arena_rings_ + opt_.ring_arena, opt_.ring_malloc_flags);
+        set_ring_offset(0);
+    }
     spacer = DevBuf{}; // freed: only the rings' placement needed it
 
     // 2-D fast path: z never shrinks and XY shrinks at every level, so every
@@ -445,9 +468,12 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
 // it stays zero for every layer that later occupies a slot; has_data words
 // start at 0 (no tag).
 void
-Stage::place_level(StageLevel& L)
+Stage::place_level(StageLevel& L, uint8_t* at)
 {
-    L.ring.alloc(L.slot_bytes * L.n_slots, opt_.ring_malloc_flags);
+    if (at)
+        L.ring.set_view(at, L.slot_bytes * L.n_slots);
+    else
+        L.ring.alloc(L.slot_bytes * L.n_slots, opt_.ring_malloc_flags);
     L.flags.alloc(size_t(L.n_chunks) * L.n_slots * 4);
     hip_check(hipMemsetAsync(L.ring.p, 0, L.ring.n, stream_), "hipMemsetAsync");
     hip_check(hipMemsetAsync(L.flags.p, 0, L.flags.n, stream_), "hipMemsetAsync");
@@ -504,7 +530,7 @@ Stage::calibrate_placement()
         n = n / g3d_ * g3d_;
     // XY stages search too when the strip kernels read acquisition order
     // themselves; with the separate transpose pass they keep the first
-    if (tries <= 1 || n == 0 || !(fused_2d_ || fused_3d_) || (xy_ && !xy_direct_) ||
+    if (tries <= 1 || n == 0 || !(fused_2d_ || fused_3d_) || (xy_ && !xy_direct_) || arena_.p ||
         ring_bytes < (uint64_t(256) << 20))
         return;
     const uint64_t fb0 = uint64_t(lv_[0].W) * lv_[0].H * bpp_;
@@ -624,6 +650,28 @@ Stage::calibrate_placement()
     hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
+}
+
+void
+Stage::set_ring_offset(uint64_t offset)
+{
+    if (!arena_.p)
+        throw Error(1, "the stage has no ring arena (bench option ring_arena_bytes)");
+    if (offset % 256 || offset + arena_rings_ > arena_.n)
+        throw Error(1, "ring offset outside the arena's slack (or not 256-B aligned)");
+    hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    uint64_t at = offset;
+    for (size_t k = 0; k < lv_.size(); ++k) {
+        StageLevel& L = lv_[k];
+        if (!(k == 0 && opt_.skip_level0_split)) {
+            place_level(L, arena_.p + at);
+            at += (L.slot_bytes * L.n_slots + 0xffffull) & ~0xffffull;
+        }
+        L.frames_written = 0;
+        L.level_frame_count = 0;
+        L.slot_layer.assign(L.n_slots, -1);
+    }
+    hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
 
 void

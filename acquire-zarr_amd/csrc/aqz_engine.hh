@@ -46,11 +46,13 @@ hipError_t launch_zero_frame_tiles(uint8_t* fb, uint64_t bpc,
 
 void hip_check(hipError_t e, const char* what);
 
-// Owning device allocation.
+// Owning device allocation (or, after set_view, a non-owning view into
+// another one).
 struct DevBuf
 {
     uint8_t* p = nullptr;
     size_t n = 0;
+    bool view = false;
     DevBuf() = default;
     explicit DevBuf(size_t bytes) { alloc(bytes); }
     ~DevBuf();
@@ -60,6 +62,8 @@ struct DevBuf
     DevBuf& operator=(DevBuf&& o) noexcept;
     // flags: hipExtMallocWithFlags flags (0 = hipMalloc)
     void alloc(size_t bytes, unsigned flags = 0);
+    // [q, q + bytes) of an allocation someone else owns (and frees)
+    void set_view(uint8_t* q, size_t bytes);
 };
 
 // Owning pinned host allocation.
@@ -213,6 +217,8 @@ struct StageOptions
     uint64_t chunk_pad = 0;        // device bytes between chunks of a layer
     uint32_t ring_malloc_flags = 0; // hipExtMallocWithFlags flags of the rings
     uint64_t ring_spacer = 0;       // allocated before the rings, freed after
+    uint64_t ring_arena = 0;        // > 0: every ring carved from one allocation
+                                    // with this much slack (set_ring_offset)
     CodecTuning codec;             // device zstd encoder A/B switches
 };
 
@@ -332,6 +338,9 @@ class Stage
     // levels in `mask`, holding the old ones until the stage is destroyed so
     // the new ones land elsewhere (placement experiments)
     void replace_rings(uint32_t mask);
+    // bench (ring_arena): move every level's ring to arena + offset (levels
+    // back to back, 64 KiB aligned); the stage restarts at frame 0
+    void set_ring_offset(uint64_t offset);
     void append(const void* frames, uint64_t n_frames, int mem);
     void synchronize();
     uint64_t frames_written(uint32_t level) const;
@@ -402,7 +411,7 @@ class Stage
     };
 
     void run_batch(const uint8_t* dsrc, uint32_t n);
-    void place_level(StageLevel& L);
+    void place_level(StageLevel& L, uint8_t* at = nullptr);
     void calibrate_placement();
     void build_shard_order(StageLevel& L);
     void ensure_comp_slots(StageLevel& L);
@@ -495,6 +504,8 @@ class Stage
     hipEvent_t ext_ev_ = nullptr;  // wait_stream
     PlacementReport placement_;         // creation-time placement search
     std::vector<DevBuf> held_;          // replace_rings: old rings kept allocated
+    DevBuf arena_;                      // ring_arena: every level's ring
+    uint64_t arena_rings_ = 0;          // bytes of the rings inside it
     bool finalized_ = false;
 };
 

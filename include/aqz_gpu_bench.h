@@ -62,6 +62,11 @@ typedef struct
                                   resident layer (chunk_pitch) */
     uint64_t ring_spacer_bytes; /* a device allocation (ring_malloc_flags) made
                                    before the rings and freed after them */
+    uint64_t ring_arena_bytes;  /* > 0: every level's ring is carved from ONE
+                                   allocation (ring_malloc_flags) with this much
+                                   slack, movable by
+                                   aqz_stage_bench_set_ring_offset; no
+                                   placement search */
 } aqz_stage_bench_options;
 
 /* aqz_stage_estimate_memory including the placement search's transient
@@ -99,6 +104,12 @@ aqz_status aqz_stage_set_tuning(aqz_stage* st, uint32_t knobs, uint32_t nt);
  * level_mask; the old ones stay allocated until the stage is destroyed, so
  * the new ones land in other memory.  Ring contents are lost (timing only). */
 aqz_status aqz_stage_bench_replace_rings(aqz_stage* st, uint32_t level_mask);
+
+/* ring_arena_bytes stages: move every level's ring to arena + offset bytes
+   (levels back to back, each 64 KiB aligned; offset a multiple of 256 and
+   within the slack).  Synchronises the stage, re-zeroes the rings and
+   restarts it at frame 0 (what was written is dropped). */
+aqz_status aqz_stage_bench_set_ring_offset(aqz_stage* st, uint64_t offset);
 
 /* Time every launch of the dominant (fused pyramid) kernel with HIP events
  * recorded on the stream it is launched on. */

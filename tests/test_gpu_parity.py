@@ -681,6 +681,29 @@ def test_stage_xy_transpose_sizes(gpu, dtype):
     st.close()
 
 
+def test_stage_ring_arena_offset(gpu):
+    """Bench option ring_arena_bytes (tools/arena_probe.py): every ring
+    carved from one allocation and moved inside it restarts the stage at
+    frame 0, oracle-exact at each offset."""
+    import aqz
+    dims = [(TIME, 0, 4, 1), (SPACE, 512, 128, 1), (SPACE, 512, 128, 1)]
+    frames = synthetic_frames(U16, 8, 512, 512, 17)
+    exp, fw, ldims = expected_stage_layers(dims, U16, MEAN, frames)
+    st = gpu.Stage(dims, U16, MEAN, layer_slots=3, max_batch_frames=8,
+                   ring_arena_bytes=4 << 20, ring_malloc_flags=4)
+    for off in (0, 1 << 20, 4 << 20):
+        st.set_ring_offset(off)
+        st.append(frames)
+        st.synchronize()
+        for (l, layer), (buf, flags) in sorted(exp.items()):
+            got, gflags = st.copy_layer(l, layer)
+            assert_same_pixels(got, buf, U16, f"offset {off} L{l} layer{layer}")
+            assert (gflags == flags).all(), (off, l, layer)
+    with pytest.raises(aqz.AqzError):
+        st.set_ring_offset((4 << 20) + 256)
+    st.close()
+
+
 @pytest.mark.parametrize("env", [{"AQZ_KNOBS": "8"}, {"AQZ_KNOBS": "32"},
                                  {"AQZ_KNOBS": "4", "AQZ_NT": "0",
                                   "AQZ_REGION_ROWS_LOG2": "4", "AQZ_CHUNK_PAD": "4096"}],

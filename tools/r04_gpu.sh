@@ -327,4 +327,56 @@ step_prof3() {
 bash tools/profile.sh c1 r04 || exit 1
 }
 
+# placement: rings carved from one arena, moved inside it (tools/arena_probe.py)
+step_g22() {
+O=gpurun_out/r4v
+mkdir -p $O
+timeout -k 10 400 python3 -u tools/arena_probe.py --config c2 --stages 3 > $O/arena_c2.txt 2>&1 || { tail $O/arena_c2.txt; exit 1; }
+timeout -k 10 300 python3 -u tools/arena_probe.py --config c2 --stages 2 --flags 0 >> $O/arena_c2.txt 2>&1 || { tail $O/arena_c2.txt; exit 1; }
+grep -v amdgpu.ids $O/arena_c2.txt
+}
+
+# the arena probe at GiB offsets (16 GiB of slack)
+step_g23() {
+O=gpurun_out/r4w
+mkdir -p $O
+timeout -k 10 400 python3 -u tools/arena_probe.py --config c2 --stages 2 --slack-mib 16384 --offsets-kib 0,1048576,2097152,3145728,4194304,6291456,8388608,12582912,16777216 > $O/arena_gib.txt 2>&1 || { tail $O/arena_gib.txt; exit 1; }
+timeout -k 10 300 python3 -u tools/arena_probe.py --config c2 --stages 1 --flags 0 --slack-mib 16384 --offsets-kib 0,1048576,2097152,3145728,4194304,6291456,8388608,12582912,16777216 >> $O/arena_gib.txt 2>&1 || { tail $O/arena_gib.txt; exit 1; }
+grep -v amdgpu.ids $O/arena_gib.txt
+}
+
+# which translation (UTCL2 / TLB) counters this rocprofv3 offers
+step_g24() {
+O=gpurun_out/r4x
+mkdir -p $O
+timeout -k 10 120 rocprofv3 -L > $O/counters.txt 2>&1 || { tail $O/counters.txt; exit 1; }
+grep -i -E "utc|tlb|translat|ATC|VM_|PTE|walk" $O/counters.txt | head -80
+}
+
+# slow vs fast placement: TCP->TCC request mix by memory type, and latencies
+step_g25() {
+O=gpurun_out/r4y
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 200 python3 -u tools/mtype_probe.py > $O/plain.txt 2>&1 || { tail $O/plain.txt; exit 1; }
+grep stage $O/plain.txt
+i=0
+for set in "TCP_TCC_RW_READ_REQ_sum TCP_TCC_NC_READ_REQ_sum TCP_TCC_CC_READ_REQ_sum TCP_TCC_UC_READ_REQ_sum" \
+           "TCP_TCC_RW_WRITE_REQ_sum TCP_TCC_NC_WRITE_REQ_sum TCP_TCC_CC_WRITE_REQ_sum TCP_TCC_UC_WRITE_REQ_sum" \
+           "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_WRITE_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum"; do
+i=$((i+1))
+timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $O/pmc$i -o run -- python3 tools/mtype_probe.py > $O/pmc$i.log 2>&1 || { tail $O/pmc$i.log; exit 1; }
+grep stage $O/pmc$i.log
+python3 tools/mtype_probe.py --summarise $O/pmc$i
+done
+}
+
+# ring arena: exactness at moved offsets
+step_g26() {
+O=gpurun_out/r4z
+mkdir -p $O
+timeout -k 10 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "ring_arena or environment_cannot" > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
+tail -3 $O/pytest.txt
+}
+
 "step_$1"
