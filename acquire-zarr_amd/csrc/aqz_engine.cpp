@@ -25,34 +25,64 @@ hip_check(hipError_t e, const char* what)
     }
 }
 
+// rings of at least this many bytes in all go to the 2 MiB-piece arena
+constexpr uint64_t kArenaMinRings = uint64_t(256) << 20;
+constexpr unsigned kArenaFlags = DevBuf::kVmm | (5u << 9); // 2 MiB pieces
+
 DevBuf::~DevBuf()
 {
-    if (p && !view)
-        (void)hipFree(p);
+    release();
+}
+
+void
+DevBuf::release()
+{
+    if (p && !view) {
+        if (!vmm.empty()) {
+            (void)hipMemUnmap(p, vmm_span);
+            for (auto h : vmm)
+                (void)hipMemRelease(h);
+            (void)hipMemAddressFree(p, vmm_span);
+        } else {
+            (void)hipFree(p);
+        }
+    }
+    p = nullptr;
+    n = 0;
+    view = false;
+    vmm.clear();
+    vmm_span = 0;
 }
 
 DevBuf::DevBuf(DevBuf&& o) noexcept
   : p(o.p)
   , n(o.n)
   , view(o.view)
+  , vmm(std::move(o.vmm))
+  , vmm_span(o.vmm_span)
 {
     o.p = nullptr;
     o.n = 0;
     o.view = false;
+    o.vmm.clear();
+    o.vmm_span = 0;
 }
 
 DevBuf&
 DevBuf::operator=(DevBuf&& o) noexcept
 {
     if (this != &o) {
-        if (p && !view)
-            (void)hipFree(p);
+        release();
         p = o.p;
         n = o.n;
         view = o.view;
+        vmm = std::move(o.vmm);
+        vmm_span = o.vmm_span;
         o.p = nullptr;
         o.n = 0;
         o.view = false;
+        o.vmm.clear();
+        o.vmm_span = 0;
     }
     return *this;
 }
@@ -60,8 +90,7 @@ DevBuf::operator=(DevBuf&& o) noexcept
 void
 DevBuf::set_view(uint8_t* q, size_t bytes)
 {
-    if (p && !view)
-        (void)hipFree(p);
+    release();
     p = q;
     n = bytes;
     view = true;
@@ -72,14 +101,47 @@ DevBuf::alloc(size_t bytes, unsigned flags)
 {
     if (p && !view && n >= bytes)
         return;
-    if (p && !view)
-        (void)hipFree(p);
-    p = nullptr;
-    n = 0;
-    view = false;
+    release();
     if (bytes == 0)
         return;
     void* q = nullptr;
+    if (flags & kVmm) {
+        int dev = 0;
+        hip_check(hipGetDevice(&dev), "hipGetDevice");
+        hipMemAllocationProp prop{};
+        prop.type = hipMemAllocationTypePinned;
+        prop.location.type = hipMemLocationTypeDevice;
+        prop.location.id = dev;
+        size_t gran = 0;
+        hip_check(hipMemGetAllocationGranularity(&gran, &prop,
+                                                 hipMemAllocationGranularityRecommended),
+                  "hipMemGetAllocationGranularity");
+        // bits 9-13 = v: pieces of 2^(16 + v) bytes (v <= 14: 64 KiB .. 1 GiB;
+        // at least the granularity); 31: one piece of the whole size
+        const unsigned v = (flags >> 9) & 31u;
+        const size_t piece =
+          v == 31u ? (bytes + gran - 1) / gran * gran
+                   : std::max<size_t>(gran, size_t(1) << (16 + std::min(v, 14u)));
+        const size_t span = (bytes + piece - 1) / piece * piece;
+        size_t align = gran; // a power of two: the largest <= piece, <= 1 GiB
+        while (align * 2 <= piece && align < (size_t(1) << 30))
+            align *= 2;
+        hip_check(hipMemAddressReserve(&q, span, align, nullptr, 0), "hipMemAddressReserve");
+        p = static_cast<uint8_t*>(q);
+        vmm_span = span;
+        for (size_t off = 0; off < span; off += piece) {
+            hipMemGenericAllocationHandle_t h{};
+            hip_check(hipMemCreate(&h, piece, &prop, 0), "hipMemCreate");
+            vmm.push_back(h);
+            hip_check(hipMemMap(p + off, piece, 0, h, 0), "hipMemMap");
+        }
+        hipMemAccessDesc acc{};
+        acc.location = prop.location;
+        acc.flags = hipMemAccessFlagsProtReadWrite;
+        hip_check(hipMemSetAccess(p, span, &acc, 1), "hipMemSetAccess");
+        n = bytes;
+        return;
+    }
     if (flags)
         hip_check(hipExtMallocWithFlags(&q, bytes, flags), "hipExtMallocWithFlags");
     else
@@ -275,12 +337,8 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         if (P > 0x7fffffffull)
             throw Error(9, "chunk-layer ring period too large");
         L.period = uint32_t(P);
-        if (!(k == 0 && opt_.skip_level0_split)) {
-            if (opt_.ring_arena)
-                arena_rings_ += (L.slot_bytes * L.n_slots + 0xffffull) & ~0xffffull;
-            else
-                place_level(L);
-        }
+        if (!(k == 0 && opt_.skip_level0_split))
+            arena_rings_ += (L.slot_bytes * L.n_slots + 0xffffull) & ~0xffffull;
         build_shard_order(L);
         L.tab_off.alloc(size_t(L.F) * 8);
         L.tab_grp.alloc(size_t(L.F) * 4);
@@ -292,9 +350,21 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
                   "hipMemcpy");
     }
 
-    if (opt_.ring_arena) {
-        arena_.alloc(arena_rings_ + opt_.ring_arena, opt_.ring_malloc_flags);
+    // The chunk-layer rings.  Shipped: one arena holding every level's ring
+    // back to back, mapped from 2 MiB virtual-memory pieces (hipMemCreate +
+    // hipMemMap), when the rings reach 256 MiB.  The fused kernels ran in the
+    // fast placement band on such memory in every configuration, box and
+    // process tried, and in the slow one on hipMalloc'd rings, on pieces of
+    // the rings' own sizes and on 1 GiB pieces (profiles/r04_vmm_rings.txt;
+    // DESIGN.md section 3).
+    if (opt_.ring_arena || (opt_.ring_malloc_flags == 0 && arena_rings_ >= kArenaMinRings)) {
+        arena_.alloc(arena_rings_ + opt_.ring_arena,
+                     opt_.ring_malloc_flags ? opt_.ring_malloc_flags : kArenaFlags);
         set_ring_offset(0);
+    } else {
+        for (size_t k = 0; k < lv_.size(); ++k)
+            if (!(k == 0 && opt_.skip_level0_split))
+                place_level(lv_[k]);
     }
     spacer = DevBuf{}; // freed: only the rings' placement needed it
 
@@ -473,7 +543,7 @@ Stage::place_level(StageLevel& L, uint8_t* at)
     if (at)
         L.ring.set_view(at, L.slot_bytes * L.n_slots);
     else
-        L.ring.alloc(L.slot_bytes * L.n_slots, opt_.ring_malloc_flags);
+        L.ring.alloc(L.slot_bytes * L.n_slots, opt_.ring_malloc_flags & ~kRingsPlain);
     L.flags.alloc(size_t(L.n_chunks) * L.n_slots * 4);
     hip_check(hipMemsetAsync(L.ring.p, 0, L.ring.n, stream_), "hipMemsetAsync");
     hip_check(hipMemsetAsync(L.flags.p, 0, L.flags.n, stream_), "hipMemsetAsync");
@@ -530,9 +600,13 @@ Stage::calibrate_placement()
         n = n / g3d_ * g3d_;
     // XY stages search too when the strip kernels read acquisition order
     // themselves; with the separate transpose pass they keep the first
-    if (tries <= 1 || n == 0 || !(fused_2d_ || fused_3d_) || (xy_ && !xy_direct_) || arena_.p ||
+    if (tries <= 1 || n == 0 || !(fused_2d_ || fused_3d_) || (xy_ && !xy_direct_) ||
         ring_bytes < (uint64_t(256) << 20))
         return;
+    if (arena_.p) { // the arena's placement is measured (reported), not searched
+        tries = 1;
+        mode = 3;
+    }
     const uint64_t fb0 = uint64_t(lv_[0].W) * lv_[0].H * bpp_;
     DevBuf src(size_t(n) * fb0);
     hip_check(hipMemsetAsync(src.p, 0, src.n, stream_), "hipMemsetAsync");
@@ -650,6 +724,22 @@ Stage::calibrate_placement()
     hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
+}
+
+void
+Stage::grant_access(int device)
+{
+    if (!arena_.p || arena_.vmm.empty())
+        return; // hipMalloc'd memory: peer access covers it
+    std::lock_guard<std::mutex> lk(access_mu_);
+    if (std::find(granted_.begin(), granted_.end(), device) != granted_.end())
+        return;
+    hipMemAccessDesc acc{};
+    acc.location.type = hipMemLocationTypeDevice;
+    acc.location.id = device;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    hip_check(hipMemSetAccess(arena_.p, arena_.vmm_span, &acc, 1), "hipMemSetAccess");
+    granted_.push_back(device);
 }
 
 void
@@ -1599,6 +1689,12 @@ Stage::memory_usage() const
         f.pinned += h_stage_[j].n;
     }
     f.device += xbuf_.n;
+    if (arena_.p) { // the rings are views: the arena's pieces beyond them
+        uint64_t views = 0;
+        for (const StageLevel& L : lv_)
+            views += L.ring.view ? L.ring.n : 0;
+        f.device += arena_.physical() - std::min<uint64_t>(views, arena_.physical());
+    }
     return f;
 }
 
@@ -1623,6 +1719,7 @@ Stage::estimate_memory(const ArrayDesc& desc, const StageOptions& opt_in)
     const uint64_t B = opt.max_batch_frames;
     Footprint f;
     uint64_t ring_bytes = 0, set_bytes = 0; // the placement search's unit
+    uint64_t arena_rings = 0;               // the rings 64 KiB aligned
     for (size_t k = 0; k < levels.size(); ++k) {
         ArrayDimensions ad(levels[k], desc.dtype);
         const uint64_t W = levels[k][n - 1].array_size_px;
@@ -1639,6 +1736,7 @@ Stage::estimate_memory(const ArrayDesc& desc, const StageOptions& opt_in)
             f.device += nc * slots; // has_data bytes
             ring_bytes += ring;
             set_bytes += set;
+            arena_rings += (ring + 0xffffull) & ~0xffffull;
         }
         f.device += F * 12 + nc * 4; // tab_off + tab_grp, shard order
         if (k > 0) {
@@ -1653,11 +1751,22 @@ Stage::estimate_memory(const ArrayDesc& desc, const StageOptions& opt_in)
     f.pinned += 2 * B * fb0; // pageable -> pinned staging
     if (base.needs_xy_transposition())
         f.device += B * fb0;
+    // the shipped ring arena: the rings 64 KiB aligned, rounded up to whole
+    // pieces (2 MiB; an upper bound of 1 GiB for the bench's other pieces)
+    const bool arena =
+      opt.ring_arena || (opt.ring_malloc_flags == 0 && arena_rings >= kArenaMinRings);
+    if (arena) {
+        const uint64_t G = opt.ring_malloc_flags ? uint64_t(1) << 30 : uint64_t(2) << 20;
+        f.device += (arena_rings + opt.ring_arena + G - 1) / G * G - ring_bytes;
+    }
     // the creation-time placement search's transient peak (calibrate_placement):
     // its random source batch, and one more ring set + the spacers (mode 0)
     // or every other candidate (mode 1).  An upper bound: the search may
-    // not run (small rings, generic cascade) or stop early.
-    if (opt.placement_tries > 1 && ring_bytes >= (uint64_t(256) << 20)) {
+    // not run (small rings, generic cascade) or stop early.  With the arena
+    // the placement is only measured (the source batch).
+    if (arena && opt.placement_tries > 1 && ring_bytes >= (uint64_t(256) << 20)) {
+        f.device += B * fb0;
+    } else if (opt.placement_tries > 1 && ring_bytes >= (uint64_t(256) << 20)) {
         const uint64_t extra = opt.placement_tries - 1;
         f.device += B * fb0;
         if (opt.placement_mode == 1) {
@@ -2372,6 +2481,7 @@ Stage::import_frames(Stage* src, uint32_t level, uint64_t layer, uint32_t first,
             if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
                 hip_check(e, "hipDeviceEnablePeerAccess");
             (void)hipGetLastError();
+            src->grant_access(desc_.device);
         }
     }
     if (count == 0)

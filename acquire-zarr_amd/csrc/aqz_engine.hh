@@ -18,6 +18,7 @@
 
 #include <deque>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -53,6 +54,14 @@ struct DevBuf
     uint8_t* p = nullptr;
     size_t n = 0;
     bool view = false;
+    // kVmm allocations (bench placement probes): physical pieces from
+    // hipMemCreate mapped into one reserved range of vmm_span bytes
+    std::vector<hipMemGenericAllocationHandle_t> vmm;
+    size_t vmm_span = 0;
+    static constexpr unsigned kVmm = 0x100u; // alloc flag; bits 9-13 = v:
+                                             // pieces of 2^(16 + v) bytes
+                                             // (31: the whole size)
+    size_t physical() const { return vmm.empty() ? n : vmm_span; }
     DevBuf() = default;
     explicit DevBuf(size_t bytes) { alloc(bytes); }
     ~DevBuf();
@@ -64,6 +73,7 @@ struct DevBuf
     void alloc(size_t bytes, unsigned flags = 0);
     // [q, q + bytes) of an allocation someone else owns (and frees)
     void set_view(uint8_t* q, size_t bytes);
+    void release();
 };
 
 // Owning pinned host allocation.
@@ -189,6 +199,9 @@ struct ArrayDesc
 
 // the placement search's spacers grow up to this (mode 0)
 constexpr uint64_t kMaxPlacementSpacer = uint64_t(4) << 30;
+// StageOptions::ring_malloc_flags bit: per-level ring allocations (the
+// round-3 placement) instead of the shipped arena
+constexpr uint32_t kRingsPlain = 0x10000u;
 
 struct StageOptions
 {
@@ -215,7 +228,11 @@ struct StageOptions
     uint32_t xcd_rot = 0;          // regions each XCD's walk is rotated by
     uint32_t region_rows_log2 = 0; // 0 = automatic
     uint64_t chunk_pad = 0;        // device bytes between chunks of a layer
-    uint32_t ring_malloc_flags = 0; // hipExtMallocWithFlags flags of the rings
+    // 0 (shipped): rings of >= 256 MiB in all are packed into one arena of
+    // 2 MiB virtual-memory pieces (DevBuf::kVmm), smaller ones hipMalloc'd
+    // per level; otherwise (bench A/B) per-level allocations with these
+    // hipExtMallocWithFlags / DevBuf flags (kRingsPlain alone = hipMalloc)
+    uint32_t ring_malloc_flags = 0;
     uint64_t ring_spacer = 0;       // allocated before the rings, freed after
     uint64_t ring_arena = 0;        // > 0: every ring carved from one allocation
                                     // with this much slack (set_ring_offset)
@@ -504,8 +521,13 @@ class Stage
     hipEvent_t ext_ev_ = nullptr;  // wait_stream
     PlacementReport placement_;         // creation-time placement search
     std::vector<DevBuf> held_;          // replace_rings: old rings kept allocated
-    DevBuf arena_;                      // ring_arena: every level's ring
+    DevBuf arena_;                      // every level's ring (the shipped arena)
     uint64_t arena_rings_ = 0;          // bytes of the rings inside it
+    std::mutex access_mu_;              // grant_access
+    std::vector<int> granted_;          // devices mapped into a VMM arena
+    // import_frames from another device reads this stage's rings: a
+    // virtual-memory arena must be mapped for that device too
+    void grant_access(int device);
     bool finalized_ = false;
 };
 

@@ -239,18 +239,20 @@ typedef struct
                                   first frame is first_frame + begin, with
                                   first_frame a multiple of the stack size.
                                   0, 0 = every plane. */
-    uint32_t placement_tries;  /* creation-time placement of the chunk-layer
-                                  rings: 0/1 = the first allocation; n > 1 =
-                                  time up to n placements on random frames
-                                  (10 launches each) and keep the fastest.
-                                  The fused kernels' launch time depends on
-                                  the physical memory the rings land in
-                                  (up to ~10% on 2-D
-                                  stages); only rings >= 256 MiB search.  The
-                                  transient peak (two ring sets, one batch of
-                                  random frames and spacers from 128 MiB
-                                  doubling to 4 GiB) is in
-                                  aqz_stage_estimate_memory. */
+    uint32_t placement_tries;  /* n > 1: time the chunk-layer rings'
+                                  placement on random frames at creation and
+                                  report it (aqz_stage_placement_report,
+                                  aqz_gpu_bench.h).  Rings of >= 256 MiB in
+                                  all are placed in one arena of 2 MiB
+                                  virtual-memory pieces, which is where the
+                                  fused kernels run fastest (DESIGN.md
+                                  section 3), so nothing is searched; stages
+                                  made with the bench header's per-level
+                                  ring allocations search up to n
+                                  placements.  The transient peak (one batch
+                                  of random frames; for a search, ring sets
+                                  and spacers) is in
+                                  aqz_stage_estimate_memory.  0/1 = none. */
     uint32_t reserved;
 } aqz_stage_options;
 

@@ -30,14 +30,17 @@ typedef struct
                                   (the drop-in default); n > 1 = time up to n
                                   placements of the chunk-layer rings on
                                   random frames and keep the fastest (the
-                                  launch time depends on the physical memory
-                                  the rings land in) */
+                                  launch time depends on the memory the rings
+                                  land in).  With the shipped
+                                  ring arena the placement is timed once and
+                                  reported (mode 3), not searched */
     uint32_t placement_mode;   /* 0: a losing placement is freed and a spacer
                                   allocation held until the search ends,
                                   doubling after every loser up to 4 GiB
                                   (peak: 2 ring sets + the spacers);
                                   1: every candidate is held (peak: n sets);
-                                  2: as 0 with a fixed spacer (round 3) */
+                                  2: as 0 with a fixed spacer (round 3);
+                                  reported 3: the ring arena, timed once */
     uint64_t placement_spacer_bytes; /* first spacer (0 = 128 MiB) */
     uint32_t placement_reps;   /* timed launches per candidate (0 = 10) */
     /* Kernel tuning for A/B runs.  The library reads none of these from the
@@ -56,8 +59,17 @@ typedef struct
                                   candidates, 4 predefined sequence tables
                                   only; bits 8-15 the parse history, bits
                                   16-19 parse variants */
-    uint32_t ring_malloc_flags; /* hipExtMallocWithFlags flags of the chunk-layer
-                                   rings (0 = hipMalloc) */
+    uint32_t ring_malloc_flags; /* 0 = shipped: rings of >= 256 MiB in all
+                                   are packed into one arena of 2 MiB
+                                   virtual-memory pieces (hipMemCreate +
+                                   hipMemMap), smaller ones hipMalloc'd.
+                                   Otherwise per-level rings (the round-3
+                                   placement, for A/B): hipExtMallocWithFlags
+                                   flags, 0x10000 alone = hipMalloc, 0x100 |
+                                   v << 9 = virtual memory in pieces of
+                                   2^(16 + v) bytes (v = 31: one piece of the
+                                   ring's own size).  With ring_arena_bytes
+                                   the arena takes these flags. */
     uint64_t chunk_pad_bytes;  /* device bytes added between the chunks of a
                                   resident layer (chunk_pitch) */
     uint64_t ring_spacer_bytes; /* a device allocation (ring_malloc_flags) made

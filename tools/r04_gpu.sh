@@ -379,4 +379,110 @@ timeout -k 10 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thre
 tail -3 $O/pytest.txt
 }
 
+# rings from the HIP virtual-memory API (hipMemCreate pieces mapped into one
+# range; ring_malloc_flags 0x100 | log2(piece / granularity) << 9), no search
+step_g27() {
+O=gpurun_out/r4aa
+mkdir -p $O
+: > $O/vmm.txt
+for rep in 1 2 3; do
+for fl in 0 256 2304 4352 4864; do
+timeout -k 10 200 python3 bench.py --steps 100 --warmup 5 --no-cpu-baseline --no-pyramid-only-line --no-hbm-probe --placement-tries 0 --tune ring_malloc_flags=$fl > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+tail -1 $O/tmp.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('flags', $fl, 'rep', $rep, 'ms', d['ms_per_step'], 'kernel_ms', r['kernel_avg_ms'], 'frac', r['frac'])" >> $O/vmm.txt
+done
+done
+cat $O/vmm.txt
+}
+
+# the VMM probe, bounded, large pieces first
+step_g28() {
+O=gpurun_out/r4ab
+mkdir -p $O
+for fl in 4864 4352 2304; do
+timeout -k 10 90 python3 -u tools/vmm_probe.py --flags $fl >> $O/vmm.txt 2>&1 || { tail $O/vmm.txt; exit 1; }
+done
+grep -v amdgpu.ids $O/vmm.txt
+}
+
+# VMM rings vs plain hipMalloc, first allocation of each process, 3 reps
+step_g29() {
+O=gpurun_out/r4ac
+mkdir -p $O
+for rep in 1 2 3; do
+for fl in 0 4864 4352 5376; do
+echo "rep $rep" >> $O/vmm.txt
+timeout -k 10 90 python3 -u tools/vmm_probe.py --flags $fl --launches 50 >> $O/vmm.txt 2>&1 || { tail $O/vmm.txt; exit 1; }
+done
+done
+grep -v amdgpu.ids $O/vmm.txt | paste - - - - - | awk '{print $2, $4, $NF-0, $(NF-1)}'
+}
+
+# VMM rings: one piece per ring (exact size) vs 1 GiB pieces vs hipMalloc,
+# on C2, C4, C3, C5, C1
+step_g30() {
+O=gpurun_out/r4ad
+mkdir -p $O
+for cfg in c2 c4 c3 c5 c1; do
+for rep in 1 2; do
+for fl in 0 7936 4864; do
+echo "$cfg rep $rep" >> $O/vmm.txt
+timeout -k 10 90 python3 -u tools/vmm_probe.py --config $cfg --flags $fl --launches 50 >> $O/vmm.txt 2>&1 || { tail $O/vmm.txt; exit 1; }
+done
+done
+done
+grep -v amdgpu.ids $O/vmm.txt | paste - - - - - | awk '{print $1, $3, $5, $(NF-1)}'
+}
+
+# VMM pieces with every ring packed into one arena (512 MiB / 1 GiB pieces)
+step_g31() {
+O=gpurun_out/r4ae
+mkdir -p $O
+for cfg in c2 c4 c3 c5 c1; do
+for fl in 4352 4864; do
+echo "$cfg" >> $O/vmm.txt
+timeout -k 10 90 python3 -u tools/vmm_probe.py --config $cfg --flags $fl --arena 4096 --launches 50 >> $O/vmm.txt 2>&1 || { tail $O/vmm.txt; exit 1; }
+done
+done
+grep -v amdgpu.ids $O/vmm.txt | paste - - - - - | awk '{print $1, $3, $5, $(NF-1)}'
+}
+
+# the shipped VMM arena inside bench.py (with / without the HBM probe and the
+# pyramid-only side run) against the standalone probe
+step_g32() {
+O=gpurun_out/r4af
+mkdir -p $O
+: > $O/arena_bench.txt
+for rep in 1 2; do
+for mode in plain noprobe default; do
+case $mode in
+plain) A="--no-cpu-baseline --no-pyramid-only-line --no-hbm-probe --tune ring_malloc_flags=65536";;
+noprobe) A="--no-cpu-baseline --no-pyramid-only-line --no-hbm-probe";;
+default) A="--no-cpu-baseline";;
+esac
+timeout -k 10 200 python3 bench.py --steps 100 --warmup 5 $A > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+tail -1 $O/tmp.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$mode', $rep, d['ms_per_step'], r['kernel_avg_ms'], r['placement']['candidates_ms'], r['placement']['mode'])" >> $O/arena_bench.txt
+done
+timeout -k 10 90 python3 -u tools/vmm_probe.py --flags 0 --launches 50 >> $O/arena_bench.txt 2>&1 || { tail $O/arena_bench.txt; exit 1; }
+done
+grep -v amdgpu.ids $O/arena_bench.txt
+}
+
+# VMM arena piece size sweep (pieces of 2^(16+v) bytes: v = 5 2 MiB, 6 4 MiB,
+# 7 8 MiB, 8 16 MiB, 10 64 MiB), hipMalloc per level (65536) as control
+step_g33() {
+O=gpurun_out/r4ag
+mkdir -p $O
+: > $O/pieces.txt
+for rep in 1 2; do
+for cfg in c2 c3 c4; do
+for fl in 65536 2816 3328 3840 4352 5376; do
+A="--arena 4096"; [ $fl = 65536 ] && A=""
+echo "$cfg" >> $O/pieces.txt
+timeout -k 10 90 python3 -u tools/vmm_probe.py --config $cfg --flags $fl $A --launches 50 >> $O/pieces.txt 2>&1 || { tail $O/pieces.txt; exit 1; }
+done
+done
+done
+grep -v amdgpu.ids $O/pieces.txt | paste - - - - - | awk '{print $1, $3, $7, $(NF-1)}'
+}
+
 "step_$1"
