@@ -32,10 +32,11 @@ DECIMATE = 0
 MEAN = 1
 BPP = {U8: 1, U16: 2, F32: 4}
 
-# Creation-time placement search (aqz_stage_options.placement_tries, DESIGN.md
-# section 3): up to 16 placements of the chunk-layer rings timed on random
-# frames, a losing placement freed and a 128 MiB spacer held until the search
-# ends (peak: two ring sets + the spacers, counted by aqz_stage_estimate_memory).
+# aqz_stage_options.placement_tries, as the binding passes it: the shipped
+# rings (one arena of 2 MiB virtual-memory pieces) are
+# timed once at creation and reported (roofline.placement, candidate0_ms),
+# not searched; with the bench flag ring_malloc_flags=0x10000 (per-level
+# hipMalloc, the round-3 placement) up to 16 placements are searched.
 PLACEMENT = dict(placement_tries=16)
 
 DTYPE_WORDS = {U8: "uint8", U16: "uint16", F32: "float32"}

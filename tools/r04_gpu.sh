@@ -485,4 +485,34 @@ done
 grep -v amdgpu.ids $O/pieces.txt | paste - - - - - | awk '{print $1, $3, $7, $(NF-1)}'
 }
 
+# every configuration's bench line with the shipped ring arena (one box)
+step_g34() {
+O=gpurun_out/r4ah
+mkdir -p $O
+: > $O/lines.jsonl
+for a in "--config c1" "--config c2" "--config c2-ref4" "--config c3" "--config c4" "--config c5" "--config c2 --xy" "--config c4 --xy"; do
+timeout -k 10 300 python3 bench.py $a --steps 200 --warmup 5 --no-cpu-baseline > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+tail -1 $O/tmp.json >> $O/lines.jsonl
+tail -1 $O/tmp.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$a', d['value'], d['ms_per_step'], r['kernel'], r['frac'], r.get('frac_of_probed_ceiling'), r['placement']['candidates_ms'], d.get('pyramid_only',{}).get('kernel_input_frac_of_probed_ceiling'))"
+done
+}
+
+# rocprofv3 trace + PMC of C2, C2 pyramid-only and C4 with the shipped arena
+step_prof4() {
+NO_SQ=1 bash tools/profile.sh c2 r04v || exit 1
+NO_SQ=1 bash tools/profile.sh c2 r04v pyr || exit 1
+NO_SQ=1 bash tools/profile.sh c4 r04v || exit 1
+}
+
+# successive arenas in one process (earlier ones held), 3 processes; plain too
+step_g35() {
+O=gpurun_out/r4ai
+mkdir -p $O
+for rep in 1 2 3; do
+timeout -k 10 120 python3 -u tools/arena_multi.py --stages 4 >> $O/multi.txt 2>&1 || { tail $O/multi.txt; exit 1; }
+done
+timeout -k 10 120 python3 -u tools/arena_multi.py --stages 4 --flags 65536 >> $O/multi.txt 2>&1 || { tail $O/multi.txt; exit 1; }
+grep -v amdgpu.ids $O/multi.txt
+}
+
 "step_$1"
