@@ -515,4 +515,16 @@ timeout -k 10 120 python3 -u tools/arena_multi.py --stages 4 --flags 65536 >> $O
 grep -v amdgpu.ids $O/multi.txt
 }
 
+# e2e codec rows with the ring arena (pinned frames), against round 3's
+step_g36() {
+O=gpurun_out/r4aj
+mkdir -p $O
+: > $O/e2e.jsonl
+for a in "--codec none" "--codec lz4 --compress 2" "--codec blosc-zstd --compress 1" "--codec blosc-zstd --compress 2" "--codec zstd" "--codec zstd --clevel 3"; do
+timeout -k 10 240 python3 bench.py --steps 16 --warmup 2 --e2e pinned $a > $O/tmp.log 2>&1 || { tail -20 $O/tmp.log; exit 1; }
+grep '^{' $O/tmp.log | tail -1 >> $O/e2e.jsonl
+grep '^{' $O/tmp.log | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$a', d['value'], d['ms_per_step'])"
+done
+}
+
 "step_$1"
