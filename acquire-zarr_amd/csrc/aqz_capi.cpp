@@ -504,6 +504,7 @@ apply_bench(const aqz_stage_bench_options* bench, StageOptions& o)
     o.codec.fit = (z & 4u) ? 0 : 1;
     o.codec.phist = (z >> 8) & 0xffu;
     o.codec.parse = (z >> 16) & 0xfu;
+    o.codec.vmm = (z >> 20) & 1u;
 }
 
 static void

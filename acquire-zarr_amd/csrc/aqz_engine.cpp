@@ -29,6 +29,16 @@ hip_check(hipError_t e, const char* what)
 constexpr uint64_t kArenaMinRings = uint64_t(256) << 20;
 constexpr unsigned kArenaFlags = DevBuf::kVmm | (5u << 9); // 2 MiB pieces
 
+// A large work buffer: from 2 MiB virtual-memory pieces when `vmm` and at
+// least 64 MiB (CodecTuning::vmm), else hipMalloc.
+static void
+alloc_large(DevBuf& b, size_t bytes, bool vmm)
+{
+    if (b.p && !b.view && b.n >= bytes)
+        return;
+    b.alloc(bytes, vmm && bytes >= (size_t(64) << 20) ? kArenaFlags : 0u);
+}
+
 DevBuf::~DevBuf()
 {
     release();
@@ -1052,7 +1062,7 @@ Stage::append(const void* frames, uint64_t n_frames, int mem)
             const int j = stage_idx_;
             stage_idx_ ^= 1;
             const size_t nbytes = size_t(b) * fbytes;
-            d_stage_[j].alloc(size_t(B) * fbytes);
+            alloc_large(d_stage_[j], size_t(B) * fbytes, opt_.codec.vmm);
             const uint8_t* hsrc = p;
             if (mem != kMemHostPinned) {
                 h_stage_[j].alloc(size_t(B) * fbytes);
@@ -2017,7 +2027,7 @@ Compressor::run(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
         return;
     }
     const uint64_t ns = uint64_t(n_chunks) * g_.spc;
-    scratch_.alloc(store_only_ ? 1 : ns * g_.slot);
+    alloc_large(scratch_, store_only_ ? 1 : ns * g_.slot, tune_.vmm);
     ssize_.alloc(ns * 4);
     spos_.alloc(ns * 4);
     fsize_.alloc(size_t(n_chunks) * 4);
@@ -2090,7 +2100,7 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
     const bool shuffle = blosc && !store_only_ &&
                          (c_.shuffle == 2 || (c_.shuffle == 1 && typesize_ > 1));
     if (shuffle) {
-        zin_.alloc(size_t(n_chunks) * nbytes_);
+        alloc_large(zin_, size_t(n_chunks) * nbytes_, tune_.vmm);
         ShuffleParams sp{ chunks, pitch, n_chunks, flags, tag, p.nbytes, typesize_,
                           uint32_t(c_.shuffle), p.seg_bytes, p.nseg, zin_.p };
         hip_check(launch_shuffle_blocks(sp, stream), "shuffle launch");
@@ -2121,14 +2131,14 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
                    (p.src_pitch & 3u) == 0 && (p.seg_bytes & 3u) == 0;
         far = far && tune_.far != 0;
         if (far) {
-            far_.alloc(nseg * p.seg_bytes * 4);
+            alloc_large(far_, nseg * p.seg_bytes * 4, tune_.vmm);
             p.far = reinterpret_cast<uint32_t*>(far_.p);
             p.phist = 0; // the far candidates cover every earlier unit
         }
         if (p.match) {
             const uint64_t nu = nblk * kZSubBlocks;
-            lits_.alloc(nu * kZSub);
-            seqs_.alloc(nu * kZSubSeq * 8);
+            alloc_large(lits_, nu * kZSub, tune_.vmm);
+            alloc_large(seqs_, nu * kZSubSeq * 8, tune_.vmm);
             snseq_.alloc(nu * 4);
             snlit_.alloc(nu * 4);
             stail_.alloc(nu * 4);
@@ -2146,7 +2156,7 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
         bkind_.alloc(nblk);
         bpay_.alloc(nblk * 4);
         bpos_.alloc(nblk * 4);
-        scratch_.alloc(nblk * zstd::kBlock);
+        alloc_large(scratch_, nblk * zstd::kBlock, tune_.vmm);
         tab_.alloc(ngrp * sizeof(ZstdSegTable));
         carrier_.alloc(ngrp * 4);
         sraw_.alloc(nseg);
@@ -2357,7 +2367,7 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
     const uint64_t cap = Compressor::max_bytes(L.bpc, L.n_chunks);
     if (L.cframes[slot].n < cap)
         hip_check(hipStreamSynchronize(cs), "hipStreamSynchronize"); // realloc below
-    L.cframes[slot].alloc(cap);
+    alloc_large(L.cframes[slot], cap, opt_.codec.vmm);
     L.coffsets[slot].alloc((size_t(L.n_chunks) + 1) * 8);
     L.h_coffsets[slot].alloc((size_t(L.n_chunks) + 1) * 8);
     // after every kernel enqueued so far; the slot's next layer waits for it.

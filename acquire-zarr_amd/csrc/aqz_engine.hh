@@ -114,6 +114,9 @@ struct CodecTuning
     uint32_t fit = 1;      // 0: predefined sequence tables only
     uint32_t phist = 0;    // parse history (KiB before a unit; 0 none)
     uint32_t parse = 0;    // parse variants for timing (bits 1/2/4/8)
+    uint32_t vmm = 0;      // 1: buffers >= 64 MiB (codec work buffers, layer
+                           // frames, H2D staging) from 2 MiB virtual-memory
+                           // pieces, as the rings (A/B)
 };
 
 // Device frames of arrays of equally sized device chunks (aqz_codec.hip):

@@ -259,7 +259,7 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
     dt, bpp = cfg["dtype"], BPP[cfg["dtype"]]
     B = args.batch or min(cfg["batch"], 128)
     st = aqz.Stage(cfg["dims"], dt, cfg["method"], force_levels=cfg["force_levels"],
-                   max_batch_frames=B, layer_slots=2, device=dev.index)
+                   max_batch_frames=B, layer_slots=2, device=dev.index, **args.tune)
     L = st.n_levels()
     sizes = level_sizes(st)
     fbytes = sizes[0][0] * sizes[0][1] * bpp
@@ -393,7 +393,7 @@ def run_paced(torch, aqz, dev, cfg, args):
     dt, bpp = cfg["dtype"], BPP[cfg["dtype"]]
     b = args.batch or 8
     st = aqz.Stage(cfg["dims"], dt, cfg["method"], force_levels=cfg["force_levels"],
-                   max_batch_frames=b, layer_slots=3, device=dev.index)
+                   max_batch_frames=b, layer_slots=3, device=dev.index, **args.tune)
     stream = torch.cuda.Stream(dev)
     st.set_stream(stream.cuda_stream)
     L = st.n_levels()

@@ -58,7 +58,10 @@ typedef struct
                                   model's byte-exact mode), 2 no far
                                   candidates, 4 predefined sequence tables
                                   only; bits 8-15 the parse history, bits
-                                  16-19 parse variants */
+                                  16-19 parse variants; bit 20: codec work
+                                  buffers, layer frames and H2D staging of
+                                  >= 64 MiB from 2 MiB virtual-memory
+                                  pieces, as the rings */
     uint32_t ring_malloc_flags; /* 0 = shipped: rings of >= 256 MiB in all
                                    are packed into one arena of 2 MiB
                                    virtual-memory pieces (hipMemCreate +

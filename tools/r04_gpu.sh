@@ -527,4 +527,19 @@ grep '^{' $O/tmp.log | tail -1 | python3 -c "import json,sys; d=json.loads(sys.s
 done
 }
 
+# e2e codec rows: codec / staging buffers from hipMalloc vs 2 MiB pieces
+# (zstd_flags bit 20), alternating
+step_g37() {
+O=gpurun_out/r4ak
+mkdir -p $O
+: > $O/e2e_vmm.txt
+for a in "--codec zstd --clevel 3" "--codec blosc-zstd --compress 2" "--codec lz4 --compress 2"; do
+for v in 0 1048576 0 1048576; do
+timeout -k 10 240 python3 bench.py --steps 16 --warmup 2 --e2e pinned $a --tune zstd_flags=$v > $O/tmp.log 2>&1 || { tail -20 $O/tmp.log; exit 1; }
+grep '^{' $O/tmp.log | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$a', 'zstd_flags=$v', d['value'], d['ms_per_step'])" >> $O/e2e_vmm.txt
+done
+done
+cat $O/e2e_vmm.txt
+}
+
 "step_$1"
