@@ -179,3 +179,20 @@ def test_memory_estimate_counts_the_rings():
     assert m["pinned_bytes"] >= staging
     big = aqz.estimate_memory(c2, ob.U16, ob.MEAN, max_batch_frames=128, layer_slots=4)
     assert big["device_bytes"] > m["device_bytes"]
+
+
+def test_memory_estimate_counts_the_ring_arena():
+    """Rings of >= 256 MiB in all are packed (64 KiB aligned) into one arena
+    of 2 MiB virtual-memory pieces: the estimate adds that rounding, which
+    the per-level allocations (bench ring_malloc_flags 0x10000) do not have;
+    smaller rings stay per level either way."""
+    plain = dict(ring_malloc_flags=0x10000)
+    # ragged 100-px chunks: ring sizes are not multiples of 64 KiB
+    big = [(ob.TIME, 0, 64, 1), (ob.SPACE, 2000, 100, 1), (ob.SPACE, 2000, 100, 1)]
+    a = aqz.estimate_memory(big, ob.U16, ob.MEAN, max_batch_frames=64, layer_slots=3)
+    b = aqz.estimate_memory(big, ob.U16, ob.MEAN, max_batch_frames=64, layer_slots=3, **plain)
+    n_levels = len(aqz.pyramid_levels(big))
+    assert 0 < a["device_bytes"] - b["device_bytes"] < (2 << 20) + n_levels * (64 << 10)
+    small = [(ob.TIME, 0, 4, 1), (ob.SPACE, 512, 128, 1), (ob.SPACE, 512, 128, 1)]
+    assert (aqz.estimate_memory(small, ob.U16, ob.MEAN) ==
+            aqz.estimate_memory(small, ob.U16, ob.MEAN, **plain))
