@@ -618,7 +618,10 @@ Stage::calibrate_placement()
         mode = 3;
     }
     const uint64_t fb0 = uint64_t(lv_[0].W) * lv_[0].H * bpp_;
-    DevBuf src(size_t(n) * fb0);
+    // the random source in the same kind of memory as the rings, so the
+    // timing is the rings' placement and not the scratch source's
+    DevBuf src;
+    alloc_large(src, size_t(n) * fb0, arena_.p != nullptr);
     hip_check(hipMemsetAsync(src.p, 0, src.n, stream_), "hipMemsetAsync");
     hip_check(launch_fill_random(src.p, src.n, 0x5eedull, stream_), "fill launch");
     uint64_t live = memory_usage().device + src.n;
@@ -1775,7 +1778,7 @@ Stage::estimate_memory(const ArrayDesc& desc, const StageOptions& opt_in)
     // not run (small rings, generic cascade) or stop early.  With the arena
     // the placement is only measured (the source batch).
     if (arena && opt.placement_tries > 1 && ring_bytes >= (uint64_t(256) << 20)) {
-        f.device += B * fb0;
+        f.device += B * fb0 + (uint64_t(2) << 20); // in 2 MiB pieces
     } else if (opt.placement_tries > 1 && ring_bytes >= (uint64_t(256) << 20)) {
         const uint64_t extra = opt.placement_tries - 1;
         f.device += B * fb0;
