@@ -286,6 +286,7 @@ def _check(status: int, what: str) -> None:
 
 PROBE_READ, PROBE_COPY, PROBE_COPY_THIRD, PROBE_READ_THIRD = 0, 1, 2, 3
 PROBE_PLAIN_STORES = 0x100
+PROBE_PIECES = 0x200
 
 
 def probe_hbm(shape: int, nbytes: int = 512 << 20, reps: int = 20, device: int = 0):

@@ -2,6 +2,7 @@
 // shapes (include/aqz_gpu_bench.h aqz_probe_hbm).  Measurement only: the
 // bench reports the stage's rates next to these ceilings, measured in the
 // same process on the same device.
+#include "aqz_engine.hh"
 #include "aqz_gpu_bench.h"
 
 #include <hip/hip_runtime.h>
@@ -61,12 +62,28 @@ probe_stream(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
 struct DevMem
 {
     void* p = nullptr;
+    aqz::DevBuf pieces; // AQZ_PROBE_PIECES
     ~DevMem()
     {
-        if (p)
+        if (p && !pieces.p)
             (void)hipFree(p);
     }
 };
+
+// hipMalloc, or (pieces) 2 MiB virtual-memory pieces as the stage's rings
+hipError_t
+probe_alloc(DevMem& m, size_t bytes, bool pieces)
+{
+    if (!pieces)
+        return hipMalloc(&m.p, bytes);
+    try {
+        m.pieces.alloc(bytes, aqz::DevBuf::kVmm | (5u << 9));
+    } catch (...) {
+        return hipErrorOutOfMemory;
+    }
+    m.p = m.pieces.p;
+    return hipSuccess;
+}
 
 } // namespace
 
@@ -76,8 +93,9 @@ aqz_probe_hbm(int32_t device, int32_t shape, uint64_t bytes, uint32_t reps, doub
 {
     const int32_t kind = shape & 0xff;
     const bool plain = (shape & AQZ_PROBE_PLAIN_STORES) != 0;
+    const bool pieces = (shape & AQZ_PROBE_PIECES) != 0;
     if (!ms || kind < AQZ_PROBE_READ || kind > AQZ_PROBE_READ_THIRD || reps == 0 ||
-        (shape & ~(0xff | AQZ_PROBE_PLAIN_STORES)) != 0)
+        (shape & ~(0xff | AQZ_PROBE_PLAIN_STORES | AQZ_PROBE_PIECES)) != 0)
         return AQZ_STATUS_INVALID_ARGUMENT;
     const uint64_t per_wg = uint64_t(kU) * 256 * 16;
     const uint64_t grid = bytes / per_wg;
@@ -99,8 +117,8 @@ aqz_probe_hbm(int32_t device, int32_t shape, uint64_t bytes, uint32_t reps, doub
                                               : AQZ_STATUS_INTERNAL_ERROR;
             return e == hipSuccess;
         };
-        if (ok(hipMalloc(&src.p, rd * kRing)) && ok(hipMalloc(&dst.p, rd)) &&
-            ok(hipMalloc(&dst3.p, rd / 3 + per_wg)) && ok(hipMalloc(&sink.p, 64)) &&
+        if (ok(probe_alloc(src, rd * kRing, pieces)) && ok(probe_alloc(dst, rd, pieces)) &&
+            ok(probe_alloc(dst3, rd / 3 + per_wg, pieces)) && ok(hipMalloc(&sink.p, 64)) &&
             ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) &&
             ok(hipEventCreate(&a)) && ok(hipEventCreate(&b)) &&
             ok(hipMemsetAsync(src.p, 1, rd * kRing, s))) {

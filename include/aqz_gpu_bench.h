@@ -175,7 +175,9 @@ enum
     AQZ_PROBE_COPY = 1,
     AQZ_PROBE_COPY_THIRD = 2,
     AQZ_PROBE_READ_THIRD = 3,
-    AQZ_PROBE_PLAIN_STORES = 0x100
+    AQZ_PROBE_PLAIN_STORES = 0x100,
+    AQZ_PROBE_PIECES = 0x200 /* buffers from 2 MiB virtual-memory pieces, as
+                                the stage's chunk-layer rings */
 };
 aqz_status aqz_probe_hbm(int32_t device, int32_t shape, uint64_t bytes, uint32_t reps,
                          double* ms, uint64_t* read_bytes);

@@ -542,4 +542,30 @@ done
 cat $O/e2e_vmm.txt
 }
 
+# the live HBM probe with hipMalloc'd vs 2 MiB-piece buffers, alternating
+step_g38() {
+O=gpurun_out/r4al
+mkdir -p $O
+timeout -k 10 200 python3 -u - > $O/probe_pieces.txt 2>&1 <<'PY' || { tail $O/probe_pieces.txt; exit 1; }
+import sys
+sys.path.insert(0, "acquire-zarr_amd")
+import aqz
+names = {aqz.PROBE_READ: "read", aqz.PROBE_COPY: "copy", aqz.PROBE_COPY_THIRD: "copy+1/3",
+         aqz.PROBE_READ_THIRD: "read+1/3"}
+wr = {aqz.PROBE_READ: 0.0, aqz.PROBE_COPY: 1.0, aqz.PROBE_COPY_THIRD: 4 / 3,
+      aqz.PROBE_READ_THIRD: 1 / 3}
+for rnd in range(3):
+    for shape in names:
+        row = []
+        for pc in (0, aqz.PROBE_PIECES):
+            best = 0.0
+            for st in (0, aqz.PROBE_PLAIN_STORES) if shape != aqz.PROBE_READ else (0,):
+                ms, rd = aqz.probe_hbm(shape | st | pc, 512 << 20, 20, 0)
+                best = max(best, rd * (1 + wr[shape]) / (ms * 1e-3) / 1e9)
+            row.append(round(best, 1))
+        print(rnd, names[shape], "hipMalloc", row[0], "pieces", row[1], "GB/s", flush=True)
+PY
+cat $O/probe_pieces.txt
+}
+
 "step_$1"
