@@ -239,10 +239,10 @@ class GpuMultiscaleArray final
             aqz_stage_options opt{};
             opt.max_batch_frames = batch_frames;
             opt.layer_slots = 2;
-            // the fused kernels' rate depends on where the chunk-layer rings
-            // land; the search's transient peak is in
-            // aqz_stage_estimate_memory
-            opt.placement_tries = 16;
+            // no placement timing: the library maps the chunk-layer rings
+            // from 2 MiB virtual-memory pieces, where the fused kernels run
+            // in the fast band without a search
+            opt.placement_tries = 0;
             if (devices.size() > 1) {
                 opt.z_slab_begin = plan.begin[r];
                 opt.z_slab_end = plan.end[r];
