@@ -568,4 +568,12 @@ PY
 cat $O/probe_pieces.txt
 }
 
+# the drop-in binding end to end with the ring arena (handoff_replay)
+step_g39() {
+O=gpurun_out/r4am
+mkdir -p $O
+timeout -k 10 400 python3 -u tools/binding_e2e.py --frames 2048 > $O/binding_e2e.jsonl 2> $O/binding_e2e.err || { tail $O/binding_e2e.err; exit 1; }
+cat $O/binding_e2e.jsonl
+}
+
 "step_$1"
