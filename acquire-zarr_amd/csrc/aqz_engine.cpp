@@ -367,15 +367,26 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
     // process tried, and in the slow one on hipMalloc'd rings, on pieces of
     // the rings' own sizes and on 1 GiB pieces (profiles/r04_vmm_rings.txt;
     // DESIGN.md section 3).
+    bool per_level = true;
     if (opt_.ring_arena || (opt_.ring_malloc_flags == 0 && arena_rings_ >= kArenaMinRings)) {
-        arena_.alloc(arena_rings_ + opt_.ring_arena,
-                     opt_.ring_malloc_flags ? opt_.ring_malloc_flags : kArenaFlags);
-        set_ring_offset(0);
-    } else {
+        try {
+            arena_.alloc(arena_rings_ + opt_.ring_arena,
+                         opt_.ring_malloc_flags ? opt_.ring_malloc_flags : kArenaFlags);
+            set_ring_offset(0);
+            per_level = false;
+        } catch (const Error& e) {
+            // out of memory is the caller's to see; a runtime without the
+            // virtual-memory API gets the per-level rings (slower placement)
+            if (e.status == 6 || opt_.ring_arena)
+                throw;
+            arena_ = DevBuf{};
+            arena_fallback_ = true;
+        }
+    }
+    if (per_level)
         for (size_t k = 0; k < lv_.size(); ++k)
             if (!(k == 0 && opt_.skip_level0_split))
                 place_level(lv_[k]);
-    }
     spacer = DevBuf{}; // freed: only the rings' placement needed it
 
     // 2-D fast path: z never shrinks and XY shrinks at every level, so every

@@ -526,6 +526,7 @@ class Stage
     std::vector<DevBuf> held_;          // replace_rings: old rings kept allocated
     DevBuf arena_;                      // every level's ring (the shipped arena)
     uint64_t arena_rings_ = 0;          // bytes of the rings inside it
+    bool arena_fallback_ = false;       // the VMM arena failed: per-level rings
     std::mutex access_mu_;              // grant_access
     std::vector<int> granted_;          // devices mapped into a VMM arena
     // import_frames from another device reads this stage's rings: a
