@@ -576,4 +576,16 @@ timeout -k 10 400 python3 -u tools/binding_e2e.py --frames 2048 > $O/binding_e2e
 cat $O/binding_e2e.jsonl
 }
 
+# kernel A/Bs on the ring arena: C4 pair vs one plane (XY and not), C3 and
+# C2 occupancy caps (knob bits 13-15 = workgroups per CU)
+step_g40() {
+O=gpurun_out/r4an
+mkdir -p $O
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c4 --xy --knobs 0,2,0,2 --instances 2 > $O/ab.txt 2>&1 || { tail $O/ab.txt; exit 1; }
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c4 --knobs 0,2,0,2 --instances 2 >> $O/ab.txt 2>&1 || { tail $O/ab.txt; exit 1; }
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c3 --knobs 0,40960,49152,57344 --instances 2 >> $O/ab.txt 2>&1 || { tail $O/ab.txt; exit 1; }
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c2 --knobs 0,40960,49152,57344 --instances 2 >> $O/ab.txt 2>&1 || { tail $O/ab.txt; exit 1; }
+grep -v amdgpu.ids $O/ab.txt
+}
+
 "step_$1"
