@@ -743,6 +743,12 @@ def main():
     }
     pl = result["roofline"]["placement"]
     pl["placement_tries"] = args.placement_tries
+    # how the chunk-layer rings were allocated (aqz_placement_report.mode)
+    pl["ring_allocation"] = (
+        "one arena of 2 MiB virtual-memory pieces, timed once (no search)"
+        if pl.get("mode") == 3 else
+        "per-level allocations, placement search" if pl.get("candidates_ms") else
+        "per-level allocations (rings under 256 MiB), no search")
     if pl.get("kept_ms_final"):
         # the steady state against the kept placement's own re-time
         pl["steady_over_kept_final"] = round(avg_ms / pl["kept_ms_final"], 4)
