@@ -745,7 +745,10 @@ def main():
     pl["placement_tries"] = args.placement_tries
     # how the chunk-layer rings were allocated (aqz_placement_report.mode)
     pl["ring_allocation"] = (
-        "one arena of 2 MiB virtual-memory pieces, timed once (no search)"
+        ("one arena of 2 MiB virtual-memory pieces (candidate 0), kept"
+         if pl.get("kept") == 0 else
+         "one arena of 2 MiB virtual-memory pieces (candidate 0) slower than a "
+         "per-level candidate, which was kept")
         if pl.get("mode") == 3 else
         "per-level allocations, placement search" if pl.get("candidates_ms") else
         "per-level allocations (rings under 256 MiB), no search")

@@ -240,18 +240,18 @@ typedef struct
                                   first_frame a multiple of the stack size.
                                   0, 0 = every plane. */
     uint32_t placement_tries;  /* n > 1: time the chunk-layer rings'
-                                  placement on random frames at creation and
-                                  report it (aqz_stage_placement_report,
+                                  placement on random frames at creation
+                                  (aqz_stage_placement_report,
                                   aqz_gpu_bench.h).  Rings of >= 256 MiB in
                                   all are placed in one arena of 2 MiB
-                                  virtual-memory pieces, which is where the
-                                  fused kernels run fastest (DESIGN.md
-                                  section 3), so nothing is searched; stages
-                                  made with the bench header's per-level
-                                  ring allocations search up to n
-                                  placements.  The transient peak (one batch
-                                  of random frames; for a search, ring sets
-                                  and spacers) is in
+                                  virtual-memory pieces, where the fused
+                                  kernels run in the fast band on nearly
+                                  every box; it is
+                                  candidate 0, and up to n - 1 per-level
+                                  placements follow only while no candidate
+                                  is 8% faster than the slowest seen.  The
+                                  transient peak (a batch of random frames,
+                                  ring sets and spacers) is in
                                   aqz_stage_estimate_memory.  0/1 = none. */
     uint32_t reserved;
 } aqz_stage_options;

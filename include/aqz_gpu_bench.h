@@ -32,15 +32,18 @@ typedef struct
                                   random frames and keep the fastest (the
                                   launch time depends on the memory the rings
                                   land in).  With the shipped
-                                  ring arena the placement is timed once and
-                                  reported (mode 3), not searched */
+                                  ring arena, candidate 0 is the arena
+                                  (reported mode 3) and per-level candidates
+                                  follow only while none is 8% faster than
+                                  the slowest seen */
     uint32_t placement_mode;   /* 0: a losing placement is freed and a spacer
                                   allocation held until the search ends,
                                   doubling after every loser up to 4 GiB
                                   (peak: 2 ring sets + the spacers);
                                   1: every candidate is held (peak: n sets);
                                   2: as 0 with a fixed spacer (round 3);
-                                  reported 3: the ring arena, timed once */
+                                  reported 3: candidate 0 was the ring
+                                  arena */
     uint64_t placement_spacer_bytes; /* first spacer (0 = 128 MiB) */
     uint32_t placement_reps;   /* timed launches per candidate (0 = 10) */
     /* Kernel tuning for A/B runs.  The library reads none of these from the

@@ -239,10 +239,12 @@ class GpuMultiscaleArray final
             aqz_stage_options opt{};
             opt.max_batch_frames = batch_frames;
             opt.layer_slots = 2;
-            // no placement timing: the library maps the chunk-layer rings
-            // from 2 MiB virtual-memory pieces, where the fused kernels run
-            // in the fast band without a search
-            opt.placement_tries = 0;
+            // the library maps the chunk-layer rings from 2 MiB virtual-
+            // memory pieces, where the fused kernels run in the fast band on
+            // nearly every box; with tries, a box where that placement is
+            // slow falls back to searching per-level allocations (DESIGN.md
+            // section 3; the transient peak is in aqz_stage_estimate_memory)
+            opt.placement_tries = 16;
             if (devices.size() > 1) {
                 opt.z_slab_begin = plan.begin[r];
                 opt.z_slab_end = plan.end[r];
