@@ -588,4 +588,16 @@ timeout -k 10 300 python3 -u tools/knob_ab.py --config c2 --knobs 0,40960,49152,
 grep -v amdgpu.ids $O/ab.txt
 }
 
+# the default bench three times (hybrid placement), then C3 and C4
+step_g41() {
+O=gpurun_out/r4ao
+mkdir -p $O
+: > $O/lines.jsonl
+for a in "--config c2" "--config c2" "--config c2" "--config c3" "--config c4"; do
+timeout -k 10 300 python3 bench.py $a --no-cpu-baseline > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+tail -1 $O/tmp.json >> $O/lines.jsonl
+tail -1 $O/tmp.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; p=r['placement']; print('$a', d['value'], d['ms_per_step'], r['frac'], r.get('frac_of_probed_ceiling'), p['candidates_ms'], p['kept'], round(p['peak_device_bytes']/1e9,1))"
+done
+}
+
 "step_$1"
