@@ -69,9 +69,9 @@ class StageOptionsC(C.Structure):
 class StageBenchOptionsC(C.Structure):
     """aqz_stage_bench_options (include/aqz_gpu_bench.h): not drop-in ABI."""
     _fields_ = [("force_levels", C.c_uint32), ("skip_level0_split", C.c_int32),
-                ("placement_tries", C.c_uint32), ("placement_mode", C.c_uint32),
-                ("placement_spacer_bytes", C.c_uint64),
-                ("placement_reps", C.c_uint32), ("knobs", C.c_uint32),
+                ("placement_tries", C.c_uint32),
+                ("placement_reps", C.c_uint32), ("placement_flags", C.c_uint32),
+                ("knobs", C.c_uint32),
                 ("nt_policy", C.c_uint32), ("xcd_rot", C.c_uint32),
                 ("region_rows_log2", C.c_uint32), ("zstd_flags", C.c_uint32),
                 ("ring_malloc_flags", C.c_uint32), ("chunk_pad_bytes", C.c_uint64),
@@ -105,7 +105,10 @@ class PlacementReportC(C.Structure):
     """aqz_placement_report (include/aqz_gpu_bench.h)."""
     _fields_ = [("n", C.c_uint32), ("kept", C.c_uint32), ("reps", C.c_uint32),
                 ("mode", C.c_uint32), ("ms", C.c_double * 32),
-                ("kept_ms_final", C.c_double), ("peak_device_bytes", C.c_uint64)]
+                ("kept_ms_final", C.c_double), ("peak_device_bytes", C.c_uint64),
+                ("probe_bus_gbs", C.c_double), ("expected_ms", C.c_double),
+                ("alg_bytes", C.c_uint64), ("accepted", C.c_uint32),
+                ("reserved", C.c_uint32), ("probe_gbs", C.c_double * 32)]
 
 
 class MemoryUsageC(C.Structure):
@@ -192,6 +195,9 @@ def lib():
         "aqz_dims_frames_per_chunk_layer": ([vp], u64),
         "aqz_dims_shard_index_for_chunk": ([vp, u32], u32),
         "aqz_dims_shard_internal_index": ([vp, u32], u32),
+        "aqz_dims_shard_geometry": ([vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)], i32),
+        "aqz_dims_skipped_internal_indices": ([vp, u32, u32, C.POINTER(u32), sz,
+                                               C.POINTER(sz)], i32),
         "aqz_pyramid_levels": ([D, sz, u32, C.POINTER(u32), D, sz], i32),
         "aqz_dims_dim1_banding": ([vp, C.POINTER(i32), C.POINTER(u32), C.POINTER(u64),
                                    C.POINTER(u32)], i32),
@@ -287,6 +293,7 @@ def _check(status: int, what: str) -> None:
 PROBE_READ, PROBE_COPY, PROBE_COPY_THIRD, PROBE_READ_THIRD = 0, 1, 2, 3
 PROBE_PLAIN_STORES = 0x100
 PROBE_PIECES = 0x200
+PROBE_DEEP = 0x400
 
 
 def probe_hbm(shape: int, nbytes: int = 512 << 20, reps: int = 20, device: int = 0):
@@ -373,6 +380,23 @@ class Dims:
     def shard_internal_index(self, c):
         return lib().aqz_dims_shard_internal_index(self.h, c)
 
+    def shard_geometry(self):
+        """(chunks_per_shard, number_of_shards, chunk_layers_per_shard)"""
+        a, b, c = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        _check(lib().aqz_dims_shard_geometry(self.h, C.byref(a), C.byref(b), C.byref(c)),
+               "aqz_dims_shard_geometry")
+        return a.value, b.value, c.value
+
+    def skipped_internal_indices(self, shard, layer):
+        """ArrayDimensions::skipped_internal_indices_for_shard_layer"""
+        n = C.c_size_t(0)
+        _check(lib().aqz_dims_skipped_internal_indices(self.h, shard, layer, None, 0,
+                                                       C.byref(n)), "skipped_internal")
+        out = (C.c_uint32 * max(1, n.value))()
+        _check(lib().aqz_dims_skipped_internal_indices(self.h, shard, layer, out, n.value,
+                                                       C.byref(n)), "skipped_internal")
+        return list(out[:n.value])
+
     def dim1_banding(self):
         """(supported, n_bands, frames_per_band, chunks_per_band)"""
         a, b, c, d = C.c_int32(), C.c_uint32(), C.c_uint64(), C.c_uint32()
@@ -402,7 +426,7 @@ def estimate_memory(dims, dtype, method, max_levels=0, layer_slots=0,
     """aqz_stage_estimate_memory: upper bound of a stage's footprint (no GPU),
     including the placement search's creation peak when placement_tries > 1.
     With bench-header options (force_levels, skip_level0_split,
-    placement_mode, ...), aqz_stage_estimate_memory_bench."""
+    placement_reps, ...), aqz_stage_estimate_memory_bench."""
     d, keep = _desc(dims, dtype, method, max_levels, True, storage_order, 0)
     o = StageOptionsC(layer_slots, max_batch_frames, 0, 0, 0, placement_tries)
     m = MemoryUsageC()
@@ -544,7 +568,7 @@ class Stage:
 
     Keyword arguments beyond the drop-in options of include/aqz_gpu.h
     (force_levels, skip_level0_split, knobs, nt, chunk_pad_bytes,
-    zstd_flags, placement_mode, ...) are the bench-only fields of
+    zstd_flags, placement_reps, ...) are the bench-only fields of
     include/aqz_gpu_bench.h (aqz_stage_create_bench)."""
 
     def __init__(self, dims, dtype, method, max_levels=0, multiscale=True,
@@ -747,13 +771,19 @@ class Stage:
     def placement(self):
         """Creation-time placement search (bench option placement_tries):
         {"candidates_ms": [...], "kept": i, "kept_ms_final", "reps", "mode",
-        "peak_device_bytes"} (empty candidate list when none ran)."""
+        "peak_device_bytes", "probe_bus_gbs", "expected_ms", "alg_bytes",
+        "accepted"} (empty candidate list when none ran)."""
         r = PlacementReportC()
         _check(lib().aqz_stage_placement_report(self.h, C.byref(r)), "placement_report")
         return {"candidates_ms": [round(r.ms[i], 5) for i in range(min(32, r.n))],
                 "kept": r.kept, "kept_ms_final": round(r.kept_ms_final, 5),
                 "reps": r.reps, "mode": r.mode,
-                "peak_device_bytes": r.peak_device_bytes}
+                "peak_device_bytes": r.peak_device_bytes,
+                "probe_bus_gbs": round(r.probe_bus_gbs, 1),
+                "expected_ms": round(r.expected_ms, 5), "alg_bytes": r.alg_bytes,
+                "accepted": bool(r.accepted),
+                "candidates_probe_gbs": [round(r.probe_gbs[i], 1)
+                                         for i in range(min(32, r.n))]}
 
     # ---- device compression of resident layers ----------------------------
     def compress_layer(self, level, layer, codec=CODEC_BLOSC_LZ4, clevel=5, shuffle=1):

@@ -325,6 +325,41 @@ aqz_dims_shard_internal_index(const aqz_dims* d, uint32_t c)
 }
 
 aqz_status
+aqz_dims_shard_geometry(const aqz_dims* d, uint32_t* chunks_per_shard, uint32_t* n_shards,
+                        uint32_t* layers_per_shard)
+{
+    if (!d)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard([&] {
+        const ArrayDimensions& a = *d->ad;
+        if (chunks_per_shard)
+            *chunks_per_shard = a.chunks_per_shard();
+        if (n_shards)
+            *n_shards = a.number_of_shards();
+        if (layers_per_shard)
+            *layers_per_shard = a.chunk_layers_per_shard();
+    });
+}
+
+aqz_status
+aqz_dims_skipped_internal_indices(const aqz_dims* d, uint32_t shard, uint32_t layer,
+                                  uint32_t* out, size_t cap, size_t* n)
+{
+    if (!d || !n || (cap && !out))
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard([&] {
+        const ArrayDimensions& a = *d->ad;
+        if (shard >= a.number_of_shards() ||
+            layer >= std::max<uint32_t>(1, a.chunk_layers_per_shard()))
+            throw Error(AQZ_STATUS_INVALID_ARGUMENT, "shard or layer out of range");
+        const auto v = a.skipped_internal_indices_for_shard_layer(shard, layer);
+        *n = v.size();
+        for (size_t i = 0; i < v.size() && i < cap; ++i)
+            out[i] = v[i];
+    });
+}
+
+aqz_status
 aqz_dims_dim1_banding(const aqz_dims* d, int32_t* supported, uint32_t* n_bands,
                       uint64_t* frames_per_band, uint32_t* chunks_per_band)
 {
@@ -482,13 +517,9 @@ apply_bench(const aqz_stage_bench_options* bench, StageOptions& o)
     o.skip_level0_split = bench->skip_level0_split != 0;
     if (bench->placement_tries)
         o.placement_tries = bench->placement_tries;
-    o.placement_mode = bench->placement_mode;
-    if (o.placement_mode > 2)
-        throw Error(AQZ_STATUS_INVALID_ARGUMENT, "placement_mode must be 0, 1 or 2");
-    if (bench->placement_spacer_bytes)
-        o.placement_spacer = bench->placement_spacer_bytes;
     if (bench->placement_reps)
         o.placement_reps = bench->placement_reps;
+    o.placement_never_accept = (bench->placement_flags & 1u) != 0;
     o.knobs = bench->knobs;
     if (bench->nt_policy)
         o.nt_mode = bench->nt_policy & 7u;
@@ -897,6 +928,12 @@ aqz_stage_placement_report(const aqz_stage* st, aqz_placement_report* out)
         out->ms[i] = r.ms[i];
     out->kept_ms_final = r.kept_ms_final;
     out->peak_device_bytes = r.peak_device;
+    out->probe_bus_gbs = r.probe_bus_gbs;
+    out->expected_ms = r.expected_ms;
+    out->alg_bytes = r.alg_bytes;
+    out->accepted = r.accepted ? 1u : 0u;
+    for (size_t i = 0; i < r.probe_gbs.size() && i < 32; ++i)
+        out->probe_gbs[i] = r.probe_gbs[i];
     return AQZ_STATUS_SUCCESS;
 }
 

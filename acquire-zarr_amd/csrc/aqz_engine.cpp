@@ -5,6 +5,7 @@
 #include "aqz_zstd.hh"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -44,17 +45,34 @@ DevBuf::~DevBuf()
     release();
 }
 
+// A failed release leaks device memory silently unless it is said: the
+// destructor path cannot throw, so it is logged once per kind.
+static void
+release_check(hipError_t e, const char* what)
+{
+    if (e == hipSuccess)
+        return;
+    (void)hipGetLastError();
+    static std::atomic<unsigned> said{ 0 };
+    if (said.fetch_add(1) < 8)
+        std::fprintf(stderr, "aqz: %s failed while releasing device memory: %s\n", what,
+                     hipGetErrorString(e));
+}
+
 void
 DevBuf::release()
 {
     if (p && !view) {
-        if (!vmm.empty()) {
-            (void)hipMemUnmap(p, vmm_span);
+        if (vmm_span) {
+            // every piece was its own hipMemMap: unmapped one by one, then
+            // the handles and the reserved range
+            for (size_t i = 0; i < vmm_mapped; ++i)
+                release_check(hipMemUnmap(p + i * vmm_piece, vmm_piece), "hipMemUnmap");
             for (auto h : vmm)
-                (void)hipMemRelease(h);
-            (void)hipMemAddressFree(p, vmm_span);
+                release_check(hipMemRelease(h), "hipMemRelease");
+            release_check(hipMemAddressFree(p, vmm_span), "hipMemAddressFree");
         } else {
-            (void)hipFree(p);
+            release_check(hipFree(p), "hipFree");
         }
     }
     p = nullptr;
@@ -62,20 +80,13 @@ DevBuf::release()
     view = false;
     vmm.clear();
     vmm_span = 0;
+    vmm_piece = 0;
+    vmm_mapped = 0;
 }
 
 DevBuf::DevBuf(DevBuf&& o) noexcept
-  : p(o.p)
-  , n(o.n)
-  , view(o.view)
-  , vmm(std::move(o.vmm))
-  , vmm_span(o.vmm_span)
 {
-    o.p = nullptr;
-    o.n = 0;
-    o.view = false;
-    o.vmm.clear();
-    o.vmm_span = 0;
+    *this = std::move(o);
 }
 
 DevBuf&
@@ -88,11 +99,15 @@ DevBuf::operator=(DevBuf&& o) noexcept
         view = o.view;
         vmm = std::move(o.vmm);
         vmm_span = o.vmm_span;
+        vmm_piece = o.vmm_piece;
+        vmm_mapped = o.vmm_mapped;
         o.p = nullptr;
         o.n = 0;
         o.view = false;
         o.vmm.clear();
         o.vmm_span = 0;
+        o.vmm_piece = 0;
+        o.vmm_mapped = 0;
     }
     return *this;
 }
@@ -137,18 +152,27 @@ DevBuf::alloc(size_t bytes, unsigned flags)
         while (align * 2 <= piece && align < (size_t(1) << 30))
             align *= 2;
         hip_check(hipMemAddressReserve(&q, span, align, nullptr, 0), "hipMemAddressReserve");
+        // from here on release() undoes exactly what was done, also when a
+        // create or map below throws
         p = static_cast<uint8_t*>(q);
         vmm_span = span;
-        for (size_t off = 0; off < span; off += piece) {
-            hipMemGenericAllocationHandle_t h{};
-            hip_check(hipMemCreate(&h, piece, &prop, 0), "hipMemCreate");
-            vmm.push_back(h);
-            hip_check(hipMemMap(p + off, piece, 0, h, 0), "hipMemMap");
+        vmm_piece = piece;
+        try {
+            for (size_t off = 0; off < span; off += piece) {
+                hipMemGenericAllocationHandle_t h{};
+                hip_check(hipMemCreate(&h, piece, &prop, 0), "hipMemCreate");
+                vmm.push_back(h);
+                hip_check(hipMemMap(p + off, piece, 0, h, 0), "hipMemMap");
+                ++vmm_mapped;
+            }
+            hipMemAccessDesc acc{};
+            acc.location = prop.location;
+            acc.flags = hipMemAccessFlagsProtReadWrite;
+            hip_check(hipMemSetAccess(p, span, &acc, 1), "hipMemSetAccess");
+        } catch (...) {
+            release();
+            throw;
         }
-        hipMemAccessDesc acc{};
-        acc.location = prop.location;
-        acc.flags = hipMemAccessFlagsProtReadWrite;
-        hip_check(hipMemSetAccess(p, span, &acc, 1), "hipMemSetAccess");
         n = bytes;
         return;
     }
@@ -582,32 +606,30 @@ Stage::place_level(StageLevel& L, uint8_t* at)
               "hipMemcpy");
 }
 
-// Placement search (bench-only, StageOptions::placement_tries > 1).  The
-// fused kernels' launch time depends on which physical memory the
-// chunk-layer rings land in: the same kernel on the same source ran a C2
-// launch in one of about three bands (0.39 / 0.41 / 0.43 ms) depending only
-// on the stage's allocations (profiles/r02_mode_probe.txt), and the same
-// virtual addresses land in different bands (r02_va_probe.txt).  Round 3
-// ruled out translation misses, extra HBM traffic, DRAM/TCC request stalls
-// (PMC per placement, profiles/r03_placement_pmc.txt), the chunk stride
-// (pitch pads), the XCD walk phase and plain streaming rates of the same
-// buffers (r03_placement_probes.txt): the effect is not observable from user
-// space, so it is searched, not predicted.  Each candidate is timed on
-// random frames over `reps` launches; a loser is freed and a spacer
-// allocation (held until the search ends) pushes the next candidate
-// elsewhere, so the peak is two ring sets plus the spacers.  Mode 0 (the
-// default) doubles the spacer after every loser, up to 4 GiB: the fast band
-// comes with earlier allocations held (round 4, profiles/
-// r04_placement_localize.txt), and on some boxes only after several GB of
-// them.  Mode 2 keeps the spacer fixed (round 3); mode 1 holds every
-// candidate (round 2).  The kept placement is re-timed alone at the end
-// (kept_ms_final).  Only for rings >= 256 MiB on the fused paths.
+// Placement search (StageOptions::placement_tries > 1; the bench and the
+// drop-in binding pass it).  The fused kernels' launch time depends on the
+// physical memory the chunk-layer rings land in: on
+// hipMalloc'd rings C2 runs 0.88-0.90 ms per 256-frame launch on every box,
+// on the shipped arena of 2 MiB pieces 0.76-0.81 ms on most boxes and about
+// 0.84-0.89 ms on a few.  The effect is not observable from user space, so
+// it is timed, not predicted:
+//   * candidate 0 is the rings as created; each candidate is timed on random
+//     frames over `reps` launches after 2 warm-ups;
+//   * the expectation is the timing launch's algorithmic bytes at the rate
+//     of the copy-third probe (the stage's 1 : 4/3 bus shape, nontemporal)
+//     streaming the same random frames into the candidate's own memory --
+//     plain streaming does not see the placement bands (r04_probe_pieces);
+//   * while the best candidate is more than kPlacementTolerance over it,
+//     a fresh ring set of the same kind (a new arena of 2 MiB pieces, or new
+//     per-level allocations) is made while the best is held, timed, and the
+//     loser freed at once.
+// Peak: two ring sets + the random frames (aqz_stage_estimate_memory).
+// The kept placement is re-timed alone at the end (kept_ms_final).  Only
+// for rings >= 256 MiB on the fused paths.
 void
 Stage::calibrate_placement()
 {
-    uint32_t tries = opt_.placement_tries;
-    uint32_t mode = opt_.placement_mode;
-    uint64_t spacer = opt_.placement_spacer;
+    const uint32_t tries = opt_.placement_tries;
     const uint32_t reps = std::max<uint32_t>(1, opt_.placement_reps);
     uint64_t ring_bytes = 0, set_bytes = 0;
     std::vector<bool> has_ring(lv_.size());
@@ -624,17 +646,14 @@ Stage::calibrate_placement()
     if (tries <= 1 || n == 0 || !(fused_2d_ || fused_3d_) || (xy_ && !xy_direct_) ||
         ring_bytes < (uint64_t(256) << 20))
         return;
-    // With the ring arena, candidate 0 is the arena; later candidates are
-    // per-level allocations (the search below), tried only while no
-    // candidate is 8% faster than the slowest seen -- on the boxes where the
-    // arena lands in the fast band that is one more candidate, on the rare
-    // box where it does not, the search (profiles/r04_bench_default_vmm_slowbox.json)
-    const bool arena0 = arena_.p != nullptr;
+    const bool arena = arena_.p != nullptr;
+    if (arena) // the rings are views: a ring set costs the whole arena
+        set_bytes = set_bytes - ring_bytes + arena_.physical();
     const uint64_t fb0 = uint64_t(lv_[0].W) * lv_[0].H * bpp_;
     // the random source in the same kind of memory as the rings, so the
     // timing is the rings' placement and not the scratch source's
     DevBuf src;
-    alloc_large(src, size_t(n) * fb0, arena_.p != nullptr);
+    alloc_large(src, size_t(n) * fb0, arena);
     hip_check(hipMemsetAsync(src.p, 0, src.n, stream_), "hipMemsetAsync");
     hip_check(launch_fill_random(src.p, src.n, 0x5eedull, stream_), "fill launch");
     uint64_t live = memory_usage().device + src.n;
@@ -647,28 +666,70 @@ Stage::calibrate_placement()
         fw0.push_back(L.frames_written);
         lfc0.push_back(L.level_frame_count);
     }
-    auto measure = [&]() {
-        run_batch(src.p, n); // warm-up
-        hip_check(hipEventRecord(a, stream_), "hipEventRecord");
-        for (uint32_t r = 0; r < reps; ++r)
-            run_batch(src.p, n);
-        hip_check(hipEventRecord(b, stream_), "hipEventRecord");
-        hip_check(hipEventSynchronize(b), "hipEventSynchronize");
-        float ms = 0;
-        hip_check(hipEventElapsedTime(&ms, a, b), "hipEventElapsedTime");
+    constexpr uint32_t kWarm = 2;
+    std::vector<uint64_t> emitted(lv_.size(), 0);
+    auto restore = [&]() {
         for (size_t k = 0; k < lv_.size(); ++k) {
             lv_[k].frames_written = fw0[k];
             lv_[k].level_frame_count = uint32_t(lfc0[k]);
             lv_[k].slot_layer.assign(lv_[k].n_slots, -1);
         }
-        return double(ms) / reps;
+    };
+    auto elapsed = [&]() {
+        hip_check(hipEventSynchronize(b), "hipEventSynchronize");
+        float ms = 0;
+        hip_check(hipEventElapsedTime(&ms, a, b), "hipEventElapsedTime");
+        return double(ms);
+    };
+    auto measure = [&]() {
+        for (uint32_t w = 0; w < kWarm; ++w)
+            run_batch(src.p, n);
+        hip_check(hipEventRecord(a, stream_), "hipEventRecord");
+        for (uint32_t r = 0; r < reps; ++r)
+            run_batch(src.p, n);
+        hip_check(hipEventRecord(b, stream_), "hipEventRecord");
+        const double ms = elapsed() / reps;
+        for (size_t k = 0; k < lv_.size(); ++k)
+            emitted[k] = (lv_[k].frames_written - fw0[k]) / (kWarm + reps);
+        restore();
+        return ms;
+    };
+    // The copy-third probe over the random frames into the candidate's
+    // memory (the arena, or the largest ring): every variant, best of 3
+    // groups of 4 launches each; the best variant's bus GB/s.
+    auto probe = [&]() {
+        DevBuf* dst = &arena_;
+        if (!arena)
+            for (auto& L : lv_)
+                if (L.ring.n > dst->n)
+                    dst = &L.ring;
+        const uint64_t rd = probe_copy_third_read_bytes(src.n, dst->n);
+        if (rd < (uint64_t(64) << 20))
+            return 0.0;
+        double best = 0;
+        for (int v = 0; v < kPlacementProbeVariants; ++v) {
+            hip_check(launch_probe_copy_third(src.p, dst->p, rd, stream_, v), "probe launch");
+            for (int g = 0; g < 3; ++g) {
+                hip_check(hipEventRecord(a, stream_), "hipEventRecord");
+                for (int r = 0; r < 4; ++r)
+                    hip_check(launch_probe_copy_third(src.p, dst->p, rd, stream_, v),
+                              "probe launch");
+                hip_check(hipEventRecord(b, stream_), "hipEventRecord");
+                const double ms = elapsed() / 4;
+                if (ms > 0 && (best == 0 || ms < best))
+                    best = ms;
+            }
+        }
+        return best > 0 ? double(rd) * (7.0 / 3.0) / (best * 1e-3) / 1e9 : 0.0;
     };
     struct Placement
     {
+        DevBuf arena;
         std::vector<DevBuf> ring, flags, ref;
     };
     auto take = [&]() {
         Placement pl;
+        pl.arena = std::move(arena_);
         for (auto& L : lv_) {
             pl.ring.push_back(std::move(L.ring));
             pl.flags.push_back(std::move(L.flags));
@@ -676,50 +737,56 @@ Stage::calibrate_placement()
         }
         return pl;
     };
+    auto fresh = [&]() {
+        if (arena) {
+            arena_.alloc(arena_rings_ + opt_.ring_arena, kArenaFlags);
+            place_rings_at(0);
+        } else {
+            for (size_t k = 0; k < lv_.size(); ++k)
+                if (has_ring[k])
+                    place_level(lv_[k]);
+        }
+    };
     PlacementReport rep;
     rep.reps = reps;
-    rep.mode = arena0 ? 3u : mode;
+    rep.mode = arena ? 3u : 4u;
     Placement best;
     double best_ms = 0;
-    std::vector<Placement> held; // mode 1
-    std::vector<DevBuf> spacers; // mode 0
     try {
         for (uint32_t t = 0; t < tries; ++t) {
             if (t > 0) {
-                for (size_t k = 0; k < lv_.size(); ++k)
-                    if (has_ring[k])
-                        place_level(lv_[k]);
+                fresh(); // the best so far is held: this set is other memory
                 live += set_bytes;
                 peak = std::max(peak, live);
             }
             const double ms = measure();
             rep.ms.push_back(ms);
+            rep.probe_gbs.push_back(probe());
+            if (t == 0) {
+                for (size_t k = 0; k < lv_.size(); ++k)
+                    rep.alg_bytes += emitted[k] * uint64_t(lv_[k].W) * lv_[k].H * bpp_ *
+                                     (k == 0 ? (opt_.skip_level0_split ? 1 : 2) : 1);
+                rep.probe_bus_gbs = rep.probe_gbs[0];
+                if (rep.probe_bus_gbs > 0)
+                    rep.expected_ms = double(rep.alg_bytes) / (rep.probe_bus_gbs * 1e9) * 1e3;
+            }
             const bool better = t == 0 || ms < best_ms;
             Placement cur = take();
-            Placement& loser = better ? best : cur;
-            if (t > 0) { // a loser exists
-                if (mode == 1)
-                    held.push_back(std::move(loser));
-                else {
-                    loser = Placement{};
-                    live -= set_bytes;
-                }
-            }
             if (better) {
+                if (t > 0)
+                    live -= set_bytes; // the old best, freed now
                 best = std::move(cur);
                 best_ms = ms;
                 rep.kept = t;
+            } else {
+                cur = Placement{};
+                live -= set_bytes;
             }
-            const double worst = *std::max_element(rep.ms.begin(), rep.ms.end());
-            if (best_ms < 0.92 * worst || t + 1 == tries)
+            rep.accepted = rep.expected_ms > 0 && !opt_.placement_never_accept &&
+                           best_ms <= (1.0 + kPlacementTolerance) * rep.expected_ms;
+            if (rep.accepted || t + 1 == tries ||
+                (rep.expected_ms == 0 && !opt_.placement_never_accept))
                 break;
-            if (mode != 1 && spacer > 0) {
-                spacers.emplace_back(spacer); // the next candidate lands elsewhere
-                live += spacer;
-                peak = std::max(peak, live);
-                if (mode == 0)
-                    spacer = std::min<uint64_t>(spacer * 2, kMaxPlacementSpacer);
-            }
         }
     } catch (const Error& e) {
         if (e.status != 6 || rep.ms.empty()) // out of memory: keep the best so far
@@ -727,18 +794,15 @@ Stage::calibrate_placement()
         (void)hipGetLastError();
     }
     hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
-    held.clear();
-    spacers.clear();
     {
         Placement cur = take(); // a candidate placed but not measured (OOM)
     }
+    arena_ = std::move(best.arena);
     for (size_t k = 0; k < lv_.size(); ++k) {
         lv_[k].ring = std::move(best.ring[k]);
         lv_[k].flags = std::move(best.flags[k]);
         lv_[k].ref_table = std::move(best.ref[k]);
     }
-    if (arena0 && rep.kept != 0)
-        arena_ = DevBuf{}; // a per-level placement won: the arena is unused
     rep.kept_ms_final = measure();
     rep.peak_device = peak;
     placement_ = rep;
@@ -757,7 +821,7 @@ Stage::calibrate_placement()
 void
 Stage::grant_access(int device)
 {
-    if (!arena_.p || arena_.vmm.empty())
+    if (!arena_.p || !arena_.vmm_span)
         return; // hipMalloc'd memory: peer access covers it
     std::lock_guard<std::mutex> lk(access_mu_);
     if (std::find(granted_.begin(), granted_.end(), device) != granted_.end())
@@ -770,6 +834,21 @@ Stage::grant_access(int device)
     granted_.push_back(device);
 }
 
+// every level's ring (has_data words, frame table) placed in the arena at
+// offset, levels back to back, each 64 KiB aligned
+void
+Stage::place_rings_at(uint64_t offset)
+{
+    uint64_t at = offset;
+    for (size_t k = 0; k < lv_.size(); ++k) {
+        StageLevel& L = lv_[k];
+        if (!(k == 0 && opt_.skip_level0_split)) {
+            place_level(L, arena_.p + at);
+            at += (L.slot_bytes * L.n_slots + 0xffffull) & ~0xffffull;
+        }
+    }
+}
+
 void
 Stage::set_ring_offset(uint64_t offset)
 {
@@ -778,13 +857,8 @@ Stage::set_ring_offset(uint64_t offset)
     if (offset % 256 || offset + arena_rings_ > arena_.n)
         throw Error(1, "ring offset outside the arena's slack (or not 256-B aligned)");
     hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
-    uint64_t at = offset;
-    for (size_t k = 0; k < lv_.size(); ++k) {
-        StageLevel& L = lv_[k];
-        if (!(k == 0 && opt_.skip_level0_split)) {
-            place_level(L, arena_.p + at);
-            at += (L.slot_bytes * L.n_slots + 0xffffull) & ~0xffffull;
-        }
+    place_rings_at(offset);
+    for (auto& L : lv_) {
         L.frames_written = 0;
         L.level_frame_count = 0;
         L.slot_layer.assign(L.n_slots, -1);
@@ -1775,40 +1849,33 @@ Stage::estimate_memory(const ArrayDesc& desc, const StageOptions& opt_in)
     }
     const uint64_t fb0 = uint64_t(levels[0][n - 1].array_size_px) *
                          levels[0][n - 2].array_size_px * bpp;
-    f.device += 2 * B * fb0; // H2D staging (host sources)
-    f.pinned += 2 * B * fb0; // pageable -> pinned staging
-    if (base.needs_xy_transposition())
-        f.device += B * fb0;
     // the shipped ring arena: the rings 64 KiB aligned, rounded up to whole
     // pieces (2 MiB; an upper bound of 1 GiB for the bench's other pieces)
     const bool arena =
       opt.ring_arena || (opt.ring_malloc_flags == 0 && arena_rings >= kArenaMinRings);
+    uint64_t arena_phys = 0;
     if (arena) {
         const uint64_t G = opt.ring_malloc_flags ? uint64_t(1) << 30 : uint64_t(2) << 20;
-        f.device += (arena_rings + opt.ring_arena + G - 1) / G * G - ring_bytes;
+        arena_phys = (arena_rings + opt.ring_arena + G - 1) / G * G;
+        f.device += arena_phys - ring_bytes;
     }
-    // the creation-time placement search's transient peak (calibrate_placement):
-    // its random source batch, and one more ring set + the spacers (mode 0)
-    // or every other candidate (mode 1).  An upper bound: the search may
-    // not run (small rings, generic cascade) or stop early.  With the arena
-    // it is candidate 0, and the per-level candidates come on top of it.
+    // Two transients that never overlap: the creation-time placement search
+    // (calibrate_placement: its random frames and a second ring set, freed
+    // before the constructor returns), and what the first appends allocate
+    // (H2D staging for host sources, the XY transposition buffer).  The
+    // bound holds the larger.
+    uint64_t steady = 2 * B * fb0; // H2D staging (host sources)
+    f.pinned += 2 * B * fb0;       // pageable -> pinned staging
+    if (base.needs_xy_transposition())
+        steady += B * fb0;
+    uint64_t creation = 0;
     if (opt.placement_tries > 1 && ring_bytes >= (uint64_t(256) << 20)) {
-        if (arena)
-            f.device += uint64_t(2) << 20; // the timing source in 2 MiB pieces
-        const uint64_t extra = opt.placement_tries - 1;
-        f.device += B * fb0;
-        if (opt.placement_mode == 1) {
-            f.device += extra * set_bytes;
-        } else {
-            f.device += set_bytes;
-            uint64_t sp = opt.placement_spacer;
-            for (uint64_t t = 0; t < extra; ++t) {
-                f.device += sp;
-                if (opt.placement_mode == 0)
-                    sp = std::min<uint64_t>(sp * 2, kMaxPlacementSpacer);
-            }
-        }
+        const uint64_t src = arena && B * fb0 >= (uint64_t(64) << 20)
+                               ? (B * fb0 + (uint64_t(2) << 20) - 1) >> 21 << 21
+                               : B * fb0;
+        creation = src + (arena ? set_bytes - ring_bytes + arena_phys : set_bytes);
     }
+    f.device += std::max(steady, creation);
     return f;
 }
 

@@ -44,6 +44,14 @@ hipError_t launch_import_frames(uint8_t* dst, const uint8_t* src, const uint64_t
 hipError_t launch_zero_frame_tiles(uint8_t* fb, uint64_t bpc,
                                    uint32_t n_tiles, uint32_t tile_bytes,
                                    hipStream_t stream);
+// aqz_probe.hip: the copy-third streaming shape (1 read : 4/3 write) of
+// read_bytes from src into dst (>= 4/3 read_bytes + one workgroup's block),
+// variant 0-2 (kPlacementProbeVariants); the largest read size a source and
+// destination of these sizes take (0 = too small)
+constexpr int kPlacementProbeVariants = 3;
+uint64_t probe_copy_third_read_bytes(uint64_t src_bytes, uint64_t dst_bytes);
+hipError_t launch_probe_copy_third(const uint8_t* src, uint8_t* dst, uint64_t read_bytes,
+                                   hipStream_t stream, int variant);
 
 void hip_check(hipError_t e, const char* what);
 
@@ -54,14 +62,18 @@ struct DevBuf
     uint8_t* p = nullptr;
     size_t n = 0;
     bool view = false;
-    // kVmm allocations (bench placement probes): physical pieces from
-    // hipMemCreate mapped into one reserved range of vmm_span bytes
+    // kVmm allocations (the ring arena): physical pieces of vmm_piece bytes
+    // from hipMemCreate, the first vmm_mapped of them mapped back to back
+    // into one reserved range of vmm_span bytes.  vmm_span != 0 marks a
+    // reserved range (released piece by piece, never hipFree'd).
     std::vector<hipMemGenericAllocationHandle_t> vmm;
     size_t vmm_span = 0;
+    size_t vmm_piece = 0;
+    size_t vmm_mapped = 0;
     static constexpr unsigned kVmm = 0x100u; // alloc flag; bits 9-13 = v:
                                              // pieces of 2^(16 + v) bytes
                                              // (31: the whole size)
-    size_t physical() const { return vmm.empty() ? n : vmm_span; }
+    size_t physical() const { return vmm_span ? vmm_span : n; }
     DevBuf() = default;
     explicit DevBuf(size_t bytes) { alloc(bytes); }
     ~DevBuf();
@@ -200,8 +212,6 @@ struct ArrayDesc
     int32_t device = 0;
 };
 
-// the placement search's spacers grow up to this (mode 0)
-constexpr uint64_t kMaxPlacementSpacer = uint64_t(4) << 30;
 // StageOptions::ring_malloc_flags bit: per-level ring allocations (the
 // round-3 placement) instead of the shipped arena
 constexpr uint32_t kRingsPlain = 0x10000u;
@@ -215,15 +225,15 @@ struct StageOptions
     uint64_t first_frame = 0;
     uint32_t z_slab_begin = 0, z_slab_end = 0; // aqz_stage_options
     // creation-time placement search (aqz_stage_options.placement_tries;
-    // 0/1 = off): up to placement_tries placements of the chunk-layer rings
-    // are timed and the fastest kept.  mode 0: a losing placement is freed
-    // and a spacer is held until the search ends, starting at
-    // placement_spacer bytes and doubling up to kMaxPlacementSpacer; mode 2:
-    // the same with a fixed spacer; mode 1: every candidate is held.
+    // 0/1 = off): the rings as created are candidate 0; while the best so far
+    // is slower than kPlacementTolerance over the expectation (the stage's
+    // algorithmic bytes at the rate of the copy-third probe over the same
+    // memory), up to placement_tries - 1 fresh ring sets of the same kind
+    // follow, each losing set freed at once (peak: 2 ring sets + the random
+    // frames).  placement_reps timed launches per candidate.
     uint32_t placement_tries = 0;
-    uint32_t placement_mode = 0;
-    uint64_t placement_spacer = uint64_t(128) << 20;
     uint32_t placement_reps = 10;
+    bool placement_never_accept = false; // bench: every try runs
     // Kernel tuning (aqz_stage_bench_options; never read from the
     // environment, so a deployed library always runs the shipped kernels).
     uint32_t knobs = 0;            // A/B switches (0 = the shipped kernels)
@@ -250,8 +260,17 @@ struct PlacementReport
     double kept_ms_final = 0;     // the kept placement re-timed alone
     uint64_t peak_device = 0;     // stage device bytes at the search's peak
     uint32_t reps = 0;            // timed launches per candidate
-    uint32_t mode = 0;
+    uint32_t mode = 0;            // 3: ring arenas, 4: per-level rings
+    std::vector<double> probe_gbs; // the copy-third probe over each candidate
+    double probe_bus_gbs = 0;     // copy-third probe over the timing memory
+    double expected_ms = 0;       // the batch's algorithmic bytes at that rate
+    uint64_t alg_bytes = 0;       // algorithmic bytes of one timing launch
+    bool accepted = false;        // the kept one is within the tolerance
 };
+
+// a candidate within this fraction over the probe's expectation ends the
+// placement search
+constexpr double kPlacementTolerance = 0.03;
 
 struct LevelLayout
 {
@@ -432,6 +451,7 @@ class Stage
 
     void run_batch(const uint8_t* dsrc, uint32_t n);
     void place_level(StageLevel& L, uint8_t* at = nullptr);
+    void place_rings_at(uint64_t offset);
     void calibrate_placement();
     void build_shard_order(StageLevel& L);
     void ensure_comp_slots(StageLevel& L);

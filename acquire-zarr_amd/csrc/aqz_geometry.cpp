@@ -298,6 +298,38 @@ ArrayDimensions::shard_internal_index(uint32_t chunk_index) const
     return static_cast<uint32_t>(index);
 }
 
+// array.dimensions.cpp:406-453: the chunks of layer `layer` (of one append-
+// dimension shard row) that belong to `shard` fill some of its internal
+// slots [layer * per_layer, (layer + 1) * per_layer); the rest is ragged
+// padding.  Computed over the layer's own chunks (the reference filters the
+// shard's whole chunk list by layer: the same set), ascending.
+std::vector<uint32_t>
+ArrayDimensions::skipped_internal_indices_for_shard_layer(uint32_t shard, uint32_t layer) const
+{
+    const uint32_t layers = std::max<uint32_t>(1, chunk_layers_per_shard());
+    const uint32_t per_layer = chunks_per_shard() / layers;
+    const uint64_t lo = uint64_t(layer) * per_layer;
+    std::vector<uint8_t> filled(per_layer, 0);
+    uint32_t n = 0;
+    const uint32_t c0 = layer * chunks_in_memory_;
+    for (uint32_t c = c0; c < c0 + chunks_in_memory_; ++c) {
+        if (shard_index_for_chunk(c) != shard)
+            continue;
+        const uint64_t internal = shard_internal_index(c);
+        if (internal >= lo && internal < lo + per_layer && !filled[internal - lo]) {
+            filled[internal - lo] = 1;
+            ++n;
+        }
+    }
+    std::vector<uint32_t> out;
+    if (n == per_layer)
+        return out;
+    for (uint32_t i = 0; i < per_layer; ++i)
+        if (!filled[i])
+            out.push_back(uint32_t(lo + i));
+    return out;
+}
+
 // ---------------------------------------------------------------------------
 // Pyramid level rule (downsampler.cpp:8-37, 494-597)
 // ---------------------------------------------------------------------------

@@ -92,6 +92,12 @@ class ArrayDimensions
     uint32_t chunks_per_shard() const;
     uint32_t number_of_shards() const;
     uint32_t chunk_layers_per_shard() const { return dims_[0].shard_size_chunks; }
+    // Internal indices of shard `shard` that no chunk of chunk layer `layer`
+    // (of one append-dimension shard row) fills -- the ragged padding the
+    // reference skips so the shard's countdown completes
+    // (array.dimensions.cpp:406-453)
+    std::vector<uint32_t> skipped_internal_indices_for_shard_layer(uint32_t shard,
+                                                                   uint32_t layer) const;
     // dim-1 banding (array.dimensions.cpp:344-373): append chunk 1 plus an
     // intermediate dim, no transposition; a band is one chunk row of dim 1
     bool supports_dim1_banding() const

@@ -7,6 +7,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 namespace {
@@ -14,8 +15,10 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // U 16-B vectors per lane, loaded before any is used (the stage's kernels
-// keep 128 B per lane in flight); U divisible by 3 for the 1/3 shapes
+// keep 128 B per lane in flight); U divisible by 3 for the 1/3 shapes.
+// AQZ_PROBE_DEEP: 12 (192 B per lane, 48 KiB per workgroup).
 constexpr int kU = 6;
+constexpr int kUDeep = 12;
 
 template<int MODE, bool NTS>
 __device__ __forceinline__ void
@@ -27,7 +30,7 @@ put(u32x4* p, u32x4 v)
         *p = v;
 }
 
-template<int MODE, bool NTS>
+template<int MODE, bool NTS, int kU = kU>
 __global__ __launch_bounds__(256) void
 probe_stream(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
              u32x4* __restrict__ dst3, uint32_t* __restrict__ sink)
@@ -87,6 +90,50 @@ probe_alloc(DevMem& m, size_t bytes, bool pieces)
 
 } // namespace
 
+namespace aqz {
+
+uint64_t
+probe_copy_third_read_bytes(uint64_t src_bytes, uint64_t dst_bytes)
+{
+    constexpr uint64_t wg = uint64_t(kUDeep) * 256 * 16; // a multiple of both
+    if (dst_bytes < 2 * wg)
+        return 0;
+    const uint64_t r = std::min<uint64_t>(src_bytes, (dst_bytes - wg) / 4 * 3);
+    return std::min<uint64_t>(r / wg, 0x7fffffffull) * wg;
+}
+
+// The stage's own bus shape (1 read : 4/3 write) from src into dst: dst
+// receives the copy and behind it the third.  variant 0: nontemporal
+// stores, 96 B per lane in flight; 1: the same with 192 B; 2: plain stores.
+// The placement search (Stage::calibrate_placement) takes the best of them
+// over its random frames and the candidate's rings: the practical ceiling
+// of this shape in that memory, at the stage's launch size.
+hipError_t
+launch_probe_copy_third(const uint8_t* src, uint8_t* dst, uint64_t read_bytes,
+                        hipStream_t stream, int variant)
+{
+    const uint64_t per_wg = uint64_t(variant == 1 ? kUDeep : kU) * 256 * 16;
+    const uint64_t grid = read_bytes / per_wg;
+    if (grid == 0 || grid > 0x7fffffffull || read_bytes % per_wg)
+        return hipErrorInvalidValue;
+    const auto* in = reinterpret_cast<const u32x4*>(src);
+    auto* o = reinterpret_cast<u32x4*>(dst);
+    auto* o3 = reinterpret_cast<u32x4*>(dst + read_bytes);
+    const dim3 g{ uint32_t(grid), 1, 1 };
+    if (variant == 1)
+        hipLaunchKernelGGL((probe_stream<AQZ_PROBE_COPY_THIRD, true, kUDeep>), g, dim3(256), 0,
+                           stream, in, o, o3, nullptr);
+    else if (variant == 2)
+        hipLaunchKernelGGL((probe_stream<AQZ_PROBE_COPY_THIRD, false>), g, dim3(256), 0,
+                           stream, in, o, o3, nullptr);
+    else
+        hipLaunchKernelGGL((probe_stream<AQZ_PROBE_COPY_THIRD, true>), g, dim3(256), 0,
+                           stream, in, o, o3, nullptr);
+    return hipGetLastError();
+}
+
+} // namespace aqz
+
 extern "C" aqz_status
 aqz_probe_hbm(int32_t device, int32_t shape, uint64_t bytes, uint32_t reps, double* ms,
               uint64_t* read_bytes)
@@ -94,10 +141,11 @@ aqz_probe_hbm(int32_t device, int32_t shape, uint64_t bytes, uint32_t reps, doub
     const int32_t kind = shape & 0xff;
     const bool plain = (shape & AQZ_PROBE_PLAIN_STORES) != 0;
     const bool pieces = (shape & AQZ_PROBE_PIECES) != 0;
+    const bool deep = (shape & AQZ_PROBE_DEEP) != 0;
     if (!ms || kind < AQZ_PROBE_READ || kind > AQZ_PROBE_READ_THIRD || reps == 0 ||
-        (shape & ~(0xff | AQZ_PROBE_PLAIN_STORES | AQZ_PROBE_PIECES)) != 0)
+        (shape & ~(0xff | AQZ_PROBE_PLAIN_STORES | AQZ_PROBE_PIECES | AQZ_PROBE_DEEP)) != 0)
         return AQZ_STATUS_INVALID_ARGUMENT;
-    const uint64_t per_wg = uint64_t(kU) * 256 * 16;
+    const uint64_t per_wg = uint64_t(deep ? kUDeep : kU) * 256 * 16;
     const uint64_t grid = bytes / per_wg;
     if (grid == 0 || grid > 0x7fffffffull)
         return AQZ_STATUS_INVALID_ARGUMENT;
@@ -129,7 +177,13 @@ aqz_probe_hbm(int32_t device, int32_t shape, uint64_t bytes, uint32_t reps, doub
                 auto* k = static_cast<uint32_t*>(sink.p);
                 const dim3 g{ uint32_t(grid), 1, 1 };
 #define PROBE_LAUNCH(MODE)                                                     \
-    if (plain)                                                                 \
+    if (plain && deep)                                                         \
+        hipLaunchKernelGGL((probe_stream<MODE, false, kUDeep>), g, dim3(256), 0, s, in, o, \
+                           o3, k);                                             \
+    else if (deep)                                                             \
+        hipLaunchKernelGGL((probe_stream<MODE, true, kUDeep>), g, dim3(256), 0, s, in, o, \
+                           o3, k);                                             \
+    else if (plain)                                                            \
         hipLaunchKernelGGL((probe_stream<MODE, false>), g, dim3(256), 0, s, in, o, o3, k); \
     else                                                                       \
         hipLaunchKernelGGL((probe_stream<MODE, true>), g, dim3(256), 0, s, in, o, o3, k)

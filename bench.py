@@ -34,10 +34,10 @@ BPP = {U8: 1, U16: 2, F32: 4}
 
 # aqz_stage_options.placement_tries, as the binding passes it: the shipped
 # rings (one arena of 2 MiB virtual-memory pieces) are
-# timed once at creation and reported (roofline.placement, candidate0_ms),
-# not searched; with the bench flag ring_malloc_flags=0x10000 (per-level
-# hipMalloc, the round-3 placement) up to 16 placements are searched.
-PLACEMENT = dict(placement_tries=16)
+# timed at creation against a streaming probe of the same memory; only when
+# they run more than 3% over that expectation does one fresh arena follow
+# (roofline.placement: candidates, expectation, the one kept).
+PLACEMENT = dict(placement_tries=2)
 
 DTYPE_WORDS = {U8: "uint8", U16: "uint16", F32: "float32"}
 
@@ -133,27 +133,40 @@ def fill_ring(torch, ring, dtype, seed):
         ring.view(torch.float32).uniform_(0.0, 65535.0, generator=g)
 
 
-def pmc_traffic(config, pyramid_only, kernel, frames):
+def pmc_traffic(config, pyramid_only, kernel, frames, ring_allocation):
     """Per-launch HBM bytes of the dominant kernel from the newest committed
-    rocprofv3 PMC summary for this configuration (tools/profile.sh ->
-    tools/pmc_summary.py -> profiles/<round>_<config>_pmc.json: FETCH_SIZE x2
-    + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md).  PMC
-    counters cannot be read inside a plain run, so the value is the profiled
-    run of this same command; None when no summary matches."""
+    rocprofv3 PMC summary for this configuration whose rings were allocated
+    the same way as this run's (tools/profile.sh -> tools/pmc_summary.py ->
+    profiles/<round>_<config>_pmc.json: FETCH_SIZE x2 + WRITE_SIZE, the
+    gfx950 correction of MI355X_MICROARCH.md; the summary records the
+    profiled bench line's ring_allocation).  PMC counters cannot be read
+    inside a plain run, so the value is the profiled run of this same
+    command; (None, None, None) when no summary matches."""
     import glob
     name = config + ("-pyr" if pyramid_only else "")
     files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{name}_pmc.json")))
     for f in reversed(files):
         d = json.load(open(f))
-        if d.get("config") == name and kernel and kernel in d.get("kernel", ""):
+        if (d.get("config") == name and kernel and kernel in d.get("kernel", "")
+                and d.get("ring_allocation") == ring_allocation):
             # (traffic is linear in the frames of a launch: a profile of
             # another launch size is scaled to this one)
             t = d["traffic_bytes_per_launch"]
             fpl = d.get("frames_per_launch")
             if fpl and fpl != frames:
                 t = int(round(t * frames / fpl))
-            return t, os.path.relpath(f, REPO)
-    return None, None
+            return t, os.path.relpath(f, REPO), d
+    return None, None, None
+
+
+def ring_allocation(pl):
+    """How the chunk-layer rings were allocated (aqz_placement_report.mode)."""
+    if pl.get("mode") == 3:
+        return ("one arena of 2 MiB virtual-memory pieces" +
+                (", fresh arena kept" if pl.get("kept") else ""))
+    if pl.get("candidates_ms"):
+        return "per-level allocations, placement search"
+    return "per-level allocations (rings under 256 MiB), no search"
 
 
 def cpu_baseline(cfg, seconds):
@@ -540,7 +553,7 @@ def main():
                          "(0: keep the first allocation)")
     ap.add_argument("--tune", action="append", default=[], metavar="FIELD=VALUE",
                     help="bench-header stage option (aqz_stage_bench_options field, e.g. "
-                         "knobs=8, nt=3, placement_mode=1); repeatable")
+                         "knobs=8, nt=3, placement_reps=20); repeatable")
     ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     args.tune = {k: int(v, 0) for k, v in (t.split("=", 1) for t in args.tune)}
@@ -647,6 +660,7 @@ def main():
         if dist:
             dist.barrier()
         elapsed = t1 - t0
+        elapsed_local = elapsed
         if dist:
             t = torch.tensor([elapsed], dtype=torch.float64, device=reduce_dev(dist, dev))
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -674,7 +688,8 @@ def main():
         out_bytes = sum(n * h * w * bpp for n, (h, w) in zip(emitted[1:], sizes[1:]))
         alg = (emitted[0] * fbytes * (1 if pyramid_only else 2) + out_bytes) // max(1, steps)
         avg_ms = kms / max(1, launches)
-        return dict(elapsed=elapsed, sizes=sizes, fbytes=fbytes, kernel=kernel,
+        return dict(elapsed=elapsed, elapsed_local=elapsed_local, sizes=sizes, fbytes=fbytes,
+                    kernel=kernel,
                     avg_ms=avg_ms, alg=alg, placement=placement,
                     achieved=alg / (avg_ms * 1e-3) / 1e9 if launches else 0.0,
                     value=world * steps * B * fbytes / elapsed / 1e9)
@@ -692,6 +707,23 @@ def main():
         return
 
     main_run = run(args.pyramid_only, args.steps, args.warmup)
+    per_rank = None
+    if dist:
+        # every rank's own kernel time, placement and creation cost, gathered
+        # after the timed region (a few numbers per rank) so a multi-GPU line
+        # shows which rank set the max
+        mp = main_run["placement"]
+        mine = {"rank": rank, "device": dev.index,
+                "kernel_avg_ms": round(main_run["avg_ms"], 5),
+                "frac": round(main_run["achieved"] / HBM_PEAK_GBS, 4),
+                "elapsed_s": round(main_run["elapsed_local"], 5),
+                "candidates_ms": mp.get("candidates_ms"), "kept": mp.get("kept"),
+                "accepted": mp.get("accepted"), "expected_ms": mp.get("expected_ms"),
+                "probe_bus_gbs": mp.get("probe_bus_gbs"),
+                "peak_device_bytes": mp.get("peak_device_bytes"),
+                "stage_create_s": mp.get("stage_create_s")}
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
     side = None
     if not args.pyramid_only and not args.no_pyramid_only_line:
         side = run(True, max(5, args.steps // 2), 2)
@@ -701,7 +733,12 @@ def main():
     sizes, elapsed, value = main_run["sizes"], main_run["elapsed"], main_run["value"]
     kernel, avg_ms, achieved = main_run["kernel"], main_run["avg_ms"], main_run["achieved"]
     alg_per_launch = main_run["alg"]
-    traffic, traffic_src = pmc_traffic(args.config, args.pyramid_only, kernel, B)
+    pl = main_run["placement"]
+    pl["placement_tries"] = args.placement_tries
+    # how the chunk-layer rings were allocated (aqz_placement_report.mode)
+    pl["ring_allocation"] = ring_allocation(pl)
+    traffic, traffic_src, prof = pmc_traffic(args.config, args.pyramid_only, kernel, B,
+                                             pl["ring_allocation"])
 
     result = {
         "metric": f"input GB/s, device-resident multiscale downsample, {DTYPE_WORDS[dt]} "
@@ -741,17 +778,13 @@ def main():
                      "placement": main_run["placement"]},
         "input_rate_frac_of_peak": round(value / world / HBM_PEAK_GBS, 4),
     }
-    pl = result["roofline"]["placement"]
-    pl["placement_tries"] = args.placement_tries
-    # how the chunk-layer rings were allocated (aqz_placement_report.mode)
-    pl["ring_allocation"] = (
-        ("one arena of 2 MiB virtual-memory pieces (candidate 0), kept"
-         if pl.get("kept") == 0 else
-         "one arena of 2 MiB virtual-memory pieces (candidate 0) slower than a "
-         "per-level candidate, which was kept")
-        if pl.get("mode") == 3 else
-        "per-level allocations, placement search" if pl.get("candidates_ms") else
-        "per-level allocations (rings under 256 MiB), no search")
+    if prof:
+        # the profiled run of this command: its rocprof kernel average and
+        # the frac it gives, next to this run's
+        pa = prof.get("steady_avg_duration_ns") or prof.get("avg_duration_ns")
+        result["roofline"]["profile_kernel_avg_ms"] = round(pa / 1e6, 5)
+        result["roofline"]["profile_frac"] = round(
+            alg_per_launch / (pa * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
     if pl.get("kept_ms_final"):
         # the steady state against the kept placement's own re-time
         pl["steady_over_kept_final"] = round(avg_ms / pl["kept_ms_final"], 4)
@@ -764,14 +797,23 @@ def main():
         result["roofline"]["frac_at_candidate0"] = round(
             alg_per_launch / (c0 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         result["roofline"]["kept_ms"] = pl["candidates_ms"][pl["kept"]]
+    pg = pl.get("candidates_probe_gbs") or []
+    if pl.get("kept", 0) < len(pg) and pg[pl["kept"]] > 0:
+        # the practical ceiling of the stage's bus shape in the stage's own
+        # memory: the best of three streaming kernels (1 read : 4/3 write,
+        # nontemporal 96 / 192 B per lane, plain stores) reading the random
+        # frames and writing the kept rings, launches of the stage's size,
+        # timed at creation (aqz_placement_report.probe_gbs)
+        result["roofline"]["probed_ceiling_same_shape"] = pg[pl["kept"]]
+        result["roofline"]["probed_ceiling_source"] = (
+            "copy-third streaming probe over the kept rings' memory at this launch size "
+            "(aqz_placement_report.probe_gbs)")
+        result["roofline"]["frac_of_probed_ceiling"] = round(achieved / pg[pl["kept"]], 4)
     if probe:
-        # this device's practical HBM rates, measured in this run (SURVEY
-        # 8(d)): the dominant kernel against a plain streaming kernel of the
-        # same read:write shape
+        # this device's streaming rates on separate buffers:
+        # 512 MiB launches over a 2 GiB source, so the MALL holds part of
+        # their working set -- a characterisation of the box, not a ceiling
         result["hbm_probe"] = probe
-        result["roofline"]["probed_ceiling_same_shape"] = probe["copy_third_bus_gbs"]
-        result["roofline"]["frac_of_probed_ceiling"] = round(
-            achieved / probe["copy_third_bus_gbs"], 4)
     if side:
         # the downsample alone (no level-0 tile split): reads each frame once
         # and writes 1/3 of it; its input rate against the HBM read peak is
@@ -792,6 +834,8 @@ def main():
                 "kernel_input_frac_of_probed_ceiling": round(
                     B * side["fbytes"] / (side["avg_ms"] * 1e-3) / 1e9 / pr, 4),
                 "probed_ceiling_source": "hbm_probe.read_third_input_gbs"})
+    if per_rank:
+        result["per_rank"] = per_rank
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:

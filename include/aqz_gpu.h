@@ -139,6 +139,18 @@ uint64_t aqz_dims_frames_per_chunk_layer(const aqz_dims* d);
 /* array.dimensions.cpp:393-548 */
 uint32_t aqz_dims_shard_index_for_chunk(const aqz_dims* d, uint32_t chunk);
 uint32_t aqz_dims_shard_internal_index(const aqz_dims* d, uint32_t chunk);
+/* chunks_per_shard, number_of_shards (one append-dimension shard row) and
+ * chunk_layers_per_shard (array.dimensions.cpp:376-392); any may be NULL. */
+aqz_status aqz_dims_shard_geometry(const aqz_dims* d, uint32_t* chunks_per_shard,
+                                   uint32_t* n_shards, uint32_t* layers_per_shard);
+/* skipped_internal_indices_for_shard_layer (array.dimensions.cpp:424-453):
+ * the internal indices of `shard` that chunk layer `layer` (< layers per
+ * shard) leaves unfilled -- ragged padding, skipped so the shard's
+ * countdown completes.  Writes min(count, cap) of them to out (may be NULL
+ * with cap 0) and the count to *n. */
+aqz_status aqz_dims_skipped_internal_indices(const aqz_dims* d, uint32_t shard,
+                                             uint32_t layer, uint32_t* out, size_t cap,
+                                             size_t* n);
 /* supports_dim1_banding, dim1_band_count, frames_per_dim1_band,
  * chunks_per_dim1_band (array.dimensions.cpp:344-373) */
 aqz_status aqz_dims_dim1_banding(const aqz_dims* d, int32_t* supported,
@@ -245,14 +257,17 @@ typedef struct
                                   aqz_gpu_bench.h).  Rings of >= 256 MiB in
                                   all are placed in one arena of 2 MiB
                                   virtual-memory pieces, where the fused
-                                  kernels run in the fast band on nearly
-                                  every box; it is
-                                  candidate 0, and up to n - 1 per-level
-                                  placements follow only while no candidate
-                                  is 8% faster than the slowest seen.  The
-                                  transient peak (a batch of random frames,
-                                  ring sets and spacers) is in
-                                  aqz_stage_estimate_memory.  0/1 = none. */
+                                  kernels run in the fast band on most boxes
+                                  (DESIGN.md section 3).  The arena is timed
+                                  against the stage's algorithmic bytes at
+                                  the rate of a streaming probe of the same
+                                  memory; only when it is more than 3% over
+                                  that, up to n - 1 fresh arenas follow, each
+                                  made while the best is held and freed at
+                                  once if slower.  The transient peak (one
+                                  batch of random frames and a second ring
+                                  set) is in aqz_stage_estimate_memory.
+                                  0/1 = none. */
     uint32_t reserved;
 } aqz_stage_options;
 

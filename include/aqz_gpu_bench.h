@@ -26,26 +26,13 @@ typedef struct
                                   one above). */
     int32_t skip_level0_split; /* 1 = do not tile-split level 0 (the
                                   pyramid-only side measurement) */
-    uint32_t placement_tries;  /* creation-time placement search: 0/1 = off
-                                  (the drop-in default); n > 1 = time up to n
-                                  placements of the chunk-layer rings on
-                                  random frames and keep the fastest (the
-                                  launch time depends on the memory the rings
-                                  land in).  With the shipped
-                                  ring arena, candidate 0 is the arena
-                                  (reported mode 3) and per-level candidates
-                                  follow only while none is 8% faster than
-                                  the slowest seen */
-    uint32_t placement_mode;   /* 0: a losing placement is freed and a spacer
-                                  allocation held until the search ends,
-                                  doubling after every loser up to 4 GiB
-                                  (peak: 2 ring sets + the spacers);
-                                  1: every candidate is held (peak: n sets);
-                                  2: as 0 with a fixed spacer (round 3);
-                                  reported 3: candidate 0 was the ring
-                                  arena */
-    uint64_t placement_spacer_bytes; /* first spacer (0 = 128 MiB) */
+    uint32_t placement_tries;  /* creation-time placement search: 0 = the
+                                  aqz_stage_options value; n > 1 = as there
+                                  (aqz_stage_options.placement_tries) */
     uint32_t placement_reps;   /* timed launches per candidate (0 = 10) */
+    uint32_t placement_flags;  /* 1: never accept a candidate against the
+                                  probe's expectation (every try runs: the
+                                  search's worst-case peak, for tests) */
     /* Kernel tuning for A/B runs.  The library reads none of these from the
      * environment: a stage made by aqz_stage_create always runs the shipped
      * kernels.  Knob bits that skip stores (timing experiments only) exist
@@ -100,11 +87,21 @@ typedef struct
     uint32_t n;                 /* candidates timed (0 = no search ran) */
     uint32_t kept;              /* index of the kept one */
     uint32_t reps;              /* timed launches per candidate (random frames) */
-    uint32_t mode;
+    uint32_t mode;              /* 3: ring arenas of 2 MiB pieces, 4: per-level
+                                   ring allocations */
     double ms[32];              /* ms per launch, candidates 0..min(n,32)-1 */
     double kept_ms_final;       /* the kept placement re-timed alone, after
                                    the others were freed */
     uint64_t peak_device_bytes; /* the stage's device bytes at the search's peak */
+    double probe_bus_gbs;       /* the copy-third probe (1 read : 4/3 write)
+                                   streaming the random frames into the first
+                                   candidate's memory, bus GB/s (0 = not run) */
+    double expected_ms;         /* alg_bytes at probe_bus_gbs */
+    uint64_t alg_bytes;         /* algorithmic bytes of one timing launch */
+    uint32_t accepted;          /* 1: the kept candidate is within 3% of
+                                   expected_ms (the search stopped there) */
+    uint32_t reserved;
+    double probe_gbs[32];       /* the probe over each candidate's memory */
 } aqz_placement_report;
 aqz_status aqz_stage_placement_report(const aqz_stage* st, aqz_placement_report* out);
 
@@ -179,8 +176,10 @@ enum
     AQZ_PROBE_COPY_THIRD = 2,
     AQZ_PROBE_READ_THIRD = 3,
     AQZ_PROBE_PLAIN_STORES = 0x100,
-    AQZ_PROBE_PIECES = 0x200 /* buffers from 2 MiB virtual-memory pieces, as
-                                the stage's chunk-layer rings */
+    AQZ_PROBE_PIECES = 0x200, /* buffers from 2 MiB virtual-memory pieces, as
+                                 the stage's chunk-layer rings */
+    AQZ_PROBE_DEEP = 0x400    /* 192 B per lane in flight (48 KiB per
+                                 workgroup) instead of 96 B */
 };
 aqz_status aqz_probe_hbm(int32_t device, int32_t shape, uint64_t bytes, uint32_t reps,
                          double* ms, uint64_t* read_bytes);

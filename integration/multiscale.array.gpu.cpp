@@ -241,10 +241,12 @@ class GpuMultiscaleArray final
             opt.layer_slots = 2;
             // the library maps the chunk-layer rings from 2 MiB virtual-
             // memory pieces, where the fused kernels run in the fast band on
-            // nearly every box; with tries, a box where that placement is
-            // slow falls back to searching per-level allocations (DESIGN.md
-            // section 3; the transient peak is in aqz_stage_estimate_memory)
-            opt.placement_tries = 16;
+            // most boxes; the arena is timed once against a streaming probe
+            // of the same memory, and only where it runs more than 3% under
+            // that is one fresh arena tried (the
+            // transient peak, one more ring set and a batch of random frames,
+            // is in aqz_stage_estimate_memory)
+            opt.placement_tries = 2;
             if (devices.size() > 1) {
                 opt.z_slab_begin = plan.begin[r];
                 opt.z_slab_end = plan.end[r];

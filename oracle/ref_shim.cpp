@@ -253,6 +253,30 @@ ref_dims_dim1_banding(void* h, int* supported, uint32_t* n_bands,
     *chunks_per_band = d->chunks_per_dim1_band();
 }
 
+// shard geometry (array.dimensions.cpp:376-392) and the ragged-padding skip
+// list of one shard layer (array.dimensions.cpp:424-453): the count, the
+// first min(count, cap) indices into out
+void
+ref_dims_shard_geometry(void* h, uint32_t* chunks_per_shard, uint32_t* n_shards,
+                        uint32_t* layers_per_shard)
+{
+    auto* d = static_cast<ArrayDimensions*>(h);
+    *chunks_per_shard = d->chunks_per_shard();
+    *n_shards = d->number_of_shards();
+    *layers_per_shard = d->chunk_layers_per_shard();
+}
+
+size_t
+ref_dims_skipped_internal_indices(void* h, uint32_t shard, uint32_t layer, uint32_t* out,
+                                  size_t cap)
+{
+    const auto v =
+      static_cast<ArrayDimensions*>(h)->skipped_internal_indices_for_shard_layer(shard, layer);
+    for (size_t i = 0; i < v.size() && i < cap; ++i)
+        out[i] = v[i];
+    return v.size();
+}
+
 // Tile split of one frame into a chunk layer using the reference's own
 // ArrayDimensions + zarr::Chunk::write_tile_rows (chunk.cpp:17-58).  The
 // driving loop restates array.cpp:537-619 (array.cpp itself needs crc32c,

@@ -69,12 +69,14 @@ def test_bench_c2_configuration_exact(gpu, cfg):
     st = gpu.Stage(dims, U16, MEAN, **kw)
     L = st.n_levels()
     assert L == (4 if cfg == "c2-ref4" else 5)
-    # the bench's placement search ran; its creation peak is within the
-    # bench estimate, and the stage keeps one ring set afterwards
+    # the bench's placement search ran (the arena against the probe of its
+    # memory); its creation peak is within the bench estimate, and the stage
+    # keeps one ring set afterwards
     pl = st.placement()
     assert 1 <= len(pl["candidates_ms"]) <= bench.PLACEMENT["placement_tries"]
     assert pl["candidates_ms"][pl["kept"]] == min(pl["candidates_ms"])
-    assert 0 < pl["kept_ms_final"]
+    assert 0 < pl["kept_ms_final"] and pl["mode"] == 3 and pl["probe_bus_gbs"] > 0
+    assert pl["accepted"] or len(pl["candidates_ms"]) == bench.PLACEMENT["placement_tries"]
     assert pl["peak_device_bytes"] <= est["device_bytes"]
     assert st.memory_usage()["device_bytes"] <= gpu.estimate_memory(
         dims, U16, MEAN, force_levels=c["force_levels"], max_batch_frames=B,
@@ -215,6 +217,15 @@ def test_bench_two_ranks_self_launched(gpu, extra):
     assert len(lines) == 1, r.stdout
     d = lines[0]
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["value"] > 0
+    if "--e2e" not in extra:
+        # each rank's kernel time, placement and creation cost, gathered
+        # into rank 0's line
+        pr = d["per_rank"]
+        assert [r["rank"] for r in pr] == [0, 1]
+        for r in pr:
+            assert r["kernel_avg_ms"] > 0 and r["stage_create_s"] > 0
+            assert r["peak_device_bytes"] > 0 and len(r["candidates_ms"]) >= 1
+            assert 0 < r["elapsed_s"] <= 1.001 * d["ms_per_step"] * d["steps"] / 1e3
 
 
 def test_hbm_probe_shapes(gpu):

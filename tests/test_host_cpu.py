@@ -164,6 +164,42 @@ def test_dim1_banding_geometry_matches_reference():
     assert aqz.Dims(c4, ob.U16).dim1_banding() == (True, 4, 64, 64)
 
 
+@pytest.mark.skipif(not ob.ref_available(), reason="oracle/_ref not built")
+def test_shard_skip_lists_match_reference():
+    """aqz_dims_shard_geometry and aqz_dims_skipped_internal_indices (what
+    the binding's ShardRouter skips on a layer's last unit) against the
+    compiled reference's chunks_per_shard / number_of_shards /
+    chunk_layers_per_shard and skipped_internal_indices_for_shard_layer
+    (array.dimensions.cpp:376-453), over random ragged shapes."""
+    import ctypes as C
+    R = ob.ref()
+    u32p = C.POINTER(C.c_uint32)
+    R.ref_dims_shard_geometry.argtypes = [C.c_void_p, u32p, u32p, u32p]
+    R.ref_dims_skipped_internal_indices.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32,
+                                                    u32p, C.c_size_t]
+    R.ref_dims_skipped_internal_indices.restype = C.c_size_t
+    rng = np.random.default_rng(15)
+    nonempty = 0
+    for _ in range(120):
+        dims = _random_dims(rng)
+        a = aqz.Dims(dims, ob.U16)
+        r = ob.OracleDims(dims, ob.U16, use_ref=True)
+        g = [C.c_uint32() for _ in range(3)]
+        R.ref_dims_shard_geometry(r.h, *[C.byref(x) for x in g])
+        assert a.shard_geometry() == tuple(x.value for x in g), dims
+        cps, ns, lps = a.shard_geometry()
+        buf = (C.c_uint32 * max(1, cps))()
+        for shard in range(ns):
+            for layer in range(max(1, lps)):
+                n = R.ref_dims_skipped_internal_indices(r.h, shard, layer, buf, cps)
+                got = a.skipped_internal_indices(shard, layer)
+                assert got == list(buf[:n]), (dims, shard, layer)
+                nonempty += bool(got)
+    assert nonempty > 0  # some shapes have ragged padding
+    with pytest.raises(aqz.AqzError):
+        aqz.Dims(dims, ob.U16).skipped_internal_indices(ns, 0)
+
+
 def test_memory_estimate_counts_the_rings():
     """aqz_stage_estimate_memory (no GPU): the chunk-layer rings dominate;
     for C2 as benched's level-0 geometry, 3 slots x 64 chunks x 8 MiB."""

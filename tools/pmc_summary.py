@@ -54,6 +54,21 @@ def main():
     }
     if fpl:
         res["frames_per_launch"] = fpl
+    # the traced bench line: how its rings were allocated (bench.py matches
+    # a summary to a run by it) and its own event-timed kernel average
+    try:
+        line = [l for l in open(os.path.join(d, "bench_trace.log")) if l.startswith("{")][-1]
+        b = json.loads(line)
+        r = b["roofline"]
+        res["ring_allocation"] = r["placement"]["ring_allocation"]
+        res["bench_kernel_avg_ms"] = r["kernel_avg_ms"]
+        res["bench_frac"] = r["frac"]
+        res["bench_command"] = os.environ.get("BENCH_CMD", "")
+        res["placement"] = {k: r["placement"].get(k) for k in
+                            ("candidates_ms", "kept", "accepted", "expected_ms",
+                             "probe_bus_gbs", "candidates_probe_gbs")}
+    except (OSError, IndexError, KeyError, ValueError):
+        pass
     # the timed launches alone: the stats average also holds the stage's
     # creation-time placement calibration (up to 10 launches per candidate)
     tr = os.path.join(d, "trace", "run_kernel_trace.csv")

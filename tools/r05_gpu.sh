@@ -1,0 +1,43 @@
+#!/usr/bin/env bash
+# Round-5 GPU runs, one function per gpurun call (the profiles/r05_* files
+# come from these):  gpurun -- bash tools/r05_gpu.sh <step>
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+
+# probe rate vs launch size; the default bench line on the same box
+step_p1() {
+O=gpurun_out/r5a
+mkdir -p $O
+timeout -k 10 200 python3 -u tools/probe_sizes.py > $O/probe_sizes.jsonl 2> $O/probe.err || { tail $O/probe.err; exit 1; }
+cat $O/probe_sizes.jsonl
+timeout -k 10 200 python3 -u bench.py --steps 20 --warmup 5 --cpu-seconds 2 > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
+cat $O/bench.json
+}
+
+# probe variants; placement tests; three default bench lines (fresh processes)
+step_p2() {
+O=gpurun_out/r5b
+mkdir -p $O
+timeout -k 10 300 python3 -u tools/probe_sizes.py > $O/probe_variants.jsonl 2> $O/probe.err || { tail $O/probe.err; exit 1; }
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_placement.py -m gpu -v -x --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -12 $O/pytest.log
+for i in 1 2 3; do
+timeout -k 10 200 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-pyramid-only-line > $O/bench$i.json 2> $O/bench$i.err || { tail $O/bench$i.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/bench$i.json')); r=d['roofline']; p=r['placement']; print(json.dumps({'frac': r['frac'], 'ms': r['kernel_avg_ms'], 'cand': p['candidates_ms'], 'kept': p['kept'], 'exp': p['expected_ms'], 'probe': p['probe_bus_gbs'], 'acc': p['accepted'], 'peak_gb': round(p['peak_device_bytes']/1e9,2), 'est_gb': round(p['estimate_device_bytes']/1e9,2), 'ceil': r.get('probed_ceiling_same_shape')}))"
+done
+}
+
+# candidates' stage time vs the streaming probe of the same memory
+step_p3() {
+O=gpurun_out/r5c
+mkdir -p $O
+for i in 1 2; do
+timeout -k 10 120 python3 -u tools/placement_r05.py --tries 6 >> $O/cand.jsonl 2>> $O/cand.err || { tail $O/cand.err; exit 1; }
+timeout -k 10 120 python3 -u tools/placement_r05.py --tries 4 --plain >> $O/cand.jsonl 2>> $O/cand.err || { tail $O/cand.err; exit 1; }
+done
+timeout -k 10 120 python3 -u tools/placement_r05.py --tries 6 --batch 64 >> $O/cand.jsonl 2>> $O/cand.err || { tail $O/cand.err; exit 1; }
+cat $O/cand.jsonl
+}
+
+"step_$1"
