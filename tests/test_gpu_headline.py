@@ -225,7 +225,7 @@ def test_bench_two_ranks_self_launched(gpu, extra):
         for r in pr:
             assert r["kernel_avg_ms"] > 0 and r["stage_create_s"] > 0
             assert r["peak_device_bytes"] > 0 and len(r["candidates_ms"]) >= 1
-            assert 0 < r["elapsed_s"] <= 1.001 * d["ms_per_step"] * d["steps"] / 1e3
+            assert 0 < r["elapsed_s"] <= 1.01 * d["ms_per_step"] * d["steps"] / 1e3 + 1e-5
 
 
 def test_hbm_probe_shapes(gpu):

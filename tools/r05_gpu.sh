@@ -40,4 +40,20 @@ timeout -k 10 120 python3 -u tools/placement_r05.py --tries 6 --batch 64 >> $O/c
 cat $O/cand.jsonl
 }
 
-"step_$1"
+# the whole GPU suite + smoke
+step_full() {
+O=gpurun_out/r5full
+mkdir -p $O
+timeout -k 10 1000 python3 -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1; rc=$?
+tail -15 $O/pytest.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
+cat $O/smoke.log
+}
+
+# rocprof trace + PMC of the default bench line (tools/profile.sh)
+step_prof() {
+STEPS=200 bash tools/profile.sh ${1:-c2} ${2:-r05} || exit 1
+}
+
+"step_$@"
