@@ -63,7 +63,11 @@ def main():
         res["ring_allocation"] = r["placement"]["ring_allocation"]
         res["bench_kernel_avg_ms"] = r["kernel_avg_ms"]
         res["bench_frac"] = r["frac"]
-        res["bench_command"] = os.environ.get("BENCH_CMD", "")
+        cmd = os.path.join(d, "bench_cmd.txt")
+        res["bench_command"] = (open(cmd).read().strip() if os.path.exists(cmd) else
+                                "python3 bench.py --config %s --steps %s --warmup 5 "
+                                "--no-cpu-baseline --no-pyramid-only-line --no-hbm-probe"
+                                % (cfg, os.environ.get("STEPS", "200")))
         res["placement"] = {k: r["placement"].get(k) for k in
                             ("candidates_ms", "kept", "accepted", "expected_ms",
                              "probe_bus_gbs", "candidates_probe_gbs")}

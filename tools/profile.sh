@@ -14,6 +14,7 @@ EXTRA="--no-cpu-baseline --no-pyramid-only-line --no-hbm-probe"
 if [ "$3" = "pyr" ]; then NAME=$CFG-pyr; EXTRA="$EXTRA --pyramid-only"; fi
 OUT=gpurun_out/prof_${TAG}_${NAME}
 mkdir -p $OUT
+echo "python3 bench.py --config $CFG --steps $STEPS --warmup 5 $EXTRA" > $OUT/bench_cmd.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --config $CFG --steps $STEPS --warmup 5 $EXTRA > $OUT/bench_trace.log 2>&1 || exit 1
 tail -1 $OUT/bench_trace.log
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --config $CFG --steps 5 --warmup 2 $EXTRA > $OUT/bench_fetch.log 2>&1 || exit 2
