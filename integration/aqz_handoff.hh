@@ -116,6 +116,167 @@ struct HandoffSink
     virtual aqz_status unit(Unit& u) = 0;
 };
 
+// ---- shard routing of a level's units ---------------------------------------
+// What a level's zarr::Array does with a completed unit's chunks and frames,
+// independent of the reference library so that the binding (GpuArray,
+// integration/multiscale.array.gpu.cpp) and the GPU replay
+// (tests/native/handoff_replay.cpp) run the same routing code.
+
+// The index math the router needs (ArrayDimensions, array.dimensions.cpp:
+// 376-548): the reference's own in the binding, aqz_dims in the replay.
+struct ShardMap
+{
+    virtual ~ShardMap() = default;
+    virtual uint32_t chunks_in_memory() const = 0; // number_of_chunks_in_memory
+    virtual uint32_t number_of_shards() const = 0;
+    virtual uint32_t shard_index_for_chunk(uint32_t chunk) const = 0;
+    virtual uint32_t shard_internal_index(uint32_t chunk) const = 0;
+    virtual std::vector<uint32_t> skipped_internal_indices(uint32_t shard,
+                                                           uint32_t layer) const = 0;
+};
+
+// What the router asks of the array it routes for: the Shard::write_chunk /
+// skip_chunk jobs on the thread pool (Array::dispatch_chunk_job_ /
+// dispatch_skip_job_, array.cpp:624-760), should_rollover_ (array.cpp:
+// 924-937, asked after the unit's frames are counted) and rollover_ with
+// write_metadata_ (array.cpp:939-951, 213-216).
+struct ShardWriter
+{
+    static constexpr uint32_t kPadding = 0xffffffffu; // skip_chunk of ragged padding
+    virtual ~ShardWriter() = default;
+    // chunk: the chunk index (current layer * chunks in memory + slot)
+    virtual void write_chunk(uint32_t shard, uint32_t internal, uint32_t chunk,
+                             const uint8_t* bytes, size_t n, const Lease& lease) = 0;
+    // chunk: as above for a chunk without data, kPadding for ragged padding
+    virtual void skip_chunk(uint32_t shard, uint32_t internal, uint32_t chunk) = 0;
+    virtual bool should_rollover() = 0;
+    virtual void rollover() = 0;
+};
+
+class ShardRouter
+{
+  public:
+    explicit ShardRouter(const ShardMap& map)
+      : map_(map)
+    {
+    }
+
+    // The chunk layer inside the current append-dimension shard row
+    // (Array::current_layer_).
+    uint32_t current_layer() const { return current_layer_; }
+
+    // Every chunk of the unit to its shard: chunk index = current_layer *
+    // chunks_in_memory + the chunk's slot in the layer (compress_and_flush_
+    // data_ / compress_and_flush_band_, array.cpp:762-871); bytes go to
+    // write_chunk, a chunk without data to skip_chunk (the job's has_data
+    // test, array.cpp:713-720).  On a layer's last unit the ragged padding
+    // of every shard is skipped so each shard's countdown completes
+    // (array.cpp:771-790, 852-862).  A compressed unit's entries carry the
+    // device's (shard, internal) of each chunk: they must agree with the
+    // map, else INTERNAL_ERROR and nothing more of the unit is routed.
+    aqz_status route(const Unit& u, ShardWriter& w) const
+    {
+        const uint32_t n_mem = map_.chunks_in_memory();
+        const uint32_t offset = current_layer_ * n_mem;
+        for (uint32_t i = 0; i < u.n_chunks; ++i) {
+            uint32_t local;
+            const uint8_t* p;
+            size_t n;
+            if (u.entries) {
+                const aqz_chunk_entry& e = u.entries[i];
+                local = e.chunk;
+                p = u.data + e.offset;
+                n = e.nbytes;
+            } else {
+                local = u.c0 + i;
+                p = u.chunks + size_t(i) * u.bytes_per_chunk;
+                n = u.has_data[i] ? u.bytes_per_chunk : 0;
+            }
+            if (local >= n_mem)
+                return AQZ_STATUS_INTERNAL_ERROR;
+            const uint32_t chunk = offset + local;
+            const uint32_t shard = map_.shard_index_for_chunk(chunk);
+            const uint32_t internal = map_.shard_internal_index(chunk);
+            if (u.entries && (u.entries[i].shard != shard || u.entries[i].internal != internal))
+                return AQZ_STATUS_INTERNAL_ERROR;
+            if (n == 0)
+                w.skip_chunk(shard, internal, chunk);
+            else
+                w.write_chunk(shard, internal, chunk, p, n, u.lease);
+        }
+        if (u.last_in_layer)
+            for (uint32_t s = 0; s < map_.number_of_shards(); ++s)
+                for (const uint32_t idx : map_.skipped_internal_indices(s, current_layer_))
+                    w.skip_chunk(s, idx, ShardWriter::kPadding);
+        return AQZ_STATUS_SUCCESS;
+    }
+
+    // After the unit's frames were counted: a layer's last complete unit
+    // ends the layer -- rollover to a new append-dimension shard row when
+    // should_rollover_ says so, else the next layer (Array::write_frame's
+    // tail, array.cpp:209-219; compress_and_flush_data_, :799-803;
+    // flush_completed_bands_, :880-898).  The last, partial layer at close
+    // (complete = false) ends nothing.  Returns true on a rollover.
+    bool commit(const Unit& u, ShardWriter& w)
+    {
+        if (!(u.last_in_layer && u.complete))
+            return false;
+        if (w.should_rollover()) {
+            w.rollover();
+            current_layer_ = 0;
+            return true;
+        }
+        ++current_layer_;
+        return false;
+    }
+
+  private:
+    const ShardMap& map_;
+    uint32_t current_layer_ = 0;
+};
+
+// aqz_dims as the router's ShardMap (the replay; any caller without the
+// reference's ArrayDimensions).  Does not own d.
+class DimsShardMap final : public ShardMap
+{
+  public:
+    explicit DimsShardMap(const aqz_dims* d)
+      : d_(d)
+    {
+        (void)aqz_dims_shard_geometry(d_, nullptr, &n_shards_, &layers_per_shard_);
+    }
+    uint32_t chunks_in_memory() const override
+    {
+        return aqz_dims_number_of_chunks_in_memory(d_);
+    }
+    uint32_t number_of_shards() const override { return n_shards_; }
+    uint32_t layers_per_shard() const { return layers_per_shard_; }
+    uint32_t shard_index_for_chunk(uint32_t c) const override
+    {
+        return aqz_dims_shard_index_for_chunk(d_, c);
+    }
+    uint32_t shard_internal_index(uint32_t c) const override
+    {
+        return aqz_dims_shard_internal_index(d_, c);
+    }
+    std::vector<uint32_t> skipped_internal_indices(uint32_t shard,
+                                                   uint32_t layer) const override
+    {
+        size_t n = 0;
+        if (aqz_dims_skipped_internal_indices(d_, shard, layer, nullptr, 0, &n) !=
+              AQZ_STATUS_SUCCESS ||
+            n == 0)
+            return {};
+        std::vector<uint32_t> v(n);
+        (void)aqz_dims_skipped_internal_indices(d_, shard, layer, v.data(), n, &n);
+        return v;
+    }
+
+  private:
+    const aqz_dims* d_;
+    uint32_t n_shards_ = 1, layers_per_shard_ = 1;
+};
+
 struct HandoffOptions
 {
     uint32_t batch_frames = 64; // frames per append

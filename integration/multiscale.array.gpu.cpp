@@ -63,57 +63,67 @@ aqz_codec_for(const std::optional<CompressionParams>& params)
     return c;
 }
 
-class GpuArray final : public Array
+// The reference's ArrayDimensions as the router's ShardMap.
+class RefShardMap final : public aqz_binding::ShardMap
 {
   public:
-    using Array::Array;
+    explicit RefShardMap(std::shared_ptr<ArrayDimensions> dims)
+      : dims_(std::move(dims))
+    {
+    }
+    uint32_t chunks_in_memory() const override { return dims_->number_of_chunks_in_memory(); }
+    uint32_t number_of_shards() const override { return dims_->number_of_shards(); }
+    uint32_t shard_index_for_chunk(uint32_t c) const override
+    {
+        return dims_->shard_index_for_chunk(c);
+    }
+    uint32_t shard_internal_index(uint32_t c) const override
+    {
+        return dims_->shard_internal_index(c);
+    }
+    std::vector<uint32_t> skipped_internal_indices(uint32_t shard,
+                                                   uint32_t layer) const override
+    {
+        return dims_->skipped_internal_indices_for_shard_layer(shard, layer);
+    }
 
-    // Every chunk of a handed-off unit to its shard: the chunk job of
-    // Array::dispatch_chunk_job_ (array.cpp:664-760) with the bytes already
-    // made -- raw when no codec is configured, else the device's frame -- and
-    // Shard::skip_chunk for a chunk without data (array.cpp:713-720).  On the
-    // layer's last unit the ragged-padding slots of every shard are skipped
-    // (array.cpp:771-790, 852-862) so each shard's countdown completes.
-    void write_unit(const aqz_binding::Unit& u)
+  private:
+    std::shared_ptr<ArrayDimensions> dims_;
+};
+
+class GpuArray final
+  : public Array
+  , private aqz_binding::ShardWriter
+{
+  public:
+    GpuArray(std::shared_ptr<ArrayConfig> config,
+             std::shared_ptr<ThreadPool> thread_pool,
+             std::shared_ptr<FileHandlePool> file_handle_pool,
+             std::shared_ptr<S3ConnectionPool> s3_connection_pool)
+      : Array(config, thread_pool, file_handle_pool, s3_connection_pool)
+      , map_(config_->dimensions)
+      , router_(map_)
+    {
+    }
+
+    // Every chunk of a handed-off unit to its shard through the shared
+    // router (aqz_handoff.hh ShardRouter::route: the chunk jobs of
+    // Array::dispatch_chunk_job_, array.cpp:664-760, with the bytes already
+    // made -- raw when no codec is configured, else the device's frame --
+    // Shard::skip_chunk for a chunk without data, and the ragged-padding
+    // skips on a layer's last unit, array.cpp:771-790, 852-862).
+    aqz_status write_unit(const aqz_binding::Unit& u)
     {
         if (data_paths_.empty())
             make_shards_();
-        const auto& dims = config_->dimensions;
-        const uint32_t chunk_offset = current_layer_ * dims->number_of_chunks_in_memory();
-        for (uint32_t i = 0; i < u.n_chunks; ++i) {
-            uint32_t local;
-            const uint8_t* p;
-            size_t n;
-            if (u.entries) {
-                const aqz_chunk_entry& e = u.entries[i];
-                local = e.chunk;
-                p = u.data + e.offset;
-                n = e.nbytes;
-            } else {
-                local = u.c0 + i;
-                p = u.chunks + size_t(i) * u.bytes_per_chunk;
-                n = u.has_data[i] ? u.bytes_per_chunk : 0;
-            }
-            const uint32_t chunk_idx = chunk_offset + local;
-            const uint32_t shard_idx = dims->shard_index_for_chunk(chunk_idx);
-            const uint32_t internal_idx = dims->shard_internal_index(chunk_idx);
-            if (n == 0)
-                dispatch_skip_job_(shards_[shard_idx], internal_idx, shard_idx);
-            else
-                dispatch_bytes_job_(shards_[shard_idx], chunk_idx, internal_idx, shard_idx, p,
-                                    n, u.lease);
-        }
-        if (u.last_in_layer)
-            for (uint32_t s = 0; s < dims->number_of_shards(); ++s)
-                for (const auto& idx :
-                     dims->skipped_internal_indices_for_shard_layer(s, current_layer_))
-                    dispatch_skip_job_(shards_[s], idx, s);
+        return router_.route(u, *this);
     }
 
     // `frames` more frames are in the shards: the tail of Array::write_frame
-    // (array.cpp:196-219) with the layer advance of compress_and_flush_data_
-    // (:799-803) / flush_completed_bands_ (:888-898).  The last, partial
-    // layer at close is already written, so close_ has nothing to flush.
+    // (array.cpp:196-219), then the router's layer advance or rollover
+    // (ShardRouter::commit: compress_and_flush_data_ :799-803,
+    // flush_completed_bands_ :880-898).  The last, partial layer at close
+    // is already written, so close_ has nothing to flush.
     WriteResult commit_unit(const aqz_binding::Unit& u)
     {
         const uint64_t nbytes = u.frames * bytes_per_frame_;
@@ -124,19 +134,32 @@ class GpuArray final : public Array
         total_bytes_written_ += nbytes;
         bytes_to_flush_ = 0;
         flushed_band_count_ = u.last_in_layer ? 0 : u.band + 1;
-        if (u.last_in_layer && u.complete) {
-            if (should_rollover_()) {
-                rollover_();
-                CHECK(write_metadata_());
-                current_layer_ = 0;
-            } else {
-                ++current_layer_;
-            }
-        }
+        router_.commit(u, *this);
+        current_layer_ = router_.current_layer();
         return WriteResult::Ok;
     }
 
   private:
+    // aqz_binding::ShardWriter: the reference's own jobs and rollover
+    void write_chunk(uint32_t shard, uint32_t internal, uint32_t chunk, const uint8_t* bytes,
+                     size_t n, const aqz_binding::Lease& lease) override
+    {
+        dispatch_bytes_job_(shards_[shard], chunk, internal, shard, bytes, n, lease);
+    }
+    void skip_chunk(uint32_t shard, uint32_t internal, uint32_t) override
+    {
+        dispatch_skip_job_(shards_[shard], internal, shard);
+    }
+    bool should_rollover() override { return should_rollover_(); }
+    void rollover() override
+    {
+        rollover_();
+        CHECK(write_metadata_());
+    }
+
+    RefShardMap map_;
+    aqz_binding::ShardRouter router_;
+
     void dispatch_bytes_job_(std::shared_ptr<Shard> shard,
                              uint32_t chunk_idx,
                              uint32_t internal_idx,
@@ -332,7 +355,11 @@ class GpuMultiscaleArray final
     aqz_status unit(aqz_binding::Unit& u) override
     {
         try {
-            gpu_arrays_[u.level]->write_unit(u);
+            const aqz_status s = gpu_arrays_[u.level]->write_unit(u);
+            if (s != AQZ_STATUS_SUCCESS) {
+                LOG_ERROR("A GPU chunk unit disagrees with the level's shard map");
+                return s;
+            }
             return gpu_arrays_[u.level]->commit_unit(u) == WriteResult::Ok
                      ? AQZ_STATUS_SUCCESS
                      : AQZ_STATUS_WRITE_OUT_OF_BOUNDS;

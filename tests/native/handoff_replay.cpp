@@ -19,13 +19,18 @@
 //   many stages, z slab r of every stack each, assembled by
 //   aqz_stage_import_frames), u64 n_frames,
 //   u64 frame_bytes, [n_frames frames].
-// OUT: "AQZ3", u32 n_levels, then per level {u64 n, n x {u64 layer,
-//   u32 chunk, u32 shard, u32 internal, u64 nbytes, nbytes bytes}}: every
-//   chunk the sink received (nbytes 0: skipped, no data).
+// OUT: "AQZ4", u32 n_levels, then per level {u64 n, n x {u64 layer,
+//   u32 chunk (0xffffffff: a shard's ragged padding), u32 append-shard row,
+//   u32 shard, u32 internal, u64 nbytes, nbytes bytes}, u64 n_rollovers,
+//   n_rollovers x u64 frames committed at the rollover}: every chunk the
+//   router handed to the recording writer (nbytes 0: skipped, no data).
+// Every unit runs through aqz_binding::ShardRouter (integration/
+// aqz_handoff.hh), the code GpuArray runs, over aqz_dims.
 // stdout: one JSON line per unit and a final summary; exit 0 only if every
 // check held: units contiguous in frame order per level, only a level's
-// last layer incomplete, every frame committed, every chunk's shard and
-// internal index equal to ArrayDimensions' (aqz_dims_*).
+// last layer incomplete, every frame committed, the router's layer the
+// unit's layer inside its shard row, every compressed entry's shard and
+// internal index equal to the map's.
 #include "aqz_gpu.h"
 #include "aqz_handoff.hh"
 
@@ -109,29 +114,77 @@ class Pool
     bool stop_ = false;
 };
 
+constexpr uint32_t kPadding = 0xffffffffu; // Record::chunk of a ragged-padding skip
+
 struct Record
 {
     uint64_t layer;
-    uint32_t chunk, shard, internal;
+    uint32_t chunk, append, shard, internal;
     std::vector<uint8_t> bytes;
 };
 
-struct LevelState
+// One level: the shipped router (aqz_binding::ShardRouter, what GpuArray
+// runs) over aqz_dims, writing into a recorder in place of the shards.
+struct LevelState final : aqz_binding::ShardWriter
 {
     uint64_t F = 0, bpc = 0, committed = 0;
-    uint32_t n_chunks = 0, layers_per_shard = 1;
+    uint32_t n_chunks = 0;
     bool incomplete_seen = false;
     uint64_t incomplete_layer = 0;
     aqz_dims* dims = nullptr;
+    std::unique_ptr<aqz_binding::DimsShardMap> map;
+    std::unique_ptr<aqz_binding::ShardRouter> router;
+    uint32_t append = 0;   // append-dimension shard rows rolled over so far
+    uint64_t layer = 0;    // the unit being routed
+    std::vector<uint64_t> rollovers; // frames committed at each rollover
+    Pool* pool = nullptr;
+    bool record = true;
+    std::atomic<uint64_t>* chunk_bytes = nullptr;
     std::mutex mu;
     std::vector<Record> rec;
+
+    // GpuArray::dispatch_bytes_job_: the copy out of the pinned buffer on a
+    // pool thread that holds the lease
+    void write_chunk(uint32_t shard, uint32_t internal, uint32_t chunk, const uint8_t* p,
+                     size_t n, const aqz_binding::Lease& lease) override
+    {
+        *chunk_bytes += n;
+        pool->push([this, ly = layer, local = chunk % n_chunks, a = append, shard, internal,
+                    p, n, lease = aqz_binding::Lease(lease)]() mutable {
+            std::vector<uint8_t> v(p, p + n);
+            lease.release();
+            if (record) {
+                std::lock_guard<std::mutex> lk(mu);
+                rec.push_back(Record{ ly, local, a, shard, internal, std::move(v) });
+            }
+        });
+    }
+    void skip_chunk(uint32_t shard, uint32_t internal, uint32_t chunk) override
+    {
+        if (!record)
+            return;
+        std::lock_guard<std::mutex> lk(mu);
+        rec.push_back(Record{ layer, chunk == kPadding ? kPadding : chunk % n_chunks, append,
+                              shard, internal, {} });
+    }
+    // Array::should_rollover_ (array.cpp:924-937): frames written a
+    // multiple of append chunk x append shard x the intermediate extents =
+    // frames per chunk layer x chunk layers per shard
+    bool should_rollover() override
+    {
+        return committed % (F * map->layers_per_shard()) == 0;
+    }
+    void rollover() override
+    {
+        rollovers.push_back(committed);
+        ++append;
+    }
 };
 
 struct RecordingSink final : aqz_binding::HandoffSink
 {
     std::vector<std::unique_ptr<LevelState>> lv;
-    Pool* pool = nullptr;
-    bool record = true, quiet = false;
+    bool quiet = false;
     std::atomic<bool> ok{ true };
     std::atomic<uint64_t> units{ 0 }, chunk_bytes{ 0 };
 
@@ -150,53 +203,26 @@ struct RecordingSink final : aqz_binding::HandoffSink
         }
         if (u.frames ? L.committed != u.first : (u.complete || u.first < L.committed))
             ok = false;
+        // the router's layer is the unit's layer inside its shard row
+        if (L.router->current_layer() != u.layer % L.map->layers_per_shard())
+            ok = false;
         if (!quiet)
             printf("{\"level\": %u, \"layer\": %llu, \"band\": %u, \"first\": %llu, "
                    "\"frames\": %llu, \"complete\": %s, \"compressed\": %s}\n",
                    u.level, (unsigned long long)u.layer, u.band,
                    (unsigned long long)L.committed, (unsigned long long)u.frames,
                    u.complete ? "true" : "false", u.entries ? "true" : "false");
-        L.committed += u.frames;
         ++units;
-        const uint32_t chunk_offset = uint32_t(u.layer % L.layers_per_shard) * L.n_chunks;
-        for (uint32_t i = 0; i < u.n_chunks; ++i) {
-            uint32_t local, shard, internal;
-            const uint8_t* p;
-            size_t n;
-            const uint32_t cidx0 = chunk_offset + (u.entries ? u.entries[i].chunk : u.c0 + i);
-            const uint32_t ref_shard = aqz_dims_shard_index_for_chunk(L.dims, cidx0);
-            const uint32_t ref_internal = aqz_dims_shard_internal_index(L.dims, cidx0);
-            if (u.entries) {
-                const aqz_chunk_entry& e = u.entries[i];
-                local = e.chunk;
-                shard = e.shard;
-                internal = e.internal;
-                p = u.data + e.offset;
-                n = e.nbytes;
-                if (shard != ref_shard || internal != ref_internal)
-                    ok = false;
-            } else {
-                local = u.c0 + i;
-                shard = ref_shard;
-                internal = ref_internal;
-                p = u.chunks + size_t(i) * u.bytes_per_chunk;
-                n = u.has_data[i] ? u.bytes_per_chunk : 0;
-            }
-            if (local >= L.n_chunks)
-                ok = false;
-            chunk_bytes += n;
-            // GpuArray::dispatch_bytes_job_: the copy out of the pinned buffer
-            // on a pool thread that holds the lease
-            pool->push([this, &L, layer = u.layer, local, shard, internal, p, n,
-                        lease = u.lease]() mutable {
-                std::vector<uint8_t> v(p, p + n);
-                lease.release();
-                if (record) {
-                    std::lock_guard<std::mutex> lk(L.mu);
-                    L.rec.push_back(Record{ layer, local, shard, internal, std::move(v) });
-                }
-            });
+        L.layer = u.layer;
+        const aqz_status s = L.router->route(u, L);
+        if (s != AQZ_STATUS_SUCCESS) {
+            ok = false;
+            return s;
         }
+        // GpuArray::commit_unit: the frames are counted, then the layer
+        // advance or rollover
+        L.committed += u.frames;
+        L.router->commit(u, L);
         return AQZ_STATUS_SUCCESS;
     }
 };
@@ -338,10 +364,8 @@ main(int argc, char** argv)
     }
     const uint32_t nl = aqz_stage_n_levels(st);
     RecordingSink sink;
-    sink.record = record;
     sink.quiet = !record;
     Pool pool(pool_threads);
-    sink.pool = &pool;
     for (uint32_t l = 0; l < nl; ++l) {
         auto L = std::make_unique<LevelState>();
         aqz_level_layout lay{};
@@ -349,12 +373,16 @@ main(int argc, char** argv)
         L->F = lay.frames_per_layer;
         L->bpc = lay.bytes_per_chunk;
         L->n_chunks = lay.chunks_per_layer;
-        aqz_stage_shard_geometry(st, l, nullptr, nullptr, &L->layers_per_shard);
         std::vector<aqz_dimension> ld(16);
         size_t n = 0;
         aqz_stage_level_dims(st, l, ld.data(), ld.size(), &n);
         if (aqz_dims_create(ld.data(), n, dtype, nullptr, &L->dims) != AQZ_STATUS_SUCCESS)
             return 1;
+        L->map = std::make_unique<aqz_binding::DimsShardMap>(L->dims);
+        L->router = std::make_unique<aqz_binding::ShardRouter>(*L->map);
+        L->pool = &pool;
+        L->record = record;
+        L->chunk_bytes = &sink.chunk_bytes;
         sink.lv.push_back(std::move(L));
     }
     int rc = 0;
@@ -413,7 +441,7 @@ main(int argc, char** argv)
     FILE* o = fopen(argv[2], "wb");
     if (!o)
         return 2;
-    fwrite("AQZ3", 1, 4, o);
+    fwrite("AQZ4", 1, 4, o);
     fwrite(&nl, 4, 1, o);
     for (auto& L : sink.lv) {
         const uint64_t n = L->rec.size();
@@ -422,11 +450,15 @@ main(int argc, char** argv)
             const uint64_t nb = r.bytes.size();
             fwrite(&r.layer, 8, 1, o);
             fwrite(&r.chunk, 4, 1, o);
+            fwrite(&r.append, 4, 1, o);
             fwrite(&r.shard, 4, 1, o);
             fwrite(&r.internal, 4, 1, o);
             fwrite(&nb, 8, 1, o);
             fwrite(r.bytes.data(), 1, nb, o);
         }
+        const uint64_t nr = L->rollovers.size();
+        fwrite(&nr, 8, 1, o);
+        fwrite(L->rollovers.data(), 8, nr, o);
     }
     fclose(o);
     return rc;

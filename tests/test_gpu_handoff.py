@@ -168,7 +168,10 @@ def test_stage_append_cuda_tensor_from_side_stream(gpu):
     st.close()
 
 
-REPLAY = None
+class Replay:
+    def __init__(self, log, summary, got, padding, rollovers):
+        self.log, self.summary, self.got = log, summary, got
+        self.padding, self.rollovers = padding, rollovers
 
 
 def _run_replay(tmp_path, dims, dtype, method, frames, batch, slots, codec=(0, 0, 0),
@@ -176,9 +179,12 @@ def _run_replay(tmp_path, dims, dtype, method, frames, batch, slots, codec=(0, 0
                 placement_tries=0, record=True, z_slabs=1):
     """tests/native/handoff_replay: the binding's hand-off
     (integration/aqz_handoff.hh, what GpuMultiscaleArray runs) over the C
-    ABI with a recording sink that does GpuArray::write_unit's per-chunk
-    copy on a thread pool.  Returns (unit log, summary, {(level, layer,
-    chunk): (shard, internal, bytes)})."""
+    ABI; every unit goes through the shipped ShardRouter (what GpuArray
+    runs) into a recording ShardWriter that does GpuArray's per-chunk copy
+    on a thread pool.  Returns a Replay: the unit log, the summary, got =
+    {(level, layer, chunk): (shard, internal, bytes, append-shard row)}, the
+    ragged-padding skips [(level, layer, row, shard, internal)] and each
+    level's rollover points (frames committed)."""
     import json
     import os
     import struct
@@ -204,22 +210,29 @@ def _run_replay(tmp_path, dims, dtype, method, frames, batch, slots, codec=(0, 0
     log = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     summary = log[-1]
     assert summary["summary"] and summary["ok"], summary
-    got = {}
+    got, padding, rollovers = {}, [], []
     if record:
         b = out.read_bytes()
-        assert b[:4] == b"AQZ3"
+        assert b[:4] == b"AQZ4"
         (nl,), o = struct.unpack_from("<I", b, 4), 8
         for l in range(nl):
             (nrec,) = struct.unpack_from("<Q", b, o)
             o += 8
             for _ in range(nrec):
-                layer, chunk, shard, internal, nb = struct.unpack_from("<QIIIQ", b, o)
-                o += 28
+                layer, chunk, append, shard, internal, nb = struct.unpack_from("<QIIIIQ", b, o)
+                o += 32
+                if chunk == 0xFFFFFFFF:  # ragged padding of a shard
+                    padding.append((l, layer, append, shard, internal))
+                    continue
                 key = (l, layer, chunk)
                 assert key not in got, f"chunk handed to its shard twice: {key}"
-                got[key] = (shard, internal, b[o:o + nb])
+                got[key] = (shard, internal, b[o:o + nb], append)
                 o += nb
-    return log[:-1], summary, got
+            (nr,) = struct.unpack_from("<Q", b, o)
+            o += 8
+            rollovers.append(list(struct.unpack_from(f"<{nr}Q", b, o)))
+            o += 8 * nr
+    return Replay(log[:-1], summary, got, padding, rollovers)
 
 
 def _decode(codec, frame, bpc):
@@ -237,10 +250,12 @@ def _decode(codec, frame, bpc):
     return zstd_decode(frame, bpc)
 
 
-def _check_replay(exp, fw, log, got, codec, bpc_of):
+def _check_replay(exp, fw, r, codec, st):
     """Every chunk of every oracle layer reached its shard exactly once:
     skipped iff the oracle's has_data is false, else bytes that decode to
-    the oracle's chunk; units contiguous and in frame order per level."""
+    the oracle's chunk; units contiguous and in frame order per level; and
+    the shard routing is the reference's (_check_routing)."""
+    log, got = r.log, r.got
     per = {}
     for e in log:
         prev = per.setdefault(e["level"], [])
@@ -252,12 +267,12 @@ def _check_replay(exp, fw, log, got, codec, bpc_of):
         assert not first_open or all(not u["complete"] for u in units[first_open[0]:])
     seen = set()
     for (l, layer), (buf, flags) in exp.items():
-        bpc = bpc_of[l]
+        bpc = st.layout(l)["bytes_per_chunk"]
         for c in range(len(flags)):
             key = (l, layer, c)
             assert key in got, f"chunk never reached its shard: {key}"
             seen.add(key)
-            _, _, data = got[key]
+            _, _, data, _ = got[key]
             if not flags[c]:
                 assert len(data) == 0, f"{key}: a chunk without data must be skipped"
                 continue
@@ -265,12 +280,58 @@ def _check_replay(exp, fw, log, got, codec, bpc_of):
             dec = _decode(codec[0], data, bpc)
             assert dec == buf[c * bpc:(c + 1) * bpc].tobytes(), f"{key}: decoded bytes differ"
     assert seen == set(got), sorted(set(got) - seen)[:5]
+    _check_routing(r, fw, st)
+
+
+def _check_routing(r, fw, st):
+    """The shipped ShardRouter's routing against the reference's rules, per
+    level: a chunk of layer k goes to append-shard row k // layers_per_shard
+    at (shard_index_for_chunk, shard_internal_index) of chunk index
+    (k mod layers_per_shard) * chunks_in_memory + slot (the compiled
+    reference's ArrayDimensions when oracle/_ref is built,
+    array.dimensions.cpp:393-548; compress_and_flush_data_, array.cpp:
+    762-811); rollovers fall exactly where should_rollover_ says (every
+    frames_per_layer * layers_per_shard committed frames, array.cpp:924-951);
+    and in every completed row each shard's internal indices are written or
+    skipped exactly once -- chunks, chunks without data and the ragged
+    padding together (skipped_internal_indices_for_shard_layer,
+    array.dimensions.cpp:424-453) -- so every shard's countdown completes."""
+    import aqz
+    from oracle_bindings import OracleDims, ref_available
+    for l in range(st.n_levels()):
+        ld = st.level_dims(l)
+        ref = OracleDims(ld, U16, use_ref=ref_available())
+        cps, ns, lps = aqz.Dims(ld, U16).shard_geometry()
+        n_mem = ref.number_of_chunks_in_memory()
+        F = ref.frames_per_chunk_layer()
+        done_layers = fw[l] // F
+        assert r.rollovers[l] == [k * F * lps for k in range(1, done_layers // lps + 1)], l
+        rows = {}
+        for (lv, layer, chunk), (shard, internal, _, append) in r.got.items():
+            if lv != l:
+                continue
+            assert append == layer // lps, (l, layer, chunk, append)
+            c = (layer % lps) * n_mem + chunk
+            assert (shard, internal) == (ref.shard_index_for_chunk(c),
+                                         ref.shard_internal_index(c)), (l, layer, chunk)
+            rows.setdefault((append, shard), []).append(internal)
+        for (lv, layer, append, shard, internal) in r.padding:
+            if lv == l:  # complete layers, and the partial last one at close
+                assert append == layer // lps and layer <= done_layers, (l, layer)
+                rows.setdefault((append, shard), []).append(internal)
+        for a in range(done_layers // lps):
+            for s_ in range(ns):
+                assert sorted(rows.get((a, s_), [])) == list(range(cps)), (l, a, s_)
 
 
 REPLAY_CASES = {
     # dim-1 bands: 3-D, chunk 1 on the append dim, z chunk 16 of 64
     "banded-3d": ([(TIME, 0, 1, 1), (SPACE, 64, 16, 1), (SPACE, 256, 64, 1),
                    (SPACE, 256, 64, 1)], 2 * 64 + 24, 8),
+    # append shards of 2 layers over 5 layers (two rollovers), banded, ragged
+    # 3-chunk x and 5-chunk y in 2x2 shards (padding in the edge shards)
+    "banded-rollover": ([(TIME, 0, 1, 2), (SPACE, 48, 16, 1), (SPACE, 300, 64, 2),
+                         (SPACE, 192, 64, 2)], 5 * 48 + 10, 8),
     # ragged dim 1 (48 planes, 32-plane chunks): the trailing band holds 16
     # frames and is complete with its layer (array.cpp:884-886)
     "banded-ragged": ([(TIME, 0, 1, 1), (SPACE, 48, 32, 1), (SPACE, 256, 64, 2),
@@ -309,15 +370,13 @@ def test_binding_handoff_replay(gpu, tmp_path, case, codec):
         frames &= 0x00ff
         frames[5:9] = 0
     exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
-    log, summary, got = _run_replay(tmp_path, dims, U16, MEAN, frames, batch, 2,
-                                    codec=CODECS[codec])
+    r = _run_replay(tmp_path, dims, U16, MEAN, frames, batch, 2, codec=CODECS[codec])
     st = gpu.Stage(dims, U16, MEAN)
-    bpc = [st.layout(l)["bytes_per_chunk"] for l in range(st.n_levels())]
-    st.close()
     if case.startswith("banded") and not CODECS[codec][0]:
-        assert len([e for e in log if e["level"] == 0]) > len(
+        assert len([e for e in r.log if e["level"] == 0]) > len(
             {k[1] for k in exp if k[0] == 0})  # bands, not layers
-    _check_replay(exp, fw, log, got, CODECS[codec], bpc)
+    _check_replay(exp, fw, r, CODECS[codec], st)
+    st.close()
 
 
 @pytest.mark.parametrize("codec", ["lz4-shuffle", "zstd-1", "raw"])
@@ -334,12 +393,11 @@ def test_binding_handoff_replay_host_slots(gpu, tmp_path, codec, slots):
     dims, n, batch = REPLAY_CASES["layers-2d-ragged"]
     frames = synthetic_frames(U16, n, dims[-2][1], dims[-1][1], 7 * slots) & 0x0fff
     exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
-    log, summary, got = _run_replay(tmp_path, dims, U16, MEAN, frames, batch, slots,
-                                    codec=CODECS[codec], pool_threads=3)
+    r = _run_replay(tmp_path, dims, U16, MEAN, frames, batch, slots, codec=CODECS[codec],
+                    pool_threads=3)
     st = gpu.Stage(dims, U16, MEAN)
-    bpc = [st.layout(l)["bytes_per_chunk"] for l in range(st.n_levels())]
+    _check_replay(exp, fw, r, CODECS[codec], st)
     st.close()
-    _check_replay(exp, fw, log, got, CODECS[codec], bpc)
 
 
 @pytest.mark.parametrize("codec", ["raw", "lz4-shuffle", "zstd-1"])
@@ -362,9 +420,8 @@ def test_binding_z_slabs(gpu, tmp_path, codec, slabs, tail):
     frames = synthetic_frames(U16, n, 256, 256, 71 + slabs + tail) & 0x0fff
     frames[70:75] = 0
     exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
-    log, summary, got = _run_replay(tmp_path, dims, U16, MEAN, frames, 8, 3,
-                                    codec=CODECS[codec], z_slabs=slabs)
+    r = _run_replay(tmp_path, dims, U16, MEAN, frames, 8, 3, codec=CODECS[codec],
+                    z_slabs=slabs)
     st = gpu.Stage(dims, U16, MEAN)
-    bpc = [st.layout(l)["bytes_per_chunk"] for l in range(st.n_levels())]
+    _check_replay(exp, fw, r, CODECS[codec], st)
     st.close()
-    _check_replay(exp, fw, log, got, CODECS[codec], bpc)

@@ -56,4 +56,13 @@ step_prof() {
 STEPS=200 bash tools/profile.sh ${1:-c2} ${2:-r05} || exit 1
 }
 
+# some GPU test files (names after the step)
+step_tests() {
+O=gpurun_out/r5t
+mkdir -p $O
+timeout -k 10 900 python3 -u -m pytest "$@" -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1; rc=$?
+tail -25 $O/pytest.log
+[ $rc -eq 0 ] || exit 1
+}
+
 "step_$@"
