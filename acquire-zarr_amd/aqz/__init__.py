@@ -441,6 +441,18 @@ def estimate_memory(dims, dtype, method, max_levels=0, layer_slots=0,
     return {"device_bytes": m.device_bytes, "pinned_bytes": m.pinned_bytes}
 
 
+def compressor_max_bytes(chunk_bytes, n_chunks):
+    """aqz_compressor_max_bytes: bytes that always hold the frames of
+    n_chunks chunks of chunk_bytes (any codec; no GPU)."""
+    return lib().aqz_compressor_max_bytes(chunk_bytes, n_chunks)
+
+
+def compressor_scratch_bytes(codec, chunk_bytes, typesize, n_chunks):
+    """aqz_compressor_scratch_bytes for codec = (codec, clevel, shuffle)."""
+    c = CompressionC(*codec)
+    return lib().aqz_compressor_scratch_bytes(C.byref(c), chunk_bytes, typesize, n_chunks)
+
+
 def pyramid_levels(dims, max_levels=0):
     """Level dims per Downsampler::make_writer_configurations_ (no GPU)."""
     d = _dims_c(dims)

@@ -359,6 +359,105 @@ slabs_from_env()
     return n > 1 ? uint32_t(n) : 1u;
 }
 
+// The drop-in's own memory for one multiscale array on the GPU path, beyond
+// what ZarrStreamSettings_estimate_max_memory_usage counts for it
+// (acquire.zarr.cpp:216-314: the frame queue and the array's frame buffer
+// stay the reference's).  An upper bound, with no GPU needed:
+//   host   -- the hand-off's pinned buffers (Handoff::host_bytes: a batch
+//             double buffer per stage, host_slots unit buffers per level at
+//             the codec's capacity with their has_data bytes), every
+//             stage's pinned memory (aqz_stage_estimate_memory) and, per
+//             compressed level and ring slot, the read-back of the frame
+//             offsets (and with AQZ_ZSTD_HOST the shuffled layer);
+//   device -- every stage's aqz_stage_estimate_memory (creation-time
+//             placement peak included), and per compressed level and ring
+//             slot the frames (aqz_compressor_max_bytes) and offsets, plus
+//             the codec's scratch (aqz_compressor_scratch_bytes).
+struct MemoryEstimate
+{
+    uint64_t host_bytes = 0, device_bytes = 0;
+};
+
+inline aqz_status
+estimate_memory(const aqz_array_desc& desc, const aqz_stage_options& opt,
+                const HandoffOptions& o, uint32_t n_stages, MemoryEstimate* out)
+{
+    if (!out || n_stages == 0)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    *out = MemoryEstimate{};
+    aqz_memory_usage st{};
+    aqz_status s = aqz_stage_estimate_memory(&desc, &opt, &st);
+    if (s != AQZ_STATUS_SUCCESS)
+        return s;
+    // the levels' storage-order dims, as the stage makes them
+    aqz_dims* base = nullptr;
+    s = aqz_dims_create(desc.dimensions, desc.dimension_count, desc.data_type,
+                        desc.storage_dimension_order, &base);
+    if (s != AQZ_STATUS_SUCCESS)
+        return s;
+    std::vector<aqz_dimension> d0(aqz_dims_ndims(base));
+    for (size_t i = 0; i < d0.size(); ++i)
+        (void)aqz_dims_get(base, i, &d0[i]);
+    aqz_dims_destroy(base);
+    uint32_t nl = 0;
+    s = aqz_pyramid_levels(d0.data(), d0.size(), desc.max_levels, &nl, nullptr, 0);
+    std::vector<aqz_dimension> lv(size_t(nl) * d0.size());
+    if (s == AQZ_STATUS_SUCCESS)
+        s = aqz_pyramid_levels(d0.data(), d0.size(), desc.max_levels, &nl, lv.data(),
+                               lv.size());
+    if (s != AQZ_STATUS_SUCCESS)
+        return s;
+    const size_t nd = d0.size();
+    static const size_t bpp_of[] = { 1, 2, 4, 8, 1, 2, 4, 8, 4, 8 };
+    const size_t bpp = desc.data_type >= 0 && desc.data_type < 10 ? bpp_of[desc.data_type] : 8;
+    const uint64_t fb = uint64_t(d0[nd - 1].array_size_px) * d0[nd - 2].array_size_px * bpp;
+    const uint32_t batch = std::max<uint32_t>(1, o.batch_frames);
+    const uint32_t B = opt.max_batch_frames ? opt.max_batch_frames : 64;
+    const uint32_t slots = std::max<uint32_t>(1, o.host_slots);
+    const bool compressed = o.comp.codec != AQZ_CODEC_NONE;
+    const char* hz = std::getenv("AQZ_ZSTD_HOST");
+    const bool host_zstd = hz && std::atoi(hz) != 0 &&
+                           (o.comp.codec == AQZ_CODEC_BLOSC_ZSTD || o.comp.codec == AQZ_CODEC_ZSTD);
+    uint64_t host = uint64_t(n_stages) * (2 * uint64_t(batch) * fb + st.pinned_bytes);
+    uint64_t dev = uint64_t(n_stages) * st.device_bytes;
+    for (uint32_t l = 0; l < nl; ++l) {
+        aqz_dims* d = nullptr;
+        s = aqz_dims_create(&lv[size_t(l) * nd], nd, desc.data_type, nullptr, &d);
+        if (s != AQZ_STATUS_SUCCESS)
+            return s;
+        const uint64_t bpc = aqz_dims_bytes_per_chunk(d);
+        const uint32_t n_chunks = aqz_dims_number_of_chunks_in_memory(d);
+        const uint64_t F = std::max<uint64_t>(1, aqz_dims_frames_per_chunk_layer(d));
+        int32_t banded = 0;
+        uint32_t n_bands = 1, per_band = n_chunks;
+        uint64_t fpb = 0;
+        (void)aqz_dims_dim1_banding(d, &banded, &n_bands, &fpb, &per_band);
+        aqz_dims_destroy(d);
+        if (compressed || !banded)
+            per_band = n_chunks;
+        const uint64_t cap =
+          compressed ? aqz_compressor_max_bytes(bpc, n_chunks) : bpc * per_band;
+        host += uint64_t(slots) * (cap + per_band);
+        if (!compressed)
+            continue;
+        const uint64_t ring_slots =
+          std::max<uint64_t>(opt.layer_slots ? opt.layer_slots : 2, (B - 1 + F - 1) / F + 1);
+        const uint64_t offs = (uint64_t(n_chunks) + 1) * 8;
+        uint64_t ldev = ring_slots * (aqz_compressor_max_bytes(bpc, n_chunks) + offs) +
+                        aqz_compressor_scratch_bytes(&o.comp, bpc, uint32_t(bpp), n_chunks);
+        uint64_t lhost = ring_slots * offs;
+        if (host_zstd) {
+            ldev += bpc * n_chunks; // the shuffled layer
+            lhost += ring_slots * (bpc * n_chunks + n_chunks);
+        }
+        dev += uint64_t(n_stages) * ldev;
+        host += uint64_t(n_stages) * lhost;
+    }
+    out->host_bytes = host;
+    out->device_bytes = dev;
+    return AQZ_STATUS_SUCCESS;
+}
+
 class Handoff
 {
   public:

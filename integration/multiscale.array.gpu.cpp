@@ -38,7 +38,9 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <memory>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -300,6 +302,10 @@ class GpuMultiscaleArray final
             aqz_stage_destroy(st);
     }
 
+    // Host memory, as ZarrStream_get_current_memory_usage sums it
+    // (zarr.stream.cpp:1057-1068): the base array's plus the stages' pinned
+    // memory and the hand-off's pinned buffers.  Device memory is not host
+    // memory: it is reported by device_memory_usage() instead.
     size_t memory_usage() const noexcept override
     {
         size_t pinned = 0;
@@ -309,6 +315,20 @@ class GpuMultiscaleArray final
             pinned += m.pinned_bytes;
         }
         return MultiscaleArray::memory_usage() + pinned + handoff_->host_bytes();
+    }
+
+    // Sidecar (not part of the reference's interface): HBM the stages hold
+    // (aqz_stage_memory_usage), for a caller that reports device memory
+    // next to the host figure.
+    size_t device_memory_usage() const noexcept
+    {
+        size_t dev = 0;
+        for (aqz_stage* st : stages_) {
+            aqz_memory_usage m{};
+            (void)aqz_stage_memory_usage(st, &m);
+            dev += m.device_bytes;
+        }
+        return dev;
     }
 
     // MultiscaleArray::write_frame (multiscale.array.cpp:57-74) with the
@@ -375,33 +395,12 @@ class GpuMultiscaleArray final
     std::unique_ptr<aqz_binding::Handoff> handoff_;
 };
 
-// The hook of ZarrStream_s::configure_array_ (zarr.stream.cpp:1231-1279):
-//
-//     #ifdef ZARR_WITH_AQZ
-//         output->array = zarr::make_gpu_multiscale_array(
-//           config, thread_pool_, file_handle_pool_, s3_connection_pool_, *settings);
-//         if (!output->array)
-//     #endif
-//         output->array = zarr::make_array(config, thread_pool_, ...);
-//
-// A multiscale array gets the GPU stage on the device AQZ_DEVICE selects
-// (aqz_handoff.hh: round robin over the visible devices by default, one
-// stream per GPU); nullptr -- no device, AQZ_DEVICE=off, not multiscale --
-// keeps the reference's CPU path.  AQZ_Z_SLABS=N splits a volume stream
-// (a z Space dimension before y, acquisition storage order) into N z slabs
-// on the next N selected devices (BASELINE configs[3]: 4 GPUs).
-inline std::unique_ptr<ArrayBase>
-make_gpu_multiscale_array(std::shared_ptr<ArrayConfig> config,
-                          std::shared_ptr<ThreadPool> thread_pool,
-                          std::shared_ptr<FileHandlePool> file_handle_pool,
-                          std::shared_ptr<S3ConnectionPool> s3_connection_pool,
-                          const ZarrArraySettings& settings)
+// AQZ_Z_SLABS=N on a volume stream (a z Space dimension before y,
+// acquisition storage order): the z-slab plan over N stages; an empty plan
+// otherwise (one stage).
+inline aqz_binding::SlabPlan
+gpu_slab_plan(const ZarrArraySettings& settings)
 {
-    if (!settings.multiscale || !config->downsampling_method)
-        return nullptr;
-    int32_t n = 0;
-    if (aqz_device_count(&n) != AQZ_STATUS_SUCCESS)
-        return nullptr;
     aqz_binding::SlabPlan plan;
     const uint32_t slabs = aqz_binding::slabs_from_env();
     const size_t nd = settings.dimension_count;
@@ -429,6 +428,85 @@ make_gpu_multiscale_array(std::shared_ptr<ArrayConfig> config,
             }
         }
     }
+    return plan;
+}
+
+// The binding's share of ZarrStreamSettings_estimate_max_memory_usage
+// (acquire.zarr.cpp:216-314) for one array the GPU path would take (the
+// same conditions as make_gpu_multiscale_array): host_bytes is added to
+// *usage there -- the pinned hand-off and stage buffers, on top of the
+// reference's own terms for the array, which stay -- and device_bytes is
+// the HBM it needs, for a caller that reports it beside (INTEGRATION.md
+// section 2).  {0, 0} for an array that stays on the CPU path.
+inline aqz_binding::MemoryEstimate
+estimate_gpu_array_memory(const ZarrArraySettings& settings,
+                          uint32_t batch_frames = 64,
+                          uint32_t host_slots = 3)
+{
+    aqz_binding::MemoryEstimate m{};
+    int32_t n = 0;
+    const char* e = std::getenv("AQZ_DEVICE");
+    if (!settings.multiscale || aqz_device_count(&n) != AQZ_STATUS_SUCCESS || n <= 0 ||
+        (e && (std::string(e) == "off" || std::string(e) == "-1")))
+        return m;
+    std::vector<aqz_dimension> dims(settings.dimension_count);
+    for (size_t i = 0; i < dims.size(); ++i) {
+        const ZarrDimensionProperties& p = settings.dimensions[i];
+        dims[i] = aqz_dimension{ int32_t(p.type), p.array_size_px, p.chunk_size_px,
+                                 p.shard_size_chunks };
+    }
+    const aqz_array_desc desc{ dims.data(),
+                               dims.size(),
+                               int32_t(settings.data_type),
+                               1,
+                               int32_t(settings.downsampling_method),
+                               settings.max_levels,
+                               settings.storage_dimension_order,
+                               0 };
+    aqz_stage_options opt{};
+    opt.max_batch_frames = batch_frames;
+    opt.layer_slots = 2;
+    opt.placement_tries = 2; // as GpuMultiscaleArray creates its stages
+    aqz_binding::HandoffOptions ho;
+    ho.batch_frames = batch_frames;
+    ho.host_slots = host_slots;
+    if (const ZarrCompressionSettings* c = settings.compression_settings)
+        ho.comp = aqz_compression{ int32_t(c->codec), int32_t(c->level), int32_t(c->shuffle) };
+    const auto plan = gpu_slab_plan(settings);
+    const uint32_t stages = uint32_t(std::max<size_t>(1, plan.begin.size()));
+    if (aqz_binding::estimate_memory(desc, opt, ho, stages, &m) != AQZ_STATUS_SUCCESS)
+        return aqz_binding::MemoryEstimate{};
+    return m;
+}
+
+// The hook of ZarrStream_s::configure_array_ (zarr.stream.cpp:1231-1279):
+//
+//     #ifdef ZARR_WITH_AQZ
+//         output->array = zarr::make_gpu_multiscale_array(
+//           config, thread_pool_, file_handle_pool_, s3_connection_pool_, *settings);
+//         if (!output->array)
+//     #endif
+//         output->array = zarr::make_array(config, thread_pool_, ...);
+//
+// A multiscale array gets the GPU stage on the device AQZ_DEVICE selects
+// (aqz_handoff.hh: round robin over the visible devices by default, one
+// stream per GPU); nullptr -- no device, AQZ_DEVICE=off, not multiscale --
+// keeps the reference's CPU path.  AQZ_Z_SLABS=N splits a volume stream
+// (a z Space dimension before y, acquisition storage order) into N z slabs
+// on the next N selected devices (BASELINE configs[3]: 4 GPUs).
+inline std::unique_ptr<ArrayBase>
+make_gpu_multiscale_array(std::shared_ptr<ArrayConfig> config,
+                          std::shared_ptr<ThreadPool> thread_pool,
+                          std::shared_ptr<FileHandlePool> file_handle_pool,
+                          std::shared_ptr<S3ConnectionPool> s3_connection_pool,
+                          const ZarrArraySettings& settings)
+{
+    if (!settings.multiscale || !config->downsampling_method)
+        return nullptr;
+    int32_t n = 0;
+    if (aqz_device_count(&n) != AQZ_STATUS_SUCCESS)
+        return nullptr;
+    const aqz_binding::SlabPlan plan = gpu_slab_plan(settings);
     std::vector<int32_t> devices;
     for (size_t r = 0; r < std::max<size_t>(1, plan.begin.size()); ++r) {
         const int32_t device = aqz_binding::select_device(n);

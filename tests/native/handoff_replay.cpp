@@ -387,6 +387,7 @@ main(int argc, char** argv)
     }
     int rc = 0;
     double seconds = 0;
+    uint64_t host_bytes = 0, device_bytes = 0, est_host = 0, est_device = 0;
     {
         aqz_binding::HandoffOptions ho;
         ho.batch_frames = batch;
@@ -411,6 +412,23 @@ main(int argc, char** argv)
         }
         pool.drain(); // the writer jobs (Array::close_ waits on write_counter_)
         seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        // what the drop-in holds now (every compressed slot in use) against
+        // its estimate (aqz_binding::estimate_memory)
+        host_bytes = h.host_bytes();
+        for (aqz_stage* s : stages) {
+            aqz_memory_usage m{};
+            aqz_stage_memory_usage(s, &m);
+            host_bytes += m.pinned_bytes;
+            device_bytes += m.device_bytes;
+        }
+        aqz_binding::MemoryEstimate est{};
+        if (aqz_binding::estimate_memory(desc, opt, ho, uint32_t(stages.size()), &est) !=
+            AQZ_STATUS_SUCCESS) {
+            fprintf(stderr, "estimate_memory: %s\n", aqz_last_error());
+            return 1;
+        }
+        est_host = est.host_bytes;
+        est_device = est.device_bytes;
     }
     for (uint32_t l = 0; l < nl && n_slabs <= 1; ++l)
         if (sink.lv[l]->committed != aqz_stage_frames_written(st, l)) {
@@ -426,11 +444,14 @@ main(int argc, char** argv)
            "\"frames\": %llu, \"seconds\": %.4f, \"input_gbs\": %.3f, "
            "\"sink_bytes_per_input_byte\": %.4f, \"codec\": %d, \"clevel\": %d, "
            "\"shuffle\": %d, \"device\": %d, \"batch\": %u, \"copy_threads\": %u, "
-           "\"pool_threads\": %u}\n",
+           "\"pool_threads\": %u, \"host_bytes\": %llu, \"device_bytes\": %llu, "
+           "\"estimate_host_bytes\": %llu, \"estimate_device_bytes\": %llu}\n",
            rc == 0 ? "true" : "false", (unsigned long long)sink.units.load(),
            (unsigned long long)aqz_stage_last_ticket(stages.back()), (unsigned long long)n_frames,
            seconds, in / seconds / 1e9, double(sink.chunk_bytes.load()) / in, codec, clevel,
-           shuffle, device, batch, copy_threads, pool_threads);
+           shuffle, device, batch, copy_threads, pool_threads, (unsigned long long)host_bytes,
+           (unsigned long long)device_bytes, (unsigned long long)est_host,
+           (unsigned long long)est_device);
     for (aqz_stage* s : stages)
         aqz_stage_destroy(s);
     for (auto& L : sink.lv)

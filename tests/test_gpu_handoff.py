@@ -281,6 +281,11 @@ def _check_replay(exp, fw, r, codec, st):
             assert dec == buf[c * bpc:(c + 1) * bpc].tobytes(), f"{key}: decoded bytes differ"
     assert seen == set(got), sorted(set(got) - seen)[:5]
     _check_routing(r, fw, st)
+    # what the live hand-off and its stages hold against the binding's
+    # estimate (aqz_binding::estimate_memory, the drop-in's memory contract)
+    sm = r.summary
+    assert 0 < sm["host_bytes"] <= sm["estimate_host_bytes"], sm
+    assert 0 < sm["device_bytes"] <= sm["estimate_device_bytes"], sm
 
 
 def _check_routing(r, fw, st):
