@@ -2707,9 +2707,9 @@ Stage::dominant_kernel() const
         const char* k = pair    ? "fused_pyramid_strip3d_pair"
                         : strip ? "fused_pyramid_strip3d"
                                 : "fused_pyramid_3d";
-        if (xy_ && xy_direct_)
-            return pair ? "fused_pyramid_strip3d_pair (XY load)"
-                        : "fused_pyramid_strip3d (XY load)";
+        if (xy_ && xy_direct_) // the pair kernel reads XY only under knob 65536
+            return pair && (knobs_ & 65536u) ? "fused_pyramid_strip3d_pair (XY load)"
+                                             : "fused_pyramid_strip3d (XY load)";
         if (xy_)
             return pair       ? "transpose_frames + fused_pyramid_strip3d_pair"
                    : strip    ? "transpose_frames + fused_pyramid_strip3d"

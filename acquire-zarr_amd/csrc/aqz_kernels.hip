@@ -1791,12 +1791,19 @@ fused_pyramid_strip3d(const FusedParams p)
 // second half emits mean2(earlier, later) (average_two_frames,
 // downsampler.cpp:208-246) and carries levels 2-4 exactly as
 // fused_pyramid_strip3d does (later z pairs in registers across j).
-// The default where it applies; tuning knob 2 selects fused_pyramid_strip3d.
-// XY: acquisition-order planes, each half through load_region_xy with its
-// own 32 KiB LDS tile (72 KiB per workgroup).
+// The default where it applies (not for XY); tuning knob 2 selects
+// fused_pyramid_strip3d.  WPE = 4 waves per SIMD (two 8-wave workgroups per
+// CU): the register budget (128) holds the whole cascade with no scratch.
+// The round-4 build ran 6 (80 VGPRs) and spilled 32 B per lane of u16 MEAN
+// to scratch every pair -- 4.7% more HBM writes than the algorithmic bytes
+// (profiles/r05_c4_pmc.json against r05_c4-single); knob 65536 keeps it for
+// A/B.  XY: acquisition-order planes, each half through load_region_xy with
+// its own 32 KiB LDS tile (2 x 32 KiB + the 16 KiB exchange = 80 KiB per
+// workgroup); it spills even at 4 waves, so XY stages run the single-plane
+// kernel unless knob 65536 asks for this one.
 // ---------------------------------------------------------------------------
-template<typename T, int M, int NTM, bool XY = false>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(XY ? 4 : 6))) void
+template<typename T, int M, int NTM, bool XY = false, int WPE = 4>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
 fused_pyramid_strip3d_pair(const FusedParams p)
 {
     typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
@@ -2304,7 +2311,11 @@ launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
     // z and the group holds whole pairs: 0.8-1.3% faster than one plane at a
     // time on C4, same stage (profiles/r04_c4_pair_ab.txt); knob 2 keeps
     // fused_pyramid_strip3d
-    const bool pair = strip && !(p.knobs & 2u) && (p.zmask & 2u) && p.G % 2 == 0;
+    // knob 65536: the round-4 pair kernels (6 waves per SIMD, spilling; the
+    // pair for XY stages too)
+    const bool r4 = (p.knobs & 65536u) != 0;
+    const bool pair =
+      strip && !(p.knobs & 2u) && (p.zmask & 2u) && p.G % 2 == 0 && (!p.xy || r4);
     // acquisition-order planes: only through the strip kernel's XY load
     if (p.xy && !(strip && dtype != 3 && dtype != 7 && dtype != 9))
         return hipErrorInvalidValue;
@@ -2318,6 +2329,9 @@ launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
         else if (p.xy && p.nt)                                                \
             hipLaunchKernelGGL((fused_pyramid_strip3d<T, MM, 7, 0, true>), gd, dim3(256), \
                                0, stream, pr);                                 \
+        else if (pair && p.nt && r4)                                          \
+            hipLaunchKernelGGL((fused_pyramid_strip3d_pair<T, MM, 7, false, 6>), gd, \
+                               dim3(512), 0, stream, pr);                      \
         else if (pair && p.nt)                                                \
             hipLaunchKernelGGL((fused_pyramid_strip3d_pair<T, MM, 7>), gd, dim3(512), 0, \
                                stream, pr);                                    \

@@ -350,6 +350,8 @@ def test_stage_timing_marks(gpu):
 # variant without the next-plane prefetch) and, with knob 256, the
 # LDS-cascade kernel it replaced (fused_pyramid_3d)
 KERNELS_3D = {"strip3d_pair": (0, "fused_pyramid_strip3d_pair"),
+              # the round-4 pair kernel (6 waves per SIMD, spills; A/B only)
+              "strip3d_pair_r4": (65536, "fused_pyramid_strip3d_pair"),
               "strip3d": (2, "fused_pyramid_strip3d"),
               "strip3d_nopf": (2 | 512, "fused_pyramid_strip3d"),
               "lds3d": (256, "fused_pyramid_3d")}
@@ -732,7 +734,8 @@ def test_environment_cannot_change_drop_in_output(gpu, monkeypatch, env):
     st.close()
 
 
-XY_KERNELS_3D = {"pair": (0, "fused_pyramid_strip3d_pair (XY load)"),
+XY_KERNELS_3D = {"default": (0, "fused_pyramid_strip3d (XY load)"),
+                 "pair": (65536, "fused_pyramid_strip3d_pair (XY load)"),
                  "single": (2, "fused_pyramid_strip3d (XY load)"),
                  "pass": (4096, "transpose_frames + fused_pyramid_strip3d_pair")}
 
@@ -744,8 +747,9 @@ def test_stage_xy_fused_strip3d(gpu, dtype, path):
     array.cpp:488-534): the 3-D strip kernel reads the acquisition-order
     planes itself (load_region_xy, one LDS transpose per plane), knob 4096
     the separate transpose pass.  Batches of whole z groups take the fused
-    load -- two planes at a time by default (fused_pyramid_strip3d_pair, each
-    half of the workgroup its own LDS tile), one at a time with knob 2; a
+    load -- one plane at a time by default, two at a time with knob 65536
+    (fused_pyramid_strip3d_pair, each half of the workgroup its own LDS
+    tile; it spills, so it is not the default); a
     batch that also needs the generic cascade (6 planes: one z group and a
     carried pair) is transposed first.  Either way every level equals the
     oracle's on the transposed frames."""

@@ -16,24 +16,38 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
                                 "acquire-zarr_amd"))
 import aqz  # noqa: E402
 
-C2 = [(2, 0, 64, 1), (0, 2048, 256, 1), (0, 2048, 256, 1)]
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tries", type=int, default=6)
     ap.add_argument("--plain", action="store_true")
-    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--instances", type=int, default=1,
+                    help="successive stages in this process, each closed before the next")
     a = ap.parse_args()
-    kw = dict(force_levels=5, max_batch_frames=a.batch, layer_slots=max(2, a.batch // 64),
-              placement_tries=a.tries, placement_flags=1)
+    c = bench.CONFIGS[a.config]
+    B = a.batch or c["batch"]
+    kw = dict(force_levels=c["force_levels"], max_batch_frames=B,
+              layer_slots=bench.layer_slots_for(c, B), placement_tries=a.tries,
+              placement_flags=1)
     if a.plain:
         kw["ring_malloc_flags"] = 0x10000
-    st = aqz.Stage(C2, 1, 1, **kw)
+    for inst in range(a.instances):
+        report(a, c, B, inst, kw)
+
+
+def report(a, c, B, inst, kw):
+    st = aqz.Stage(c["dims"], c["dtype"], c["method"], **kw)
     pl = st.placement()
     st.close()
     alg = pl["alg_bytes"]
-    print(json.dumps({"plain": a.plain, "batch": a.batch, "mode": pl["mode"],
+    print(json.dumps({"config": a.config, "inst": inst, "plain": a.plain, "batch": B,
+                      "mode": pl["mode"],
                       "stage_ms": pl["candidates_ms"],
                       "stage_bus_gbs": [round(alg / (m * 1e-3) / 1e9, 1)
                                         for m in pl["candidates_ms"]],

@@ -65,4 +65,42 @@ tail -25 $O/pytest.log
 [ $rc -eq 0 ] || exit 1
 }
 
+# C4 pair vs single-plane kernel: same-stage timing, PMC of each; C3 SQ/TA
+step_p5() {
+O=gpurun_out/r5e
+mkdir -p $O
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c4 --knobs 0,2 --instances 3 > $O/c4_knob_ab.txt 2>&1 || { tail $O/c4_knob_ab.txt; exit 1; }
+cat $O/c4_knob_ab.txt
+timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
+STEPS=200 bash tools/profile.sh c4 r05 || exit 1
+STEPS=200 BENCH_EXTRA="--tune knobs=2" NAME_SUFFIX=-single bash tools/profile.sh c4 r05 || exit 1
+STEPS=200 SQ2="TA_BUSY_avr TA_TA_BUSY_sum SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_VALU" bash tools/profile.sh c3 r05 || exit 1
+}
+
+# placement: stage vs probe over successive arenas; C4 write-request PMC
+step_p6() {
+O=gpurun_out/r5f
+mkdir -p $O
+timeout -k 10 200 python3 -u tools/placement_r05.py --config c4 --tries 3 --instances 5 >> $O/cand.jsonl 2>> $O/cand.err || { tail $O/cand.err; exit 1; }
+timeout -k 10 200 python3 -u tools/placement_r05.py --config c2 --tries 3 --instances 4 >> $O/cand.jsonl 2>> $O/cand.err || { tail $O/cand.err; exit 1; }
+cat $O/cand.jsonl
+B="python3 bench.py --config c4 --steps 5 --warmup 2 --no-cpu-baseline --no-pyramid-only-line --no-hbm-probe"
+for v in 0 2; do
+timeout -s KILL 90 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_WRITE_sum TCC_WRITE_SECTORS_sum --output-format csv -d $O/k$v-a -o run -- $B --tune knobs=$v > $O/k$v-a.log 2>&1 || exit 1
+timeout -s KILL 90 rocprofv3 --pmc TCC_NORMAL_WRITEBACK_sum TCC_WRITEBACK_sum TCC_NORMAL_EVICT_sum TCC_STREAMING_REQ_sum --output-format csv -d $O/k$v-b -o run -- $B --tune knobs=$v > $O/k$v-b.log 2>&1 || exit 1
+done
+}
+
+# C4 pair kernel without spills: A/B, parity, PMC
+step_p7() {
+O=gpurun_out/r5g
+mkdir -p $O
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c4 --knobs 0,65536,2 --instances 3 > $O/c4_ab.txt 2>&1 || { tail $O/c4_ab.txt; exit 1; }
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c4 --xy --knobs 0,65536 --instances 2 >> $O/c4_ab.txt 2>&1 || { tail $O/c4_ab.txt; exit 1; }
+cat $O/c4_ab.txt
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_headline.py -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider -k "3d or xy or c4" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -3 $O/pytest.log
+NO_SQ=1 STEPS=200 bash tools/profile.sh c4 r05b || exit 1
+}
+
 "step_$@"
