@@ -26,13 +26,16 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--placement-tries", type=int, default=0)
     ap.add_argument("--xy", action="store_true", help="XY-transposed storage order")
+    ap.add_argument("--batch", type=int, default=0, help="frames per launch (default: bench's)")
     args = ap.parse_args()
     c = bench.CONFIGS[args.config]
-    B = c["batch"]
+    B = args.batch or c["batch"]
     h, w = c["dims"][-2][1], c["dims"][-1][1]
     fbytes = h * w * {0: 1, 1: 2, 8: 4}[c["dtype"]]
     src = torch.empty(2 * B * fbytes, dtype=torch.uint8, device="cuda")
     src.view(torch.int16).random_(-32768, 32767)
+    # (two batches of frames: >= 2 GiB at the bench's batch sizes, past the
+    # 256 MiB MALL)
     knobs = [int(x) for x in args.knobs.split(",")]
     nd = len(c["dims"])
     xy = dict(storage_order=list(range(nd - 2)) + [nd - 1, nd - 2]) if args.xy else {}
@@ -54,7 +57,7 @@ def main():
                 ms = st.timing_elapsed() / args.reps
                 row = row + [ms] if rnd == 0 else row
                 row[j] = min(row[j], ms)
-        print(f"{args.config} inst{inst} {st.placement()['candidates_ms']} " +
+        print(f"{args.config} B{B} inst{inst} {st.placement()['candidates_ms']} " +
               " ".join(f"k{k}={v:.4f}" for k, v in zip(knobs, row)), flush=True)
         st.close()
 

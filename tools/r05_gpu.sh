@@ -103,4 +103,14 @@ tail -3 $O/pytest.log
 NO_SQ=1 STEPS=200 bash tools/profile.sh c4 r05b || exit 1
 }
 
+# C3: launch size and occupancy A/Bs
+step_p8() {
+O=gpurun_out/r5h
+mkdir -p $O
+for B in 64 128; do
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c3 --batch $B --knobs 0,40960,49152,57344 --instances 2 >> $O/c3_ab.txt 2>&1 || { tail $O/c3_ab.txt; exit 1; }
+done
+cat $O/c3_ab.txt
+}
+
 "step_$@"
