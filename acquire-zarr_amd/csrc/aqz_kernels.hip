@@ -2207,6 +2207,9 @@ launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t stream)
         default: return hipErrorInvalidValue;                                  \
     }
 
+// workgroups of the 2-D strip kernel per CU (launch_interior)
+constexpr uint32_t kStripWgPerCu = 6;
+
 // The strip kernel takes 64-row interior regions of <= 4-byte pixels when
 // no level 3-4 output goes to scratch; fused_pyramid takes the rest.
 template<typename T, int M>
@@ -2225,31 +2228,32 @@ launch_interior(uint32_t blocks, const FusedParams& p, hipStream_t stream)
         }
         if (p.rh_log2 == 6 && !(p.knobs & 128u) &&
             (p.scratch_level == 0 || p.scratch_level >= 5)) {
-            // tuning knob bits 13-15 = v: unused LDS that caps the strip
-            // kernel at v workgroups per CU (an occupancy A/B)
+            // Occupancy: at most kStripWgPerCu workgroups per CU, held by
+            // unused dynamic LDS (the kernel's registers would allow 8).
+            // Same stage A/Bs, round 5 (profiles/r05_occupancy_cap.txt):
+            // 6 per CU is 0.5-1.8% faster on C1, C2, C2-ref4 and C3 and
+            // within 0.1% on C5 -- fewer streams of row reads in flight per
+            // CU contend less for the memory channels.  Tuning knob bits
+            // 13-15 = v: 0 the shipped cap, 1 uncapped, else v per CU.
             const uint32_t v = (p.knobs >> 13) & 7u;
-            const uint32_t cap_lds = v ? (163840u / v - 512u) & ~255u : 0u;
-            if (cap_lds && p.nt == 7) {
-                hipLaunchKernelGGL((fused_pyramid_strip<T, M, 7>), dim3(blocks), dim3(256),
-                                   cap_lds, stream, p);
-                return;
-            }
+            const uint32_t per_cu = v == 0 ? kStripWgPerCu : v;
+            const uint32_t lds = per_cu > 1 ? (163840u / per_cu - 512u) & ~255u : 0u;
             switch (p.nt) {
                 case 1:
                     hipLaunchKernelGGL((fused_pyramid_strip<T, M, 1>), dim3(blocks),
-                                       dim3(256), 0, stream, p);
+                                       dim3(256), lds, stream, p);
                     break;
                 case 3:
                     hipLaunchKernelGGL((fused_pyramid_strip<T, M, 3>), dim3(blocks),
-                                       dim3(256), 0, stream, p);
+                                       dim3(256), lds, stream, p);
                     break;
                 case 7:
                     hipLaunchKernelGGL((fused_pyramid_strip<T, M, 7>), dim3(blocks),
-                                       dim3(256), 0, stream, p);
+                                       dim3(256), lds, stream, p);
                     break;
                 default:
                     hipLaunchKernelGGL((fused_pyramid_strip<T, M, 0>), dim3(blocks),
-                                       dim3(256), 0, stream, p);
+                                       dim3(256), lds, stream, p);
             }
             return;
         }

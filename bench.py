@@ -62,10 +62,13 @@ CONFIGS = {
                              "at 256-px chunks), t-chunk 64, mean, device-resident",
                     dims=[(TIME, 0, 64, 1), (SPACE, 2048, 256, 1), (SPACE, 2048, 256, 1)],
                     dtype=U16, method=MEAN, force_levels=0, batch=128, ring=256),
+    # 128-frame launches (2 GiB of input, as C2's 256): 4.7% faster than 64
+    # on the same stage (profiles/r05_c3_launch_ab.txt) -- a launch's ramp
+    # and tail are a smaller share
     "c3": dict(workload="uint8 4096x4096 frames, 6-level pyramid, 128x128 chunks, mean, "
                         "device-resident",
                dims=[(TIME, 0, 32, 1), (SPACE, 4096, 128, 1), (SPACE, 4096, 128, 1)],
-               dtype=U8, method=MEAN, force_levels=0, batch=64, ring=160),
+               dtype=U8, method=MEAN, force_levels=0, batch=128, ring=256),
     # BASELINE configs[3]: a 256-plane volume, 2x2x2 pyramid (z 256->128->
     # 64->64, xy 2048->1024->512->256).  With --gpus N rank r owns z slab
     # [lo, hi) of every volume of the stream (aqz_stage_options z_slab_*,

@@ -113,4 +113,25 @@ done
 cat $O/c3_ab.txt
 }
 
+# occupancy cap (unused LDS: v workgroups per CU) on every strip-kernel config
+step_p9() {
+O=gpurun_out/r5i
+mkdir -p $O
+for cfg in "c2 256" "c3 128" "c5 8" "c1 1024" "c2-ref4 128"; do
+set -- $cfg
+timeout -k 10 300 python3 -u tools/knob_ab.py --config $1 --batch $2 --knobs 0,40960,49152,57344 --instances 2 >> $O/cap_ab.txt 2>&1 || { tail $O/cap_ab.txt; exit 1; }
+done
+cat $O/cap_ab.txt
+}
+
+# bench lines of every config with the current build (device-resident)
+step_lines() {
+O=gpurun_out/r5lines${1:-}
+mkdir -p $O
+for c in c2 c3 c4 c5 c1 c2-ref4; do
+timeout -k 10 200 python3 -u bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline > $O/$c.json 2> $O/$c.err || { tail $O/$c.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/$c.json')); r=d['roofline']; p=r['placement']; print(json.dumps({'cfg': '$c', 'value': d['value'], 'frac': r['frac'], 'ms': r['kernel_avg_ms'], 'kernel': r['kernel'], 'cand': p.get('candidates_ms'), 'acc': p.get('accepted'), 'probe': r.get('probe_same_shape_gbs'), 'fop': r.get('frac_of_probe_same_shape'), 'traffic': r.get('traffic'), 'pyr': (d.get('pyramid_only') or {}).get('input_rate_frac_of_peak')}))" | tee -a $O/lines.jsonl
+done
+}
+
 "step_$@"
