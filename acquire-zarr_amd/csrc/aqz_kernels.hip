@@ -1802,7 +1802,7 @@ fused_pyramid_strip3d(const FusedParams p)
 // workgroup); it spills even at 4 waves, so XY stages run the single-plane
 // kernel unless knob 65536 asks for this one.
 // ---------------------------------------------------------------------------
-template<typename T, int M, int NTM, bool XY = false, int WPE = 4>
+template<typename T, int M, int NTM, bool XY = false, int WPE = 4, int PF = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
 fused_pyramid_strip3d_pair(const FusedParams p)
 {
@@ -1850,24 +1850,33 @@ fused_pyramid_strip3d_pair(const FusedParams p)
     const uint32_t g3 = g2 >> ((zm >> 3) & 1u);
     const uint32_t g4 = g3 >> ((zm >> 4) & 1u);
 
+    // this half's plane of pair jj into ra/rb; PF: pair j+1's loads are
+    // issued as soon as pair j's level-0 stores and level-1 sums no longer
+    // need them, so they are in flight across the exchange barrier and
+    // levels 1-4 (not for XY, whose loads go through LDS behind barriers)
+    uint4 ra[4], rb[4];
+    auto load_pair = [&](uint32_t jj) {
+        const uint8_t* s = src0 + uint64_t(2 * jj) * p.src_stride;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u32x4v a = gload<(NTM & 1) != 0, u32x4v>(s + uint64_t(4 * i) * row);
+            const u32x4v b = gload<(NTM & 1) != 0, u32x4v>(s + uint64_t(4 * i + 1) * row);
+            ra[i] = uint4{ a.x, a.y, a.z, a.w };
+            rb[i] = uint4{ b.x, b.y, b.z, b.w };
+        }
+    };
+    if constexpr (!XY && PF)
+        load_pair(0);
     for (uint32_t j = 0; 2 * j < G; ++j) {
         const uint32_t pl = 2 * j + half;
-        uint4 ra[4], rb[4];
         if constexpr (XY) {
             // the previous pair's gathers are behind the level-1 exchange's
             // barrier; the transpose addresses are recomputed per pair
             uint32_t tid = t, ryo = ry, cvo = cv;
             asm volatile("" : "+v"(tid), "+v"(ryo), "+v"(cvo));
             load_region_xy<T, NTM, 2>(p, grp * G + pl, y0, x0, ryo, cvo, ra, rb, tid, half);
-        } else {
-            const uint8_t* s = src0 + uint64_t(2 * j) * p.src_stride;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const u32x4v a = gload<(NTM & 1) != 0, u32x4v>(s + uint64_t(4 * i) * row);
-                const u32x4v b = gload<(NTM & 1) != 0, u32x4v>(s + uint64_t(4 * i + 1) * row);
-                ra[i] = uint4{ a.x, a.y, a.z, a.w };
-                rb[i] = uint4{ b.x, b.y, b.z, b.w };
-            }
+        } else if constexpr (!PF) {
+            load_pair(j);
         }
         // level 0: both halves
         {
@@ -1885,20 +1894,26 @@ fused_pyramid_strip3d_pair(const FusedParams p)
             }
             flush_tile_flag(t0);
         }
-        if (nf < 1)
-            continue;
         // level-1 2x2 sums of this half's plane
         uint2 o1[4];
+        if (nf >= 1) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            T r0[VEC], r1[VEC], o[HV];
-            __builtin_memcpy(r0, &ra[i], 16);
-            __builtin_memcpy(r1, &rb[i], 16);
+            for (int i = 0; i < 4; ++i) {
+                T r0[VEC], r1[VEC], o[HV];
+                __builtin_memcpy(r0, &ra[i], 16);
+                __builtin_memcpy(r1, &rb[i], 16);
 #pragma unroll
-            for (int q = 0; q < HV; ++q)
-                o[q] = reduce4<M, T>(r0[2 * q], r0[2 * q + 1], r1[2 * q], r1[2 * q + 1]);
-            __builtin_memcpy(&o1[i], o, 8);
+                for (int q = 0; q < HV; ++q)
+                    o[q] = reduce4<M, T>(r0[2 * q], r0[2 * q + 1], r1[2 * q], r1[2 * q + 1]);
+                __builtin_memcpy(&o1[i], o, 8);
+            }
         }
+        if constexpr (!XY && PF) {
+            if (2 * (j + 1) < G)
+                load_pair(j + 1);
+        }
+        if (nf < 1)
+            continue;
         if (half == 0) {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -2335,6 +2350,9 @@ launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
                                0, stream, pr);                                 \
         else if (pair && p.nt && r4)                                          \
             hipLaunchKernelGGL((fused_pyramid_strip3d_pair<T, MM, 7, false, 6>), gd, \
+                               dim3(512), 0, stream, pr);                      \
+        else if (pair && p.nt && (p.knobs & 131072u))                         \
+            hipLaunchKernelGGL((fused_pyramid_strip3d_pair<T, MM, 7, false, 4, 1>), gd, \
                                dim3(512), 0, stream, pr);                      \
         else if (pair && p.nt)                                                \
             hipLaunchKernelGGL((fused_pyramid_strip3d_pair<T, MM, 7>), gd, dim3(512), 0, \

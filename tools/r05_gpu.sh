@@ -147,4 +147,14 @@ python3 -c "import json; d=json.load(open('$O/tmp.json')); print(d['metric'][:60
 done
 }
 
+# C4 pair kernel with next-pair prefetch: A/B and parity
+step_p10() {
+O=gpurun_out/r5p10
+mkdir -p $O
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c4 --knobs 0,131072,2 --instances 3 > $O/c4_pf_ab.txt 2>&1 || { tail $O/c4_pf_ab.txt; exit 1; }
+cat $O/c4_pf_ab.txt
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider -k "3d" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+}
+
 "step_$@"
