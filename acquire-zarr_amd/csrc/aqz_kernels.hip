@@ -1792,7 +1792,10 @@ fused_pyramid_strip3d(const FusedParams p)
 // downsampler.cpp:208-246) and carries levels 2-4 exactly as
 // fused_pyramid_strip3d does (later z pairs in registers across j).
 // The default where it applies (not for XY); tuning knob 2 selects
-// fused_pyramid_strip3d.  WPE = 4 waves per SIMD (two 8-wave workgroups per
+// fused_pyramid_strip3d.  PF: pair j+1's loads are issued while pair j's
+// levels 1-4 are formed (1.1-1.3% faster on C4, same stage,
+// profiles/r05_c4_prefetch_ab.txt; knob 131072 turns it off, 107 VGPRs with
+// it, 87 without).  WPE = 4 waves per SIMD (two 8-wave workgroups per
 // CU): the register budget (128) holds the whole cascade with no scratch.
 // The round-4 build ran 6 (80 VGPRs) and spilled 32 B per lane of u16 MEAN
 // to scratch every pair -- 4.7% more HBM writes than the algorithmic bytes
@@ -1802,7 +1805,7 @@ fused_pyramid_strip3d(const FusedParams p)
 // workgroup); it spills even at 4 waves, so XY stages run the single-plane
 // kernel unless knob 65536 asks for this one.
 // ---------------------------------------------------------------------------
-template<typename T, int M, int NTM, bool XY = false, int WPE = 4, int PF = 0>
+template<typename T, int M, int NTM, bool XY = false, int WPE = 4, int PF = 1>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
 fused_pyramid_strip3d_pair(const FusedParams p)
 {
@@ -2349,10 +2352,10 @@ launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
             hipLaunchKernelGGL((fused_pyramid_strip3d<T, MM, 7, 0, true>), gd, dim3(256), \
                                0, stream, pr);                                 \
         else if (pair && p.nt && r4)                                          \
-            hipLaunchKernelGGL((fused_pyramid_strip3d_pair<T, MM, 7, false, 6>), gd, \
+            hipLaunchKernelGGL((fused_pyramid_strip3d_pair<T, MM, 7, false, 6, 0>), gd, \
                                dim3(512), 0, stream, pr);                      \
         else if (pair && p.nt && (p.knobs & 131072u))                         \
-            hipLaunchKernelGGL((fused_pyramid_strip3d_pair<T, MM, 7, false, 4, 1>), gd, \
+            hipLaunchKernelGGL((fused_pyramid_strip3d_pair<T, MM, 7, false, 4, 0>), gd, \
                                dim3(512), 0, stream, pr);                      \
         else if (pair && p.nt)                                                \
             hipLaunchKernelGGL((fused_pyramid_strip3d_pair<T, MM, 7>), gd, dim3(512), 0, \

@@ -352,8 +352,8 @@ def test_stage_timing_marks(gpu):
 KERNELS_3D = {"strip3d_pair": (0, "fused_pyramid_strip3d_pair"),
               # the round-4 pair kernel (6 waves per SIMD, spills; A/B only)
               "strip3d_pair_r4": (65536, "fused_pyramid_strip3d_pair"),
-              # next-pair prefetch (A/B)
-              "strip3d_pair_pf": (131072, "fused_pyramid_strip3d_pair"),
+              # without the next-pair prefetch (A/B)
+              "strip3d_pair_nopf": (131072, "fused_pyramid_strip3d_pair"),
               "strip3d": (2, "fused_pyramid_strip3d"),
               "strip3d_nopf": (2 | 512, "fused_pyramid_strip3d"),
               "lds3d": (256, "fused_pyramid_3d")}

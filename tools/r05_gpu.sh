@@ -157,4 +157,14 @@ timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -q -x --t
 tail -2 $O/pytest.log
 }
 
+# C4 launch size 128 vs 256 planes (prefetching pair kernel), and no-prefetch A/B
+step_p11() {
+O=gpurun_out/r5p11
+mkdir -p $O
+for B in 128 256; do
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c4 --batch $B --knobs 0,131072 --instances 2 >> $O/c4_ab.txt 2>&1 || { tail $O/c4_ab.txt; exit 1; }
+done
+cat $O/c4_ab.txt
+}
+
 "step_$@"
