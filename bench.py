@@ -43,11 +43,13 @@ DTYPE_WORDS = {U8: "uint8", U16: "uint16", F32: "float32"}
 
 CONFIGS = {
     # BASELINE.json configs[0], the reference's CPU-runnable case (SURVEY
-    # §8a: u16 512x512, 3 levels at 128-px chunks, decimate), device-resident
+    # §8a: u16 512x512, 3 levels at 128-px chunks, decimate), device-resident;
+    # 2048-frame launches (1 GiB of input): 2-8% faster than 1024 on the same
+    # stages (profiles/r05_c1_launch_ab.txt)
     "c1": dict(workload="uint16 512x512 frames, 3-level pyramid (512..128 px), 128x128 "
                         "chunks (t-chunk 64), decimate, device-resident",
                dims=[(TIME, 0, 64, 1), (SPACE, 512, 128, 1), (SPACE, 512, 128, 1)],
-               dtype=U16, method=DECIMATE, force_levels=0, batch=1024, ring=4096),
+               dtype=U16, method=DECIMATE, force_levels=0, batch=2048, ring=4096),
     # BASELINE.json configs[1] -- the metric's config.  The reference level
     # rule (downsampler.cpp:512-541) stops at 4 levels for 256-px chunks;
     # force_levels keeps halving to the requested 5 (L4 = 128 px, one

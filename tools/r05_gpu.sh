@@ -167,4 +167,16 @@ done
 cat $O/c4_ab.txt
 }
 
+# C1 launch size; C5 and C1 PMC
+step_p12() {
+O=gpurun_out/r5p12
+mkdir -p $O
+for B in 1024 2048; do
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c1 --batch $B --knobs 0,8192 --instances 2 >> $O/c1_ab.txt 2>&1 || { tail $O/c1_ab.txt; exit 1; }
+done
+cat $O/c1_ab.txt
+NO_SQ=1 STEPS=100 bash tools/profile.sh c5 r05 || exit 1
+NO_SQ=1 STEPS=200 bash tools/profile.sh c1 r05 || exit 1
+}
+
 "step_$@"
