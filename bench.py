@@ -138,7 +138,7 @@ def fill_ring(torch, ring, dtype, seed):
         ring.view(torch.float32).uniform_(0.0, 65535.0, generator=g)
 
 
-def pmc_traffic(config, pyramid_only, kernel, frames, ring_allocation):
+def pmc_traffic(config, pyramid_only, kernel, frames, ring_allocation, run_ms=None):
     """Per-launch HBM bytes of the dominant kernel from the newest committed
     rocprofv3 PMC summary for this configuration whose rings were allocated
     the same way as this run's (tools/profile.sh -> tools/pmc_summary.py ->
@@ -150,18 +150,30 @@ def pmc_traffic(config, pyramid_only, kernel, frames, ring_allocation):
     import glob
     name = config + ("-pyr" if pyramid_only else "")
     files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{name}_pmc.json")))
-    for f in reversed(files):
+    found = []
+    for f in files:
         d = json.load(open(f))
         if (d.get("config") == name and kernel and kernel in d.get("kernel", "")
                 and d.get("ring_allocation") == ring_allocation):
-            # (traffic is linear in the frames of a launch: a profile of
-            # another launch size is scaled to this one)
-            t = d["traffic_bytes_per_launch"]
-            fpl = d.get("frames_per_launch")
-            if fpl and fpl != frames:
-                t = int(round(t * frames / fpl))
-            return t, os.path.relpath(f, REPO), d
-    return None, None, None
+            found.append((f, d))
+    if not found:
+        return None, None, None
+    # MI355X boxes run the same kernel at different speeds (DESIGN.md
+    # section 5); the bytes do not change with the box.  Of the profiles of
+    # this configuration and ring allocation, the one whose kernel time is
+    # closest to this run's represents it best (newest on a tie).
+    def gap(fd):
+        pa = fd[1].get("steady_avg_duration_ns") or fd[1].get("avg_duration_ns") or 0.0
+        fpl = fd[1].get("frames_per_launch") or frames
+        return abs(pa * 1e-6 * frames / fpl - run_ms) if run_ms else 0.0
+    f, d = min(reversed(found), key=gap)
+    # (traffic is linear in the frames of a launch: a profile of another
+    # launch size is scaled to this one)
+    t = d["traffic_bytes_per_launch"]
+    fpl = d.get("frames_per_launch")
+    if fpl and fpl != frames:
+        t = int(round(t * frames / fpl))
+    return t, os.path.relpath(f, REPO), d
 
 
 def ring_allocation(pl):
@@ -743,7 +755,7 @@ def main():
     # how the chunk-layer rings were allocated (aqz_placement_report.mode)
     pl["ring_allocation"] = ring_allocation(pl)
     traffic, traffic_src, prof = pmc_traffic(args.config, args.pyramid_only, kernel, B,
-                                             pl["ring_allocation"])
+                                             pl["ring_allocation"], avg_ms)
 
     result = {
         "metric": f"input GB/s, device-resident multiscale downsample, {DTYPE_WORDS[dt]} "
@@ -787,6 +799,7 @@ def main():
         # the profiled run of this command: its rocprof kernel average and
         # the frac it gives, next to this run's
         pa = prof.get("steady_avg_duration_ns") or prof.get("avg_duration_ns")
+        pa *= B / (prof.get("frames_per_launch") or B)
         result["roofline"]["profile_kernel_avg_ms"] = round(pa / 1e6, 5)
         result["roofline"]["profile_frac"] = round(
             alg_per_launch / (pa * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
@@ -831,16 +844,17 @@ def main():
             "achieved": round(side["achieved"], 1),
             "input_rate_frac_of_peak": round(side["value"] / world / HBM_PEAK_GBS, 4)}
         if probe:
-            # the same shape's ceiling on a plain streaming kernel, this run
+            # a plain streaming kernel of the same shape (1 read : 1/3
+            # write) on separate buffers, this run: a reference rate
             pr = probe["read_third_input_gbs"]
             result["pyramid_only"].update({
-                "probed_ceiling_input_gbs": pr,
-                "input_rate_frac_of_probed_ceiling": round(side["value"] / world / pr, 4),
+                "probe_input_gbs": pr,
+                "input_rate_frac_of_probe": round(side["value"] / world / pr, 4),
                 # kernel time only (no launch gaps): input bytes per launch
                 # over the event-timed launch duration
-                "kernel_input_frac_of_probed_ceiling": round(
+                "kernel_input_frac_of_probe": round(
                     B * side["fbytes"] / (side["avg_ms"] * 1e-3) / 1e9 / pr, 4),
-                "probed_ceiling_source": "hbm_probe.read_third_input_gbs"})
+                "probe_source": "hbm_probe.read_third_input_gbs"})
     if per_rank:
         result["per_rank"] = per_rank
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
