@@ -984,6 +984,11 @@ load_region_xy(const FusedParams& p, uint32_t f, uint32_t y0, uint32_t x0, uint3
     constexpr uint32_t VR = 4 * sizeof(T); // 16-B vectors per 64-pixel row segment
     constexpr uint32_t PV = 8 / sizeof(T); // column pairs per 16-B vector
     __shared__ PT xt_slots[SLOTS * RW * 32]; // 32 KiB per slot
+    static_assert(sizeof(PT) * RW * 32 == 32768, "one transpose slot is 32 KiB");
+    // with the pair kernel's 16 KiB level-1 exchange: 2 x 32 + 16 = 80 KiB
+    // per workgroup, two workgroups per CU in gfx950's 160 KiB
+    static_assert(SLOTS * 32768 + (SLOTS > 1 ? 16384 : 0) <= 163840 / 2,
+                  "the XY kernels' LDS must leave room for two workgroups per CU");
     PT* const xt = xt_slots + slot * (RW * 32);
     const uint64_t pitch = uint64_t(p.H[0]) * sizeof(T); // acquisition row bytes
     const uint8_t* s =
