@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--placement-tries", type=int, default=0)
     ap.add_argument("--xy", action="store_true", help="XY-transposed storage order")
     ap.add_argument("--batch", type=int, default=0, help="frames per launch (default: bench's)")
+    ap.add_argument("--appends", default="",
+                    help="append sizes (frames, dividing the batch) to compare on the same "
+                         "stage: ms per batch of frames for each (with the first knob)")
     args = ap.parse_args()
     c = bench.CONFIGS[args.config]
     B = args.batch or c["batch"]
@@ -57,8 +60,28 @@ def main():
                 ms = st.timing_elapsed() / args.reps
                 row = row + [ms] if rnd == 0 else row
                 row[j] = min(row[j], ms)
+        extra = ""
+        if args.appends:
+            st.set_tuning(knobs[0], args.nt)
+            sizes = [int(x) for x in args.appends.split(",")]
+            best = {}
+            for rnd in range(2):
+                for a in sizes:
+                    per = B // a
+                    for i in range(2 * per):
+                        st.append_ptr(src.data_ptr() + (i // per % 2) * B * fbytes +
+                                      (i % per) * a * fbytes, a)
+                    st.synchronize()
+                    st.timing_mark(0)
+                    for i in range(args.reps * per):
+                        st.append_ptr(src.data_ptr() + (i // per % 2) * B * fbytes +
+                                      (i % per) * a * fbytes, a)
+                    st.timing_mark(1)
+                    ms = st.timing_elapsed() / args.reps
+                    best[a] = min(best.get(a, ms), ms)
+            extra = " " + " ".join(f"append{a}={v:.4f}" for a, v in best.items())
         print(f"{args.config} B{B} inst{inst} {st.placement()['candidates_ms']} " +
-              " ".join(f"k{k}={v:.4f}" for k, v in zip(knobs, row)), flush=True)
+              " ".join(f"k{k}={v:.4f}" for k, v in zip(knobs, row)) + extra, flush=True)
         st.close()
 
 

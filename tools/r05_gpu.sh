@@ -179,4 +179,14 @@ NO_SQ=1 STEPS=100 bash tools/profile.sh c5 r05 || exit 1
 NO_SQ=1 STEPS=200 bash tools/profile.sh c1 r05 || exit 1
 }
 
+# C2 launch size 256 vs 512 frames; C2 profile of the shipped build
+step_p13() {
+O=gpurun_out/r5p13
+mkdir -p $O
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c2 --batch 512 --knobs 0 --appends 256,512 --instances 2 >> $O/c2_ab.txt 2>&1 || { tail $O/c2_ab.txt; exit 1; }
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c4 --batch 256 --knobs 0 --appends 128,256 --instances 2 >> $O/c2_ab.txt 2>&1 || { tail $O/c2_ab.txt; exit 1; }
+cat $O/c2_ab.txt
+STEPS=200 bash tools/profile.sh c2 r05d || exit 1
+}
+
 "step_$@"
