@@ -54,25 +54,29 @@ CONFIGS = {
     # rule (downsampler.cpp:512-541) stops at 4 levels for 256-px chunks;
     # force_levels keeps halving to the requested 5 (L4 = 128 px, one
     # partial 256x256 chunk), pixel values unchanged.
+    # 512-frame launches (4 GiB of input): a launch's ramp-up and drain cost
+    # ~15 us whatever its size; 2.3-3.1% faster than 256 on the same stage,
+    # 1024 adds 0.5% more (profiles/r05_launch_size_ab.txt)
     "c2": dict(workload="uint16 2048x2048 frames, 5-level pyramid (2048..128 px), "
                         "256x256 chunks (t-chunk 64), mean, level-0 split + pyramid + "
                         "tile split of all levels, device-resident",
                dims=[(TIME, 0, 64, 1), (SPACE, 2048, 256, 1), (SPACE, 2048, 256, 1)],
-               dtype=U16, method=MEAN, force_levels=5, batch=256, ring=256),
+               dtype=U16, method=MEAN, force_levels=5, batch=512, ring=512),
     # same, reference level rule (4 levels)
     "c2-ref4": dict(workload="uint16 2048x2048 frames, 4-level pyramid (reference rule "
                              "at 256-px chunks), t-chunk 64, mean, device-resident",
                     dims=[(TIME, 0, 64, 1), (SPACE, 2048, 256, 1), (SPACE, 2048, 256, 1)],
-                    dtype=U16, method=MEAN, force_levels=0, batch=128, ring=256),
-    # 128-frame launches (2 GiB of input, as C2's 256): 4.7% faster than 64
-    # on the same stage (profiles/r05_c3_launch_ab.txt) -- a launch's ramp
-    # and tail are a smaller share
+                    dtype=U16, method=MEAN, force_levels=0, batch=512, ring=512),
+    # 256-frame launches (4 GiB of input): 128 was 4.7% faster than 64
+    # (profiles/r05_c3_launch_ab.txt), 256 1.6-2.4% faster than 128 on the
+    # same stage (profiles/r05_launch_size_ab.txt)
     "c3": dict(workload="uint8 4096x4096 frames, 6-level pyramid, 128x128 chunks, mean, "
                         "device-resident",
                dims=[(TIME, 0, 32, 1), (SPACE, 4096, 128, 1), (SPACE, 4096, 128, 1)],
-               dtype=U8, method=MEAN, force_levels=0, batch=128, ring=256),
+               dtype=U8, method=MEAN, force_levels=0, batch=256, ring=256),
     # BASELINE configs[3]: a 256-plane volume, 2x2x2 pyramid (z 256->128->
-    # 64->64, xy 2048->1024->512->256).  With --gpus N rank r owns z slab
+    # 64->64, xy 2048->1024->512->256), one volume per launch (1.7-7% faster
+    # than half a volume on the same stage).  With --gpus N rank r owns z slab
     # [lo, hi) of every volume of the stream (aqz_stage_options z_slab_*,
     # slabs aligned to the 4-plane z groups): its stage receives only those
     # planes, and frame ids skip the other ranks' planes.
@@ -80,11 +84,12 @@ CONFIGS = {
                         "pyramid, 256x256x64 chunks, mean, device-resident",
                dims=[(TIME, 0, 1, 1), (SPACE, 256, 64, 1), (SPACE, 2048, 256, 1),
                      (SPACE, 2048, 256, 1)],
-               dtype=U16, method=MEAN, force_levels=0, batch=128, ring=256),
+               dtype=U16, method=MEAN, force_levels=0, batch=256, ring=512),
+    # 16-frame launches (4 GiB): 1.2-2.7% faster than 8 on the same stage
     "c5": dict(workload="float32 8192x8192 frames, 7-level pyramid, 128x128 chunks, mean, "
                         "device-resident (one camera stream per GPU)",
                dims=[(TIME, 0, 4, 1), (SPACE, 8192, 128, 1), (SPACE, 8192, 128, 1)],
-               dtype=F32, method=MEAN, force_levels=0, batch=8, ring=12),
+               dtype=F32, method=MEAN, force_levels=0, batch=16, ring=16),
 }
 
 

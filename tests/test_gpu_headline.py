@@ -2,8 +2,8 @@
 
 * C2 as benched: u16 2048x2048, 256-px chunks, t-chunk 64, force_levels=5
   (the BASELINE "5-level @ 256-px chunks" geometry; the reference rule
-  stops at 4 levels, downsampler.cpp:512-541), 128-frame launches from a
-  device-resident ring, the bench's layer_slots=2 ring.  Pixels of every
+  stops at 4 levels, downsampler.cpp:512-541), the bench's launch size
+  and chunk-layer ring, from a device-resident ring of frames.  Pixels of every
   level come from the oracle run at 128-px chunks (5 levels by the
   reference rule, the same pixels -- level values do not depend on the
   chunk size) tiled at the forced 256-px level dims.
@@ -94,7 +94,9 @@ def test_bench_c2_configuration_exact(gpu, cfg):
     if c["force_levels"]:  # c2, c2-xy
         odims[-1] = (SPACE, w, 128, 1)
         odims[-2] = (SPACE, h, 128, 1)
-    n = 2 * max(B, 128)
+    # one full launch and a half one: more frames than the ring's slots hold
+    # (9 layers of 64 at B = 512), so every slot is reused once
+    n = B + B // 2
     frames = distinct_frames(n, h, w, 7 + L)
     stored = np.ascontiguousarray(frames.transpose(0, 2, 1)) if xy else frames
     exp, fw, _ = expected_stage_layers(odims, U16, MEAN, stored, level_dims=ldims)
@@ -103,8 +105,8 @@ def test_bench_c2_configuration_exact(gpu, cfg):
     ring = _device_ring(frames)
     F = [st.layout(l)["frames_per_layer"] for l in range(L)]
     done = [0] * L
-    for s in range(n // B):
-        st.append_ptr(ring.data_ptr() + s * B * h * w * 2, B)
+    for s in range(0, n, B):
+        st.append_ptr(ring.data_ptr() + s * h * w * 2, min(B, n - s))
         st.synchronize()
         # check every layer completed by this launch before the 3-slot
         # ring reuses its slot

@@ -189,4 +189,14 @@ cat $O/c2_ab.txt
 STEPS=200 bash tools/profile.sh c2 r05d || exit 1
 }
 
+# C2 / C3 / C5 launch sizes on one stage
+step_p14() {
+O=gpurun_out/r5p14
+mkdir -p $O
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c2 --batch 1024 --knobs 0 --appends 256,512,1024 --instances 2 --reps 10 >> $O/ab.txt 2>&1 || { tail $O/ab.txt; exit 1; }
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c3 --batch 512 --knobs 0 --appends 128,256,512 --instances 2 --reps 10 >> $O/ab.txt 2>&1 || { tail $O/ab.txt; exit 1; }
+timeout -k 10 300 python3 -u tools/knob_ab.py --config c5 --batch 32 --knobs 0 --appends 8,16,32 --instances 2 --reps 10 >> $O/ab.txt 2>&1 || { tail $O/ab.txt; exit 1; }
+cat $O/ab.txt
+}
+
 "step_$@"
