@@ -143,7 +143,19 @@ def fill_ring(torch, ring, dtype, seed):
         ring.view(torch.float32).uniform_(0.0, 65535.0, generator=g)
 
 
-def pmc_traffic(config, pyramid_only, kernel, frames, ring_allocation, run_ms=None):
+def lib_sha256():
+    """sha256 of the libaqz_gpu.so this process loaded (aqz.lib())."""
+    import hashlib
+    import aqz
+    try:
+        with open(aqz.lib()._name, "rb") as fh:
+            return hashlib.sha256(fh.read()).hexdigest()
+    except (OSError, AttributeError):
+        return None
+
+
+def pmc_traffic(config, pyramid_only, kernel, frames, ring_allocation, run_ms=None,
+                lib_sha=None):
     """Per-launch HBM bytes of the dominant kernel from the newest committed
     rocprofv3 PMC summary for this configuration whose rings were allocated
     the same way as this run's (tools/profile.sh -> tools/pmc_summary.py ->
@@ -163,6 +175,9 @@ def pmc_traffic(config, pyramid_only, kernel, frames, ring_allocation, run_ms=No
             found.append((f, d))
     if not found:
         return None, None, None
+    # a profile of the library build this run loaded, when there is one
+    same = [fd for fd in found if lib_sha and fd[1].get("lib_sha256") == lib_sha]
+    found = same or found
     # MI355X boxes run the same kernel at different speeds (DESIGN.md
     # section 5); the bytes do not change with the box.  Of the profiles of
     # this configuration and ring allocation, the one whose kernel time is
@@ -760,7 +775,7 @@ def main():
     # how the chunk-layer rings were allocated (aqz_placement_report.mode)
     pl["ring_allocation"] = ring_allocation(pl)
     traffic, traffic_src, prof = pmc_traffic(args.config, args.pyramid_only, kernel, B,
-                                             pl["ring_allocation"], avg_ms)
+                                             pl["ring_allocation"], avg_ms, lib_sha256())
 
     result = {
         "metric": f"input GB/s, device-resident multiscale downsample, {DTYPE_WORDS[dt]} "
@@ -801,6 +816,8 @@ def main():
         "input_rate_frac_of_peak": round(value / world / HBM_PEAK_GBS, 4),
     }
     if prof:
+        result["roofline"]["traffic_profile_same_build"] = bool(
+            prof.get("lib_sha256") and prof.get("lib_sha256") == lib_sha256())
         # the profiled run of this command: its rocprof kernel average and
         # the frac it gives, next to this run's
         pa = prof.get("steady_avg_duration_ns") or prof.get("avg_duration_ns")

@@ -54,6 +54,11 @@ def main():
     }
     if fpl:
         res["frames_per_launch"] = fpl
+    # the library build that was profiled (bench.py prefers a summary of
+    # the build it runs)
+    shaf = os.path.join(d, "lib.sha256")
+    if os.path.exists(shaf):
+        res["lib_sha256"] = open(shaf).read().strip()
     # the traced bench line: how its rings were allocated (bench.py matches
     # a summary to a run by it) and its own event-timed kernel average
     try:

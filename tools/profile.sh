@@ -18,6 +18,7 @@ NAME=$NAME$NAME_SUFFIX
 OUT=gpurun_out/prof_${TAG}_${NAME}
 mkdir -p $OUT
 echo "python3 bench.py --config $CFG --steps $STEPS --warmup 5 $EXTRA" > $OUT/bench_cmd.txt
+sha256sum acquire-zarr_amd/libaqz_gpu.so | cut -d' ' -f1 > $OUT/lib.sha256
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --config $CFG --steps $STEPS --warmup 5 $EXTRA > $OUT/bench_trace.log 2>&1 || exit 1
 tail -1 $OUT/bench_trace.log
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --config $CFG --steps 5 --warmup 2 $EXTRA > $OUT/bench_fetch.log 2>&1 || exit 2
