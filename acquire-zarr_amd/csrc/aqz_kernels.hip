@@ -839,11 +839,12 @@ fast_pass(const FusedParams& p, uint32_t pass, const uint4& ra, const uint4& rb,
 // launch's regions, so horizontally adjacent regions -- whose level >= 3
 // rows share cache lines -- meet in the same L2 and leave it as whole lines.
 __device__ __forceinline__ uint32_t
-region_of(const FusedParams& p, uint32_t b, uint32_t total)
+region_of_block(const FusedParams& p)
 {
+    const uint32_t b = blockIdx.x;
     if (!p.xcd_order)
         return b;
-    const uint32_t per = total >> 3;
+    const uint32_t per = gridDim.x >> 3;
     if (b >= (per << 3))
         return b;
     const uint32_t x = b & 7u;
@@ -860,12 +861,6 @@ region_of(const FusedParams& p, uint32_t b, uint32_t total)
         i = ((s + u) & p.xskew) * nreg + u;
     }
     return x * per + i;
-}
-
-__device__ __forceinline__ uint32_t
-region_of_block(const FusedParams& p)
-{
-    return region_of(p, blockIdx.x, gridDim.x);
 }
 
 // x * xcd_rot mod (blocks / 8) for the 8 XCDs (region_of_block)
@@ -1217,201 +1212,6 @@ fused_pyramid_strip(const FusedParams p)
         lean_level<T, M, 5, RW>(p, f, y0, x0, lds4, lds5);
     else
         lean_pair<T, M, 5, RW>(p, f, y0, x0, lds4);
-}
-
-// ---------------------------------------------------------------------------
-// fused_pyramid_strip_loop: the strip kernel as a persistent grid (a few
-// workgroups per CU) walking the launch's regions with a stride of the grid
-// (virtual block vb = blockIdx.x + k * gridDim.x, the same XCD-contiguous
-// region order as one block per region when gridDim.x is a multiple of 8).
-// The next region's rows are loaded as soon as this region's level-0 stores
-// and level-1/2 sums no longer need ra/rb, so they are in flight across the
-// level-3+ stores and the flag flushes.  Interior regions, non-XY.
-// ---------------------------------------------------------------------------
-template<typename T, int M, int NTM>
-__global__ __launch_bounds__(256) void
-fused_pyramid_strip_loop(const FusedParams p, uint32_t n_blocks)
-{
-    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-    constexpr int VEC = 16 / sizeof(T);
-    constexpr int HV = VEC / 2;
-    constexpr int QV = VEC / 4;
-    constexpr uint32_t RW = 32 * VEC;
-    static_assert(QV >= 1, "strip kernel needs <= 4-byte pixels");
-    constexpr int N3 = QV >= 2 ? QV / 2 : 1;
-    constexpr int S3 = QV >= 2 ? 1 : 2;
-    constexpr int N4 = N3 >= 2 ? N3 / 2 : 1;
-    constexpr int S4 = N3 >= 2 ? S3 : 2 * S3;
-    __shared__ __attribute__((aligned(16))) T lds4[4 * (RW / 16)];
-    __shared__ __attribute__((aligned(16))) T lds5[2 * (RW / 32)];
-
-    const uint32_t w = threadIdx.x >> 6;
-    const uint32_t hw = (threadIdx.x >> 5) & 1u;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t cv = threadIdx.x & 31u;
-    const uint32_t trow = p.tw * uint32_t(sizeof(T));
-    const uint32_t nf = p.n_fused;
-    const uint32_t ry = 16 * w + 2 * hw;
-    const uint64_t row = uint64_t(p.W[0]) * sizeof(T);
-    const uint32_t nreg = p.nbx_in * p.nby_in;
-
-    uint4 ra[4], rb[4];
-    uint32_t f, y0, x0;
-    auto locate = [&](uint32_t vb, uint32_t& ff, uint32_t& yy, uint32_t& xx) {
-        const uint32_t r = region_of(p, vb, n_blocks);
-        ff = fdiv(r, p.d_nreg_in);
-        uint32_t by, bx;
-        region_xy(p, r - ff * nreg, by, bx, false);
-        yy = by << 6;
-        xx = bx * RW;
-    };
-    auto load = [&](uint32_t ff, uint32_t yy, uint32_t xx) {
-        const uint8_t* s = p.src + uint64_t(ff) * p.src_stride + uint64_t(yy + ry) * row +
-                           uint64_t(xx + cv * VEC) * sizeof(T);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const u32x4v a = gload<(NTM & 1) != 0, u32x4v>(s + uint64_t(4 * i) * row);
-            const u32x4v b = gload<(NTM & 1) != 0, u32x4v>(s + uint64_t(4 * i + 1) * row);
-            ra[i] = uint4{ a.x, a.y, a.z, a.w };
-            rb[i] = uint4{ b.x, b.y, b.z, b.w };
-        }
-    };
-    uint32_t vb = blockIdx.x;
-    if (vb >= n_blocks)
-        return;
-    locate(vb, f, y0, x0);
-    load(f, y0, x0);
-    for (;;) {
-        FastTile t0 = fast_tile<T>(p, 0, f, y0 + ry, x0 + cv * VEC);
-        FastTile t1{}, t2{};
-        if (nf >= 1)
-            t1 = fast_tile<T>(p, 1, f, (y0 >> 1) + 8 * w + hw, (x0 >> 1) + cv * HV);
-        if (nf >= 2)
-            t2 = fast_tile<T>(p, 2, f, (y0 >> 2) + 4 * w, (x0 >> 2) + cv * QV);
-        T q2[4][QV];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (t0.p) {
-                gstore<(NTM & 2) != 0>(t0.p + uint64_t(4 * i) * trow,
-                                       u32x4v{ ra[i].x, ra[i].y, ra[i].z, ra[i].w });
-                gstore<(NTM & 2) != 0>(t0.p + uint64_t(4 * i + 1) * trow,
-                                       u32x4v{ rb[i].x, rb[i].y, rb[i].z, rb[i].w });
-                t0.nz |= ((ra[i].x | ra[i].y | ra[i].z | ra[i].w) |
-                          (rb[i].x | rb[i].y | rb[i].z | rb[i].w)) != 0u;
-            }
-            if (nf < 1)
-                continue;
-            T r0[VEC], r1[VEC], o[HV];
-            __builtin_memcpy(r0, &ra[i], 16);
-            __builtin_memcpy(r1, &rb[i], 16);
-#pragma unroll
-            for (int j = 0; j < HV; ++j)
-                o[j] = reduce4<M, T>(r0[2 * j], r0[2 * j + 1], r1[2 * j], r1[2 * j + 1]);
-            if (t1.p) {
-                gstore_px<T, HV, (NTM & 4) != 0>(t1.p + uint64_t(2 * i) * trow, o);
-                t1.nz |= any_nonzero<T, HV>(o);
-            }
-            if (nf < 2)
-                continue;
-            uint2 mine, below;
-            __builtin_memcpy(&mine, o, 8);
-            below.x = __shfl_xor(mine.x, 32);
-            below.y = __shfl_xor(mine.y, 32);
-            T b[HV];
-            __builtin_memcpy(b, &below, 8);
-#pragma unroll
-            for (int j = 0; j < QV; ++j)
-                q2[i][j] = reduce4<M, T>(o[2 * j], o[2 * j + 1], b[2 * j], b[2 * j + 1]);
-            if (lane < 32 && t2.p) {
-                gstore_px<T, QV, (NTM & 4) != 0>(t2.p + uint64_t(i) * trow, q2[i]);
-                t2.nz |= any_nonzero<T, QV>(q2[i]);
-            }
-        }
-        // the next region's rows, in flight across levels 3+ and the flags
-        const uint32_t nvb = vb + gridDim.x;
-        const bool more = nvb < n_blocks;
-        uint32_t nf_f = 0, ny0 = 0, nx0 = 0;
-        if (more) {
-            locate(nvb, nf_f, ny0, nx0);
-            load(nf_f, ny0, nx0);
-        }
-        flush_tile_flag(t0);
-        flush_tile_flag(t1);
-        flush_tile_flag(t2);
-        if (nf >= 3) {
-            T v3[2][N3];
-#pragma unroll
-            for (int rr = 0; rr < 2; ++rr) {
-                const T* a = q2[2 * rr];
-                const T* c = q2[2 * rr + 1];
-                if constexpr (QV >= 2) {
-#pragma unroll
-                    for (int j = 0; j < N3; ++j)
-                        v3[rr][j] = reduce4<M, T>(a[2 * j], a[2 * j + 1], c[2 * j], c[2 * j + 1]);
-                } else {
-                    const T ar = shfl_down_t(a[0], 1), cr = shfl_down_t(c[0], 1);
-                    v3[rr][0] = reduce4<M, T>(a[0], ar, c[0], cr);
-                }
-            }
-            {
-                const bool valid = lane < 32 && (cv % S3) == 0;
-                FastTile t3{};
-                if (valid)
-                    t3 = fast_tile<T>(p, 3, f, (y0 >> 3) + 2 * w, (x0 >> 3) + (cv / S3) * N3);
-                if (t3.p) {
-#pragma unroll
-                    for (int rr = 0; rr < 2; ++rr) {
-                        gstore_px<T, N3, false>(t3.p + uint64_t(rr) * trow, v3[rr]);
-                        t3.nz |= any_nonzero<T, N3>(v3[rr]);
-                    }
-                }
-                flush_tile_flag(t3);
-            }
-            if (nf >= 4) {
-                T v4[N4];
-                if constexpr (N3 >= 2) {
-#pragma unroll
-                    for (int j = 0; j < N4; ++j)
-                        v4[j] = reduce4<M, T>(v3[0][2 * j], v3[0][2 * j + 1], v3[1][2 * j],
-                                              v3[1][2 * j + 1]);
-                } else {
-                    const T ar = shfl_down_t(v3[0][0], S3), cr = shfl_down_t(v3[1][0], S3);
-                    v4[0] = reduce4<M, T>(v3[0][0], ar, v3[1][0], cr);
-                }
-                const bool valid4 = lane < 32 && (cv % S4) == 0;
-                {
-                    FastTile t4{};
-                    if (valid4)
-                        t4 = fast_tile<T>(p, 4, f, (y0 >> 4) + w, (x0 >> 4) + (cv / S4) * N4);
-                    if (t4.p) {
-                        gstore_px<T, N4, false>(t4.p, v4);
-                        t4.nz |= any_nonzero<T, N4>(v4);
-                    }
-                    flush_tile_flag(t4);
-                }
-                if (nf >= 5) {
-                    // levels 5-6 across the waves, from the level-4 rows in LDS
-                    if (valid4) {
-#pragma unroll
-                        for (int j = 0; j < N4; ++j)
-                            lds4[w * (RW / 16) + (cv / S4) * N4 + j] = v4[j];
-                    }
-                    __syncthreads();
-                    if (nf == 5)
-                        lean_level<T, M, 5, RW>(p, f, y0, x0, lds4, lds5);
-                    else
-                        lean_pair<T, M, 5, RW>(p, f, y0, x0, lds4);
-                    __syncthreads(); // lds4 / lds5 are rewritten by the next region
-                }
-            }
-        }
-        if (!more)
-            break;
-        vb = nvb;
-        f = nf_f;
-        y0 = ny0;
-        x0 = nx0;
-    }
 }
 
 // Edge regions (right column strip, bottom row strip; or every region when
@@ -2433,24 +2233,6 @@ launch_fill_random(void* p, uint64_t bytes, uint64_t seed, hipStream_t stream)
 // workgroups of the 2-D strip kernel per CU (launch_interior)
 constexpr uint32_t kStripWgPerCu = 6;
 
-// compute units of the current device (cached per device ordinal)
-static uint32_t
-n_cus()
-{
-    static uint32_t cache[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
-        return 256;
-    if (!cache[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            n <= 0)
-            n = 256;
-        cache[dev] = uint32_t(n);
-    }
-    return cache[dev];
-}
-
 // The strip kernel takes 64-row interior regions of <= 4-byte pixels when
 // no level 3-4 output goes to scratch; fused_pyramid takes the rest.
 template<typename T, int M>
@@ -2479,17 +2261,6 @@ launch_interior(uint32_t blocks, const FusedParams& p, hipStream_t stream)
             const uint32_t v = (p.knobs >> 13) & 7u;
             const uint32_t per_cu = v == 0 ? kStripWgPerCu : v;
             const uint32_t lds = per_cu > 1 ? (163840u / per_cu - 512u) & ~255u : 0u;
-            if ((p.knobs & 262144u) && p.nt == 7 && (p.knobs & 32u) == 0 &&
-                (p.knobs & 8u) == 0) {
-                // persistent grid: per_cu workgroups on every CU, a multiple
-                // of 8 so each keeps its XCD's region range
-                // (~110 VGPRs: four workgroups per CU are resident)
-                const uint32_t resident = v == 0 ? 4u : v;
-                const uint32_t grid = std::min<uint32_t>(blocks, (n_cus() * resident) & ~7u);
-                hipLaunchKernelGGL((fused_pyramid_strip_loop<T, M, 7>), dim3(grid ? grid : 8),
-                                   dim3(256), 0, stream, p, blocks);
-                return;
-            }
             switch (p.nt) {
                 case 1:
                     hipLaunchKernelGGL((fused_pyramid_strip<T, M, 1>), dim3(blocks),

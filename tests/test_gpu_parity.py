@@ -266,22 +266,6 @@ def test_stage_baseline_configs(gpu, cfg):
     _check_stage(gpu, dims, dt, m, frames, batch=2)
 
 
-@pytest.mark.parametrize("dtype", [U8, U16, F32], ids=lambda d: DTYPE_NAMES[d])
-def test_stage_strip_loop(gpu, dtype):
-    """Tuning knob 262144: the strip kernel as a persistent grid walking the
-    launch's regions (A/B only).  2048 x 2048 frames at 64-px chunks (every
-    fused level down to the LDS levels 5-6, more regions per launch than the
-    grid) and a ragged 300 x 1100 stage, two methods."""
-    for h, w, c, n, batch in ((2048, 2048, 64, 10, 8), (300, 1100, 128, 5, 3)):
-        dims = [(TIME, 0, 4, 1), (SPACE, h, c, 1), (SPACE, w, c, 1)]
-        for m in (MEAN, MAX):
-            frames = _frames(dtype, n, h, w, 13 * m + dtype + h)
-            st = gpu.Stage(dims, dtype, m, knobs=262144)
-            assert st.dominant_kernel() == "fused_pyramid_strip"
-            st.close()
-            _check_stage(gpu, dims, dtype, m, frames, batch=batch, knobs=262144)
-
-
 @pytest.mark.parametrize("nf", [1, 2])
 @pytest.mark.parametrize("dtype", [U8, U16, I16, U32, F32], ids=lambda d: DTYPE_NAMES[d])
 def test_stage_shallow_pyramid_strip(gpu, dtype, nf):

@@ -199,17 +199,4 @@ timeout -k 10 300 python3 -u tools/knob_ab.py --config c5 --batch 32 --knobs 0 -
 cat $O/ab.txt
 }
 
-# the persistent strip kernel (knob 262144; 3 WGs per CU: 286720)
-step_p15() {
-O=gpurun_out/r5p15
-mkdir -p $O
-timeout -k 10 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "strip_loop" > $O/t.txt 2>&1 || { tail -30 $O/t.txt; exit 1; }
-tail -3 $O/t.txt
-for c in "c2 512" "c3 256" "c5 16" "c1 2048"; do
-set -- $c
-timeout -k 10 300 python3 -u tools/knob_ab.py --config $1 --batch $2 --knobs 0,262144,286720 --instances 2 >> $O/ab.txt 2>&1 || { tail $O/ab.txt; exit 1; }
-done
-cat $O/ab.txt
-}
-
 "step_$@"
