@@ -199,4 +199,23 @@ timeout -k 10 300 python3 -u tools/knob_ab.py --config c5 --batch 32 --knobs 0 -
 cat $O/ab.txt
 }
 
+# the final build: GPU suite + smoke, every config's line, the default
+# line, the C2 profile
+step_final() {
+step_full || exit 1
+step_lines ${1:-f} || exit 1
+O=gpurun_out/r5final
+mkdir -p $O
+timeout -k 10 300 python3 -u bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail $O/bench_default.err; exit 1; }
+cat $O/bench_default.json
+STEPS=200 bash tools/profile.sh c2 ${2:-r05f} || exit 1
+}
+
+# final-build profiles of the other configs
+step_profs() {
+for c in c3 c4 c5 c1; do
+STEPS=200 bash tools/profile.sh $c ${1:-r05f} || exit 1
+done
+}
+
 "step_$@"
