@@ -799,7 +799,13 @@ static_assert(kZSub == 4 * kFarThreads, "one parse unit per far step, 4 position
 __device__ __forceinline__ uint32_t
 far_hash(uint32_t lo, uint32_t hi)
 {
-    uint32_t h = lo * 0x9E3779B1u + hi * 0x7FEB352Du;
+    // the two products kept apart: fused into v_mad_u64_u32, their sum took
+    // a 64-bit addend whose undefined high half the allocator could place in
+    // a register a prefetch is loading, and the step waited for that load
+    uint32_t m0 = lo * 0x9E3779B1u, m1 = hi * 0x7FEB352Du;
+    asm volatile("" : "+v"(m0));
+    asm volatile("" : "+v"(m1));
+    uint32_t h = m0 + m1;
     h ^= h >> 15;
     h *= 0x846CA68Bu;
     h ^= h >> 16;
@@ -837,6 +843,88 @@ zstd_far(const ZstdParams p)
     if (slice == 0)
         for (uint32_t i = nkey + t; i < len; i += kFarThreads)
             far[i] = 0;
+    const uint32_t nsteps = (nkey + kZSub - 1) / kZSub;
+    // one step: probe the slice's positions among [i0, i0 + 4) (bytes
+    // [i0, i0 + 8) in a, d), store their candidates, then insert them
+    auto hash4 = [&](uint32_t a, uint32_t d, uint32_t* h) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            h[k] = far_hash(__builtin_amdgcn_alignbyte(d, a, k), (d >> (8 * k)) & 255u);
+    };
+    auto step = [&](uint32_t i0, const uint32_t* h, auto&& store) {
+        bool mine[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t i = i0 + k;
+            mine[k] = i < nkey && (sbits == 0 || (h[k] >> (32u - sbits)) == slice);
+            uint32_t fv = 0;
+            if (mine[k]) {
+                const uint32_t e = T[(h[k] >> bshift) & ((1u << FL) - 1u)];
+                fv = (e != 0 && (e & tmask) == (h[k] & tmask)) ? (e >> TB) : 0u;
+            }
+            store(i, mine[k], fv);
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            if (mine[k])
+                atomicMax(&T[(h[k] >> bshift) & ((1u << FL) - 1u)],
+                          ((i0 + k + 1) << TB) | (h[k] & tmask));
+        __syncthreads();
+    };
+    if ((len & 3u) == 0 && uint64_t(len) * 4 < (uint64_t(1) << 31)) {
+        // Buffer loads and stores: a load past the segment reads 0 and a
+        // store to another slice's position goes to an out-of-range offset
+        // and is dropped, so no memory access sits under a branch and the
+        // compiler's wait before a step's first use of its bytes leaves the
+        // younger loads and the stores in flight.  The bytes are loaded
+        // kFarAhead steps ahead.  (len % 4 == 0: a dword is in or out.)
+        constexpr uint32_t kFarAhead = 4;
+        const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint8_t*>(src), 0, int32_t(len), 0x00020000);
+        const __amdgpu_buffer_rsrc_t fr =
+          __builtin_amdgcn_make_buffer_rsrc(far, 0, int32_t(nkey * 4), 0x00020000);
+        auto ld = [&](uint32_t off) -> uint32_t {
+            return __builtin_amdgcn_raw_buffer_load_b32(sr, int32_t(off), 0, 0);
+        };
+        auto st = [&](uint32_t i, bool m, uint32_t fv) {
+            __builtin_amdgcn_raw_buffer_store_b32(fv, fr, int32_t(m ? 4 * i : 0x80000000u), 0,
+                                                  0);
+        };
+        uint32_t ra[kFarAhead], rd[kFarAhead];
+        // the prologue issues what a step issues (two loads, four stores;
+        // the stores out of range, dropped): the compiler's wait at the loop
+        // head merges this path with the back edge, and a shorter queue here
+        // would make it wait for all but the last step's loads there
+#pragma unroll
+        for (uint32_t u = 0; u < kFarAhead; ++u) {
+            ra[u] = ld(u * kZSub + 4 * t);
+            rd[u] = ld(u * kZSub + 4 * t + 4);
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) // distinct, unmergeable offsets
+                __builtin_amdgcn_raw_buffer_store_b32(0u, fr, int32_t(0x80000000u + 256 * (4 * u + k)),
+                                                      0, 0);
+        }
+        __syncthreads();
+        // whole groups of kFarAhead steps: a step past the segment loads
+        // zeros and stores nothing (no break, so each ra/rd keeps its
+        // register and a load is waited for only where it is used)
+        for (uint32_t s = 0; s < nsteps; s += kFarAhead) {
+#pragma unroll
+            for (uint32_t u = 0; u < kFarAhead; ++u) {
+                const uint32_t i0 = (s + u) * kZSub + 4 * t;
+                // hash first: ra/rd are dead before their next load is
+                // issued into them (no copy at the loop's back edge, which
+                // would wait for the loads of the last steps)
+                uint32_t h[4];
+                hash4(ra[u], rd[u], h);
+                ra[u] = ld(i0 + kFarAhead * kZSub);
+                rd[u] = ld(i0 + kFarAhead * kZSub + 4);
+                step(i0, h, st);
+            }
+        }
+        return;
+    }
     // bytes [i0, i0 + 8) of this thread's step (zero past the segment)
     auto load = [&](uint32_t i0, uint32_t& a, uint32_t& d) {
         if (i0 + 8 <= len) {
@@ -848,6 +936,10 @@ zstd_far(const ZstdParams p)
                 (k < 4 ? a : d) |= uint32_t(src[i0 + k]) << (8 * (k & 3u));
         }
     };
+    auto gst = [&](uint32_t i, bool m, uint32_t fv) {
+        if (m)
+            far[i] = fv;
+    };
     uint32_t a = 0, d = 0;
     if (4 * t < nkey)
         load(4 * t, a, d);
@@ -858,30 +950,8 @@ zstd_far(const ZstdParams p)
         if (i0 + kZSub < nkey)
             load(i0 + kZSub, na, nd);
         uint32_t h[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k)
-            h[k] = far_hash(__builtin_amdgcn_alignbyte(d, a, k), (d >> (8 * k)) & 255u);
-        // probe
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t i = i0 + k;
-            if (i < nkey && (sbits == 0 || (h[k] >> (32u - sbits)) == slice)) {
-                const uint32_t e = T[(h[k] >> bshift) & ((1u << FL) - 1u)];
-                const uint32_t fv = (e != 0 && (e & tmask) == (h[k] & tmask)) ? (e >> TB) : 0u;
-                if (!(p.dbg & 32u)) // A/B: 32 = no far[] stores (frames invalid)
-                    far[i] = fv;
-            }
-        }
-        __syncthreads();
-        // insert
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t i = i0 + k;
-            if (i < nkey && (sbits == 0 || (h[k] >> (32u - sbits)) == slice) && !(p.dbg & 64u))
-                atomicMax(&T[(h[k] >> bshift) & ((1u << FL) - 1u)],
-                          ((i + 1) << TB) | (h[k] & tmask));
-        }
-        __syncthreads();
+        hash4(a, d, h);
+        step(i0, h, gst);
         a = na;
         d = nd;
     }

@@ -218,4 +218,18 @@ STEPS=200 bash tools/profile.sh $c ${1:-r05f} || exit 1
 done
 }
 
+# device zstd: the far-candidate pass (zstd_far) with buffer loads/stores
+step_p16() {
+O=gpurun_out/r5p16
+mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_zstd.py tests/test_gpu_codec.py -m gpu > $O/t.txt 2>&1 || { tail -30 $O/t.txt; exit 1; }
+tail -3 $O/t.txt
+bash tools/prof_zstd3.sh "--codec zstd --shuffle 0 --clevel 3" "--codec blosc-zstd --shuffle 2 --clevel 5" || exit 1
+for a in "--clevel 3" "--clevel 1"; do
+timeout -k 10 200 python3 -u bench.py --steps 16 --warmup 4 --e2e pinned --codec zstd $a --no-cpu-baseline > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+cat $O/tmp.json >> $O/bench_e2e.jsonl
+python3 -c "import json; d=json.load(open('$O/tmp.json')); print('$a', d['value'], d['ms_per_step'])"
+done
+}
+
 "step_$@"
