@@ -232,4 +232,14 @@ python3 -c "import json; d=json.load(open('$O/tmp.json')); print('$a', d['value'
 done
 }
 
+# the shipped library after the zstd_far change: suite + smoke, C2 line + profile
+step_final2() {
+step_full || exit 1
+O=gpurun_out/r5final2
+mkdir -p $O
+timeout -k 10 300 python3 -u bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail $O/bench_default.err; exit 1; }
+cat $O/bench_default.json
+STEPS=200 bash tools/profile.sh c2 ${1:-r05g} || exit 1
+}
+
 "step_$@"
