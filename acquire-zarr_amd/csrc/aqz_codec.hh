@@ -184,6 +184,8 @@ struct ZstdParams
     uint32_t far_tb;        // tag bits of a far table entry (32 - position bits)
     uint32_t far_slices;    // hash slices (workgroups) per segment: 1, 2, 4 or 8
     uint32_t far_log;       // log2 of a slice's table entries (<= kFarLog)
+    uint32_t far_ranges;    // ranges per segment walked in parallel (1, 2, 4, 8;
+                            // each warmed up with the kFarWarm steps before it)
     uint32_t dbg;           // parse A/B switches (bench option zstd_flags; 0 = shipped)
     const uint32_t* flags;  // has_data words (nullptr: every chunk has data)
     uint32_t tag;
@@ -238,6 +240,8 @@ constexpr uint32_t kZHist2 = 28 * 1024;
 // slices camera 1.624 (libzstd level 5: 1.699 / 3.377)
 constexpr uint32_t kFarLog = 15;
 constexpr uint32_t kFarMin = 5;
+// a far range after the first inserts the 1 MiB before it first (no probes)
+constexpr uint32_t kFarWarm = 256; // steps of kZSub bytes
 constexpr uint32_t kZOffMax = (1u << 24) - 4; // largest match distance (aqz_codec.hip zseq_codes)
 // tag bits for a segment of seg_bytes split into `slices` hash slices of
 // 2^far_log entries (0: segments too large for the pass)

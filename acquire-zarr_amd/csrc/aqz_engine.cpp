@@ -2051,6 +2051,18 @@ Compressor::Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compressio
 //                1.983, c-blosc clevel 5 1.974); byte shuffle: none (its
 //                planes lose from longer matches: camera 1.891 -> 1.845)
 // (tools/zstd_lab.cpp far=..., farbatch=4096)
+// compute units of the current device (the far pass's range split)
+static uint64_t
+device_cus()
+{
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+        return 256;
+    return uint64_t(n);
+}
+
 uint32_t
 zstd_far_slices(const Compression& c, uint32_t typesize)
 {
@@ -2219,6 +2231,19 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
             alloc_large(far_, nseg * p.seg_bytes * 4, tune_.vmm);
             p.far = reinterpret_cast<uint32_t*>(far_.p);
             p.phist = 0; // the far candidates cover every earlier unit
+            // A layer of few segments (the small levels' layers) walks each
+            // segment in parallel ranges of >= 1 MiB: a range first inserts
+            // the kFarWarm steps before it, so its positions miss only
+            // candidates further back than that (the sequential walk of one
+            // segment per slice is 2048 dependent steps for 8 MiB, whatever
+            // the layer's size).  Layers that fill the device keep one range.
+            const uint64_t wgs = nseg * p.far_slices;
+            const uint64_t steps = (uint64_t(p.seg_bytes) + kZSub - 1) / kZSub;
+            const uint64_t cus = device_cus();
+            p.far_ranges = 1;
+            while (p.far_ranges < 8 && wgs * p.far_ranges * 2 <= cus &&
+                   steps / (2u * p.far_ranges) >= kFarWarm)
+                p.far_ranges *= 2;
         }
         if (p.match) {
             const uint64_t nu = nblk * kZSubBlocks;
