@@ -242,4 +242,16 @@ cat $O/bench_default.json
 STEPS=200 bash tools/profile.sh c2 ${1:-r05g} || exit 1
 }
 
+# the shipped library: suite + smoke, default line, every configuration's profile
+step_final3() {
+step_full || exit 1
+O=gpurun_out/r5final3
+mkdir -p $O
+timeout -k 10 300 python3 -u bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail $O/bench_default.err; exit 1; }
+cat $O/bench_default.json
+for c in c2 c3 c4 c5 c1; do
+STEPS=200 bash tools/profile.sh $c ${1:-r05h} || exit 1
+done
+}
+
 "step_$@"
