@@ -140,7 +140,7 @@ O=gpurun_out/r5e2e
 mkdir -p $O
 timeout -k 10 400 python3 -u tools/binding_e2e.py --frames 2048 --placement-tries 2 > $O/binding.jsonl 2> $O/binding.err || { tail $O/binding.err; exit 1; }
 cat $O/binding.jsonl
-for a in "--e2e pinned" "--e2e pinned --compress 1" "--e2e pinned --codec zstd" "--e2e pageable"; do
+for a in "--e2e pinned" "--e2e pinned --compress 1" "--e2e pinned --codec zstd" "--e2e pinned --codec zstd --clevel 3" "--e2e pinned --codec blosc-zstd --compress 2" "--e2e pageable"; do
 timeout -k 10 200 python3 -u bench.py --steps 16 --warmup 4 $a > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
 cat $O/tmp.json >> $O/bench_e2e.jsonl
 python3 -c "import json; d=json.load(open('$O/tmp.json')); print(d['metric'][:60], d['value'], d.get('d2h_gbs_per_gpu'))"
