@@ -1619,20 +1619,39 @@ zseq_encode(const TL& tll, const TO& tof, const TM& tml, const uint64_t* sv, uin
     w.add((v >> 17) & 0x1FFFu, zstd::ll_bits(llc));
     w.add((v >> 30) & 0x7FFu, zstd::ml_bits(mlc));
     w.add(v >> 41, ofc);
-    uint64_t nx = n >= 2 ? sv[n - 2] : 0;
-    for (int i = int(n) - 2; i >= 0; --i) {
-        v = nx;
-        if (i > 0)
-            nx = sv[i - 1]; // in flight while this sequence is coded
-        llc = uint32_t(v & 63u);
-        mlc = uint32_t((v >> 6) & 63u);
-        ofc = uint32_t((v >> 12) & 31u);
-        zstd::fse_enc(w, sof, t.of, ofc);
-        zstd::fse_enc(w, sml, t.ml, mlc);
-        zstd::fse_enc(w, sll, t.ll, llc);
-        w.add((v >> 17) & 0x1FFFu, zstd::ll_bits(llc));
-        w.add((v >> 30) & 0x7FFu, zstd::ml_bits(mlc));
-        w.add(v >> 41, ofc);
+    // sequences n-2 .. 0, kSeqAhead at a time: the next group's words are
+    // loaded while this group is coded.  (The bit writer's stores sit under
+    // branches, so the compiler waits for every store before a loaded word is
+    // used: one wait per group, not one per sequence.)  Indices below 0 load
+    // word 0 and are not coded.
+    constexpr int kSeqAhead = 8;
+    uint64_t cur[kSeqAhead], nxt[kSeqAhead];
+    int hi = int(n) - 2;
+#pragma unroll
+    for (int u = 0; u < kSeqAhead; ++u)
+        cur[u] = sv[max(hi - u, 0)];
+    for (; hi >= 0; hi -= kSeqAhead) {
+#pragma unroll
+        for (int u = 0; u < kSeqAhead; ++u)
+            nxt[u] = sv[max(hi - kSeqAhead - u, 0)];
+#pragma unroll
+        for (int u = 0; u < kSeqAhead; ++u) {
+            if (hi - u < 0)
+                break;
+            v = cur[u];
+            llc = uint32_t(v & 63u);
+            mlc = uint32_t((v >> 6) & 63u);
+            ofc = uint32_t((v >> 12) & 31u);
+            zstd::fse_enc(w, sof, t.of, ofc);
+            zstd::fse_enc(w, sml, t.ml, mlc);
+            zstd::fse_enc(w, sll, t.ll, llc);
+            w.add((v >> 17) & 0x1FFFu, zstd::ll_bits(llc));
+            w.add((v >> 30) & 0x7FFu, zstd::ml_bits(mlc));
+            w.add(v >> 41, ofc);
+        }
+#pragma unroll
+        for (int u = 0; u < kSeqAhead; ++u)
+            cur[u] = nxt[u];
     }
     zstd::fse_flush(w, sml, t.ml);
     zstd::fse_flush(w, sof, t.of);
