@@ -254,4 +254,10 @@ STEPS=200 bash tools/profile.sh $c ${1:-r05h} || exit 1
 done
 }
 
+# the shipped library: final3 (suite, default line, profiles), then the e2e rows
+step_final4() {
+step_final3 ${1:-r05i} || exit 1
+step_e2e || exit 1
+}
+
 "step_$@"
