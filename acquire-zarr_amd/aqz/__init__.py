@@ -81,6 +81,7 @@ class StageBenchOptionsC(C.Structure):
 
 # zstd_flags bits of aqz_stage_bench_options
 ZSTD_LITERALS_ONLY, ZSTD_NO_FAR, ZSTD_NO_FIT = 1, 2, 4
+ZSTD_FAR_ONE_RANGE = 1 << 21  # A/B: no parallel far ranges
 BENCH_FIELDS = tuple(f for f, _ in StageBenchOptionsC._fields_ if f != "reserved")
 
 

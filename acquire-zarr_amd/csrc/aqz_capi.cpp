@@ -536,6 +536,7 @@ apply_bench(const aqz_stage_bench_options* bench, StageOptions& o)
     o.codec.phist = (z >> 8) & 0xffu;
     o.codec.parse = (z >> 16) & 0xfu;
     o.codec.vmm = (z >> 20) & 1u;
+    o.codec.ranges = (z & (1u << 21)) ? 0 : 1;
 }
 
 static void

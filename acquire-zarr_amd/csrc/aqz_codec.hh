@@ -185,7 +185,8 @@ struct ZstdParams
     uint32_t far_slices;    // hash slices (workgroups) per segment: 1, 2, 4 or 8
     uint32_t far_log;       // log2 of a slice's table entries (<= kFarLog)
     uint32_t far_ranges;    // ranges per segment walked in parallel (1, 2, 4, 8;
-                            // each warmed up with the kFarWarm steps before it)
+                            // each warmed up with the far_warm steps before it)
+    uint32_t far_warm;      // steps a range after the first inserts first
     uint32_t dbg;           // parse A/B switches (bench option zstd_flags; 0 = shipped)
     const uint32_t* flags;  // has_data words (nullptr: every chunk has data)
     uint32_t tag;
@@ -240,7 +241,9 @@ constexpr uint32_t kZHist2 = 28 * 1024;
 // slices camera 1.624 (libzstd level 5: 1.699 / 3.377)
 constexpr uint32_t kFarLog = 15;
 constexpr uint32_t kFarMin = 5;
-// a far range after the first inserts the 1 MiB before it first (no probes)
+// a far range after the first inserts at least the 1 MiB before it first (no
+// probes), and at least two of the chunk's planes (the previous planes are
+// where camera data repeats)
 constexpr uint32_t kFarWarm = 256; // steps of kZSub bytes
 constexpr uint32_t kZOffMax = (1u << 24) - 4; // largest match distance (aqz_codec.hip zseq_codes)
 // tag bits for a segment of seg_bytes split into `slices` hash slices of

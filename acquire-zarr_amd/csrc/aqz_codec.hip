@@ -793,8 +793,8 @@ zchunk_skip(const ZstdParams& p, uint32_t c)
 // the current one is probed.  The slices of one segment run on one XCD
 // (their far[] stores interleave in the same lines).  The parse verifies
 // every candidate.  A layer of few segments splits each into p.far_ranges
-// ranges walked at once: a range first inserts the kFarWarm steps before it
-// without probing, so it misses only candidates further back than that
+// ranges walked at once: a range first inserts the p.far_warm steps before
+// it without probing, so it misses only candidates further back than that
 // (e2e zstd level 3: 22.5 -> 28.4 GB/s, the same bytes to 4 digits).
 constexpr uint32_t kFarThreads = 1024;
 static_assert(kZSub == 4 * kFarThreads, "one parse unit per far step, 4 positions a thread");
@@ -905,7 +905,7 @@ zstd_far(const ZstdParams p)
         // this workgroup's range of steps [s1, s2), warmed up from s0
         const uint32_t per = (nsteps + R - 1) / R;
         const uint32_t s1 = min(range * per, nsteps), s2 = min(s1 + per, nsteps);
-        const uint32_t s0 = s1 > kFarWarm ? s1 - kFarWarm : 0u;
+        const uint32_t s0 = s1 > p.far_warm ? s1 - p.far_warm : 0u;
         const uint32_t iwarm = s0 * kZSub, ibeg = s1 * kZSub, iend = min(s2 * kZSub, nkey);
         uint32_t ra[kFarAhead], rd[kFarAhead];
         // the prologue issues what a step issues (two loads, four stores;

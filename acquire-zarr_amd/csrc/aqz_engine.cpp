@@ -2232,17 +2232,20 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
             p.far = reinterpret_cast<uint32_t*>(far_.p);
             p.phist = 0; // the far candidates cover every earlier unit
             // A layer of few segments (the small levels' layers) walks each
-            // segment in parallel ranges of >= 1 MiB: a range first inserts
-            // the kFarWarm steps before it, so its positions miss only
-            // candidates further back than that (the sequential walk of one
-            // segment per slice is 2048 dependent steps for 8 MiB, whatever
-            // the layer's size).  Layers that fill the device keep one range.
+            // segment in parallel ranges, each at least as long as its
+            // warm-up: a range first inserts the 1 MiB and the two chunk
+            // planes before it, so its positions miss only candidates
+            // further back than that (the sequential walk of one segment per
+            // slice is 2048 dependent steps for 8 MiB, whatever the layer's
+            // size).  Layers that fill the device keep one range.
             const uint64_t wgs = nseg * p.far_slices;
             const uint64_t steps = (uint64_t(p.seg_bytes) + kZSub - 1) / kZSub;
             const uint64_t cus = device_cus();
+            const uint64_t warm = std::max<uint64_t>(kFarWarm, (2 * plane_bytes_ + kZSub - 1) / kZSub);
+            p.far_warm = uint32_t(std::min<uint64_t>(warm, steps));
             p.far_ranges = 1;
-            while (p.far_ranges < 8 && wgs * p.far_ranges * 2 <= cus &&
-                   steps / (2u * p.far_ranges) >= kFarWarm)
+            while (tune_.ranges && p.far_ranges < 8 && wgs * p.far_ranges * 2 <= cus &&
+                   steps / (2u * p.far_ranges) >= warm)
                 p.far_ranges *= 2;
         }
         if (p.match) {
@@ -2463,6 +2466,7 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
         hip_check(hipStreamSynchronize(cs), "hipStreamSynchronize");
         hip_check(hipStreamSynchronize(d2h_), "hipStreamSynchronize");
         L.comp = std::make_unique<Compressor>(L.bpc, uint32_t(bpp_), c, opt_.codec);
+        L.comp->set_plane_bytes(uint64_t(L.tw) * L.th * bpp_);
         L.comp_cfg = c;
     }
     ensure_comp_slots(L);

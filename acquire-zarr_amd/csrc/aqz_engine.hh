@@ -129,6 +129,7 @@ struct CodecTuning
     uint32_t vmm = 0;      // 1: buffers >= 64 MiB (codec work buffers, layer
                            // frames, H2D staging) from 2 MiB virtual-memory
                            // pieces, as the rings (A/B)
+    uint32_t ranges = 1;   // 0: the far pass walks every segment as one range
 };
 
 // Device frames of arrays of equally sized device chunks (aqz_codec.hip):
@@ -159,6 +160,9 @@ class Compressor
              const uint32_t* flags, uint32_t tag, uint8_t* out, uint64_t* offsets,
              hipStream_t stream, const uint32_t* order = nullptr);
     const BloscGeom& geom() const { return g_; }
+    // bytes of one plane (a frame's tile) of a chunk: the far pass's ranged
+    // walk warms up over at least two of them (0: unknown)
+    void set_plane_bytes(uint64_t b) { plane_bytes_ = b; }
     uint64_t chunk_bytes() const { return nbytes_; }
     // the blosc block size recorded in the frames (0: plain zstd)
     uint32_t blocksize() const
@@ -192,6 +196,7 @@ class Compressor
     Compression c_;
     CodecTuning tune_;
     uint64_t nbytes_ = 0;
+    uint64_t plane_bytes_ = 0;
     uint32_t typesize_ = 1;
     BloscGeom g_{};
     bool store_only_;

@@ -51,7 +51,8 @@ typedef struct
                                   16-19 parse variants; bit 20: codec work
                                   buffers, layer frames and H2D staging of
                                   >= 64 MiB from 2 MiB virtual-memory
-                                  pieces, as the rings */
+                                  pieces, as the rings; bit 21: the far
+                                  pass walks every segment as one range */
     uint32_t ring_malloc_flags; /* 0 = shipped: rings of >= 256 MiB in all
                                    are packed into one arena of 2 MiB
                                    virtual-memory pieces (hipMemCreate +

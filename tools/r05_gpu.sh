@@ -222,7 +222,7 @@ done
 step_p16() {
 O=gpurun_out/r5p16
 mkdir -p $O
-timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_zstd.py tests/test_gpu_codec.py -m gpu > $O/t.txt 2>&1 || { tail -30 $O/t.txt; exit 1; }
+timeout -k 10 600 python3 -u -m pytest -x -q -s --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_zstd.py tests/test_gpu_codec.py -m gpu > $O/t.txt 2>&1 || { tail -30 $O/t.txt; exit 1; }
 tail -3 $O/t.txt
 bash tools/prof_zstd3.sh "--codec zstd --shuffle 0 --clevel 3" "--codec blosc-zstd --shuffle 2 --clevel 5" || exit 1
 for a in "--clevel 3" "--clevel 1"; do
