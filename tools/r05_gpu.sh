@@ -260,4 +260,15 @@ step_final3 ${1:-r05i} || exit 1
 step_e2e || exit 1
 }
 
+# e2e codec rows only (stream-priority A/B)
+step_p17() {
+O=gpurun_out/r5p17
+mkdir -p $O
+for a in "--e2e pinned --codec zstd --clevel 3" "--e2e pinned --codec blosc-zstd --compress 2" "--e2e pinned --compress 1" "--e2e pinned --codec zstd" "--e2e pinned"; do
+timeout -k 10 200 python3 -u bench.py --steps 16 --warmup 4 $a --no-cpu-baseline > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+cat $O/tmp.json >> $O/bench_e2e.jsonl
+python3 -c "import json; d=json.load(open('$O/tmp.json')); print('$a', d['value'], d['ms_per_step'], d.get('sink_bytes_per_input_byte'))"
+done
+}
+
 "step_$@"
