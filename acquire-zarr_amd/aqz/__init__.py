@@ -109,7 +109,7 @@ class PlacementReportC(C.Structure):
                 ("kept_ms_final", C.c_double), ("peak_device_bytes", C.c_uint64),
                 ("probe_bus_gbs", C.c_double), ("expected_ms", C.c_double),
                 ("alg_bytes", C.c_uint64), ("accepted", C.c_uint32),
-                ("reserved", C.c_uint32), ("probe_gbs", C.c_double * 32)]
+                ("stop", C.c_uint32), ("probe_gbs", C.c_double * 32)]
 
 
 class MemoryUsageC(C.Structure):
@@ -795,6 +795,8 @@ class Stage:
                 "probe_bus_gbs": round(r.probe_bus_gbs, 1),
                 "expected_ms": round(r.expected_ms, 5), "alg_bytes": r.alg_bytes,
                 "accepted": bool(r.accepted),
+                "stop": {1: "accepted", 2: "every try ran", 3: "no expectation (probe too small)",
+                         4: "out of memory"}.get(r.stop, "no search"),
                 "candidates_probe_gbs": [round(r.probe_gbs[i], 1)
                                          for i in range(min(32, r.n))]}
 

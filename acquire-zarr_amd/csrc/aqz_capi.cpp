@@ -933,6 +933,7 @@ aqz_stage_placement_report(const aqz_stage* st, aqz_placement_report* out)
     out->expected_ms = r.expected_ms;
     out->alg_bytes = r.alg_bytes;
     out->accepted = r.accepted ? 1u : 0u;
+    out->stop = r.stop;
     for (size_t i = 0; i < r.probe_gbs.size() && i < 32; ++i)
         out->probe_gbs[i] = r.probe_gbs[i];
     return AQZ_STATUS_SUCCESS;

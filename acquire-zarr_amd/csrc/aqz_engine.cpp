@@ -696,7 +696,11 @@ Stage::calibrate_placement()
     };
     // The copy-third probe over the random frames into the candidate's
     // memory (the arena, or the largest ring): every variant, best of 3
-    // groups of 4 launches each; the best variant's bus GB/s.
+    // groups of 4 launches each; the best variant's bus GB/s.  A stage
+    // without the level-0 split (1 read : 1/3 write) takes the read-third
+    // probe, its own shape.
+    const bool third_only = opt_.skip_level0_split;
+    const double bus_per_read = third_only ? 4.0 / 3.0 : 7.0 / 3.0;
     auto probe = [&]() {
         DevBuf* dst = &arena_;
         if (!arena)
@@ -708,11 +712,12 @@ Stage::calibrate_placement()
             return 0.0;
         double best = 0;
         for (int v = 0; v < kPlacementProbeVariants; ++v) {
-            hip_check(launch_probe_copy_third(src.p, dst->p, rd, stream_, v), "probe launch");
+            hip_check(launch_probe_copy_third(src.p, dst->p, rd, stream_, v, third_only),
+                      "probe launch");
             for (int g = 0; g < 3; ++g) {
                 hip_check(hipEventRecord(a, stream_), "hipEventRecord");
                 for (int r = 0; r < 4; ++r)
-                    hip_check(launch_probe_copy_third(src.p, dst->p, rd, stream_, v),
+                    hip_check(launch_probe_copy_third(src.p, dst->p, rd, stream_, v, third_only),
                               "probe launch");
                 hip_check(hipEventRecord(b, stream_), "hipEventRecord");
                 const double ms = elapsed() / 4;
@@ -720,7 +725,7 @@ Stage::calibrate_placement()
                     best = ms;
             }
         }
-        return best > 0 ? double(rd) * (7.0 / 3.0) / (best * 1e-3) / 1e9 : 0.0;
+        return best > 0 ? double(rd) * bus_per_read / (best * 1e-3) / 1e9 : 0.0;
     };
     struct Placement
     {
@@ -739,7 +744,9 @@ Stage::calibrate_placement()
     };
     auto fresh = [&]() {
         if (arena) {
-            arena_.alloc(arena_rings_ + opt_.ring_arena, kArenaFlags);
+            // the same kind of memory as candidate 0 (the constructor's flags)
+            arena_.alloc(arena_rings_ + opt_.ring_arena,
+                         opt_.ring_malloc_flags ? opt_.ring_malloc_flags : kArenaFlags);
             place_rings_at(0);
         } else {
             for (size_t k = 0; k < lv_.size(); ++k)
@@ -784,6 +791,9 @@ Stage::calibrate_placement()
             }
             rep.accepted = rep.expected_ms > 0 && !opt_.placement_never_accept &&
                            best_ms <= (1.0 + kPlacementTolerance) * rep.expected_ms;
+            rep.stop = rep.accepted ? 1u
+                       : (rep.expected_ms == 0 && !opt_.placement_never_accept) ? 3u
+                                                                               : 2u;
             if (rep.accepted || t + 1 == tries ||
                 (rep.expected_ms == 0 && !opt_.placement_never_accept))
                 break;
@@ -792,6 +802,7 @@ Stage::calibrate_placement()
         if (e.status != 6 || rep.ms.empty()) // out of memory: keep the best so far
             throw;
         (void)hipGetLastError();
+        rep.stop = 4;
     }
     hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
     {

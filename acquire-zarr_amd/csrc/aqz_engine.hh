@@ -46,12 +46,13 @@ hipError_t launch_zero_frame_tiles(uint8_t* fb, uint64_t bpc,
                                    hipStream_t stream);
 // aqz_probe.hip: the copy-third streaming shape (1 read : 4/3 write) of
 // read_bytes from src into dst (>= 4/3 read_bytes + one workgroup's block),
-// variant 0-2 (kPlacementProbeVariants); the largest read size a source and
-// destination of these sizes take (0 = too small)
+// variant 0-2 (kPlacementProbeVariants); third_only: the read-third shape
+// (1 read : 1/3 write) of a stage without the level-0 split.  The largest
+// read size a source and destination of these sizes take (0 = too small)
 constexpr int kPlacementProbeVariants = 3;
 uint64_t probe_copy_third_read_bytes(uint64_t src_bytes, uint64_t dst_bytes);
 hipError_t launch_probe_copy_third(const uint8_t* src, uint8_t* dst, uint64_t read_bytes,
-                                   hipStream_t stream, int variant);
+                                   hipStream_t stream, int variant, bool third_only = false);
 
 void hip_check(hipError_t e, const char* what);
 
@@ -271,6 +272,8 @@ struct PlacementReport
     double expected_ms = 0;       // the batch's algorithmic bytes at that rate
     uint64_t alg_bytes = 0;       // algorithmic bytes of one timing launch
     bool accepted = false;        // the kept one is within the tolerance
+    uint32_t stop = 0;            // 1 accepted, 2 every try ran, 3 no
+                                  // expectation (probe too small), 4 OOM
 };
 
 // a candidate within this fraction over the probe's expectation ends the

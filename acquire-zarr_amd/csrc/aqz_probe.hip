@@ -105,12 +105,14 @@ probe_copy_third_read_bytes(uint64_t src_bytes, uint64_t dst_bytes)
 // The stage's own bus shape (1 read : 4/3 write) from src into dst: dst
 // receives the copy and behind it the third.  variant 0: nontemporal
 // stores, 96 B per lane in flight; 1: the same with 192 B; 2: plain stores.
-// The placement search (Stage::calibrate_placement) takes the best of them
-// over its random frames and the candidate's rings: the practical ceiling
-// of this shape in that memory, at the stage's launch size.
+// third_only: the pyramid-only shape (1 read : 1/3 write, a stage without
+// the level-0 split), the third at dst.  The placement search
+// (Stage::calibrate_placement) takes the best of them over its random frames
+// and the candidate's rings: the practical ceiling of the stage's shape in
+// that memory, at the stage's launch size.
 hipError_t
 launch_probe_copy_third(const uint8_t* src, uint8_t* dst, uint64_t read_bytes,
-                        hipStream_t stream, int variant)
+                        hipStream_t stream, int variant, bool third_only)
 {
     const uint64_t per_wg = uint64_t(variant == 1 ? kUDeep : kU) * 256 * 16;
     const uint64_t grid = read_bytes / per_wg;
@@ -118,9 +120,19 @@ launch_probe_copy_third(const uint8_t* src, uint8_t* dst, uint64_t read_bytes,
         return hipErrorInvalidValue;
     const auto* in = reinterpret_cast<const u32x4*>(src);
     auto* o = reinterpret_cast<u32x4*>(dst);
-    auto* o3 = reinterpret_cast<u32x4*>(dst + read_bytes);
+    auto* o3 = reinterpret_cast<u32x4*>(third_only ? dst : dst + read_bytes);
     const dim3 g{ uint32_t(grid), 1, 1 };
-    if (variant == 1)
+    if (third_only) {
+        if (variant == 1)
+            hipLaunchKernelGGL((probe_stream<AQZ_PROBE_READ_THIRD, true, kUDeep>), g, dim3(256),
+                               0, stream, in, o, o3, nullptr);
+        else if (variant == 2)
+            hipLaunchKernelGGL((probe_stream<AQZ_PROBE_READ_THIRD, false>), g, dim3(256), 0,
+                               stream, in, o, o3, nullptr);
+        else
+            hipLaunchKernelGGL((probe_stream<AQZ_PROBE_READ_THIRD, true>), g, dim3(256), 0,
+                               stream, in, o, o3, nullptr);
+    } else if (variant == 1)
         hipLaunchKernelGGL((probe_stream<AQZ_PROBE_COPY_THIRD, true, kUDeep>), g, dim3(256), 0,
                            stream, in, o, o3, nullptr);
     else if (variant == 2)

@@ -848,7 +848,8 @@ def main():
         # channels at least as well as a copy loop does.
         result["roofline"]["probe_same_shape_gbs"] = pg[pl["kept"]]
         result["roofline"]["probe_same_shape_source"] = (
-            "copy-third streaming kernels over the kept rings' memory at this launch size "
+            ("read-third" if args.pyramid_only else "copy-third") +
+            " streaming kernels over the kept rings' memory at this launch size "
             "(aqz_placement_report.probe_gbs)")
         result["roofline"]["frac_of_probe_same_shape"] = round(achieved / pg[pl["kept"]], 4)
     if probe:
@@ -877,6 +878,18 @@ def main():
                 "kernel_input_frac_of_probe": round(
                     B * side["fbytes"] / (side["avg_ms"] * 1e-3) / 1e9 / pr, 4),
                 "probe_source": "hbm_probe.read_third_input_gbs"})
+        spl = side["placement"]
+        spg = spl.get("candidates_probe_gbs") or []
+        if spl.get("kept", 0) < len(spg) and spg[spl["kept"]] > 0:
+            # the read-third probe (1 read : 1/3 write) over this stage's own
+            # kept rings, from the random frames, at this launch size: the
+            # same-memory reference rate of the pyramid-only shape
+            result["pyramid_only"].update({
+                "probe_same_memory_bus_gbs": spg[spl["kept"]],
+                "kernel_frac_of_probe_same_memory": round(
+                    side["achieved"] / spg[spl["kept"]], 4),
+                "placement_candidates_ms": spl.get("candidates_ms"),
+                "placement_kept": spl.get("kept")})
     if per_rank:
         result["per_rank"] = per_rank
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

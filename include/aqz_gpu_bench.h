@@ -94,14 +94,19 @@ typedef struct
     double kept_ms_final;       /* the kept placement re-timed alone, after
                                    the others were freed */
     uint64_t peak_device_bytes; /* the stage's device bytes at the search's peak */
-    double probe_bus_gbs;       /* the copy-third probe (1 read : 4/3 write)
+    double probe_bus_gbs;       /* the probe of the stage's bus shape -- copy-
+                                   third (1 read : 4/3 write), or read-third
+                                   (1 : 1/3) without the level-0 split --
                                    streaming the random frames into the first
                                    candidate's memory, bus GB/s (0 = not run) */
     double expected_ms;         /* alg_bytes at probe_bus_gbs */
     uint64_t alg_bytes;         /* algorithmic bytes of one timing launch */
     uint32_t accepted;          /* 1: the kept candidate is within 3% of
                                    expected_ms (the search stopped there) */
-    uint32_t reserved;
+    uint32_t stop;              /* why the search stopped: 1 accepted, 2 every
+                                   try ran, 3 no expectation (the probe's
+                                   source or memory too small), 4 out of
+                                   memory (the best so far kept) */
     double probe_gbs[32];       /* the probe over each candidate's memory */
 } aqz_placement_report;
 aqz_status aqz_stage_placement_report(const aqz_stage* st, aqz_placement_report* out);

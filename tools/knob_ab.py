@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--instances", type=int, default=3)
     ap.add_argument("--knobs", default="0,512,256")
     ap.add_argument("--nt", type=int, default=7)
+    ap.add_argument("--nts", default="", help="nontemporal policies to cross with --knobs")
+    ap.add_argument("--pyramid-only", action="store_true",
+                    help="stages without the level-0 split (skip_level0_split)")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--placement-tries", type=int, default=0)
     ap.add_argument("--xy", action="store_true", help="XY-transposed storage order")
@@ -40,16 +43,19 @@ def main():
     # (two batches of frames: >= 2 GiB at the bench's batch sizes, past the
     # 256 MiB MALL)
     knobs = [int(x) for x in args.knobs.split(",")]
+    nts = [int(x) for x in args.nts.split(",")] if args.nts else [args.nt]
+    variants = [(k, t) for k in knobs for t in nts]
     nd = len(c["dims"])
     xy = dict(storage_order=list(range(nd - 2)) + [nd - 1, nd - 2]) if args.xy else {}
     for inst in range(args.instances):
         st = aqz.Stage(c["dims"], c["dtype"], c["method"], max_batch_frames=B,
                        layer_slots=bench.layer_slots_for(c, B), force_levels=c["force_levels"],
-                       placement_tries=args.placement_tries, **xy)
+                       placement_tries=args.placement_tries,
+                       skip_level0_split=args.pyramid_only, **xy)
         row = []
         for rnd in range(2):
-            for j, k in enumerate(knobs):
-                st.set_tuning(k, args.nt)
+            for j, (k, nt) in enumerate(variants):
+                st.set_tuning(k, nt)
                 for i in range(2):
                     st.append_ptr(src.data_ptr() + (i % 2) * B * fbytes, B)
                 st.synchronize()
@@ -81,7 +87,7 @@ def main():
                     best[a] = min(best.get(a, ms), ms)
             extra = " " + " ".join(f"append{a}={v:.4f}" for a, v in best.items())
         print(f"{args.config} B{B} inst{inst} {st.placement()['candidates_ms']} " +
-              " ".join(f"k{k}={v:.4f}" for k, v in zip(knobs, row)) + extra, flush=True)
+              " ".join(f"k{k}/nt{t}={v:.4f}" for (k, t), v in zip(variants, row)) + extra, flush=True)
         st.close()
 
 

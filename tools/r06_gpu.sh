@@ -1,0 +1,61 @@
+#!/usr/bin/env bash
+# Round-6 GPU runs, one function per gpurun call (the profiles/r06_* files
+# come from these):  gpurun -- bash tools/r06_gpu.sh <step> [args]
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+
+# the whole GPU suite + smoke
+step_full() {
+O=gpurun_out/r6full
+mkdir -p $O
+timeout -k 10 1000 python3 -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1; rc=$?
+tail -15 $O/pytest.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
+cat $O/smoke.log
+}
+
+# some GPU test files (names after the step)
+step_tests() {
+O=gpurun_out/r6t
+mkdir -p $O
+timeout -k 10 900 python3 -u -m pytest "$@" -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1; rc=$?
+tail -25 $O/pytest.log
+[ $rc -eq 0 ] || exit 1
+}
+
+# the default bench line
+step_default() {
+O=gpurun_out/r6default${1:-}
+mkdir -p $O
+timeout -k 10 300 python3 -u bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail $O/bench_default.err; exit 1; }
+cat $O/bench_default.json
+}
+
+# rocprof trace + PMC of one bench configuration (tools/profile.sh CFG TAG [pyr])
+step_prof() {
+STEPS=${STEPS:-200} bash tools/profile.sh "$@" || exit 1
+}
+
+# start of round: suite + smoke, default line, C2 pyramid-only profile
+step_base() {
+step_full || exit 1
+step_default || exit 1
+NO_SQ=${NO_SQ:-} STEPS=200 bash tools/profile.sh c2 r06 pyr || exit 1
+}
+
+# pyramid-only: occupancy cap x nontemporal policy on one stage; the
+# pyramid-only bench line with its same-memory read-third probe
+step_p1() {
+O=gpurun_out/r6p1
+mkdir -p $O
+timeout -k 10 400 python3 -u tools/knob_ab.py --config c2 --pyramid-only --knobs 0,8192,32768,40960,57344 --nts 7,1,0 --instances 2 > $O/pyr_ab.txt 2>&1 || { tail $O/pyr_ab.txt; exit 1; }
+cat $O/pyr_ab.txt
+for i in 1 2; do
+timeout -k 10 200 python3 -u bench.py --pyramid-only --steps 50 --warmup 5 --no-cpu-baseline --no-hbm-probe > $O/pyr$i.json 2> $O/pyr$i.err || { tail $O/pyr$i.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/pyr$i.json')); r=d['roofline']; p=r['placement']; print(json.dumps({'frac': r['frac'], 'ms': r['kernel_avg_ms'], 'cand': p['candidates_ms'], 'kept': p['kept'], 'exp': p['expected_ms'], 'probe': p['probe_bus_gbs'], 'stop': p.get('stop'), 'fop': r.get('frac_of_probe_same_shape')}))"
+done
+}
+
+"step_$@"
