@@ -63,7 +63,7 @@ class StageOptionsC(C.Structure):
     _fields_ = [("layer_slots", C.c_uint32), ("max_batch_frames", C.c_uint32),
                 ("first_frame", C.c_uint64), ("z_slab_begin", C.c_uint32),
                 ("z_slab_end", C.c_uint32), ("placement_tries", C.c_uint32),
-                ("reserved", C.c_uint32)]
+                ("level0_split_on_host", C.c_uint32)]
 
 
 class StageBenchOptionsC(C.Structure):
@@ -200,6 +200,9 @@ def lib():
         "aqz_dims_skipped_internal_indices": ([vp, u32, u32, C.POINTER(u32), sz,
                                                C.POINTER(sz)], i32),
         "aqz_pyramid_levels": ([D, sz, u32, C.POINTER(u32), D, sz], i32),
+        "aqz_dims_split_frame_rows": ([vp, vp, u64, u32, u32, u32, vp, sz, vp, sz], i32),
+        "aqz_stage_split_level0_host": ([vp, vp, u64, u64, u32, vp, sz, vp, sz], i32),
+        "aqz_stage_split_level0_rows": ([vp, vp, u64, u32, u32, vp, u32, vp, sz, vp, sz], i32),
         "aqz_dims_dim1_banding": ([vp, C.POINTER(i32), C.POINTER(u32), C.POINTER(u64),
                                    C.POINTER(u32)], i32),
         "aqz_downsampling_method_name": ([i32], C.c_char_p),
@@ -398,6 +401,20 @@ class Dims:
                                                        C.byref(n)), "skipped_internal")
         return list(out[:n.value])
 
+    def split_frame_rows(self, frame, frame_id, dst, has_data, row_begin=0, row_end=None,
+                         chunk0=0):
+        """aqz_dims_split_frame_rows: rows [row_begin, row_end) of one frame
+        (numpy, acquisition order) into the packed chunks [chunk0, ...) of a
+        layer (numpy uint8 dst, has_data)."""
+        frame = np.ascontiguousarray(frame)
+        if row_end is None:
+            row_end = frame.shape[-2] if frame.ndim >= 2 else 0
+        assert dst.dtype == np.uint8 and has_data.dtype == np.uint8
+        _check(lib().aqz_dims_split_frame_rows(self.h, frame.ctypes.data, frame_id, row_begin,
+                                               row_end, chunk0, dst.ctypes.data, dst.nbytes,
+                                               has_data.ctypes.data, has_data.size),
+               "aqz_dims_split_frame_rows")
+
     def dim1_banding(self):
         """(supported, n_bands, frames_per_band, chunks_per_band)"""
         a, b, c, d = C.c_int32(), C.c_uint32(), C.c_uint64(), C.c_uint32()
@@ -423,13 +440,14 @@ def downsampling_metadata_json(method):
 
 def estimate_memory(dims, dtype, method, max_levels=0, layer_slots=0,
                     max_batch_frames=0, storage_order=None, placement_tries=0,
-                    **bench):
+                    level0_split_on_host=False, **bench):
     """aqz_stage_estimate_memory: upper bound of a stage's footprint (no GPU),
     including the placement search's creation peak when placement_tries > 1.
     With bench-header options (force_levels, skip_level0_split,
     placement_reps, ...), aqz_stage_estimate_memory_bench."""
     d, keep = _desc(dims, dtype, method, max_levels, True, storage_order, 0)
-    o = StageOptionsC(layer_slots, max_batch_frames, 0, 0, 0, placement_tries)
+    o = StageOptionsC(layer_slots, max_batch_frames, 0, 0, 0, placement_tries,
+                      int(bool(level0_split_on_host)))
     m = MemoryUsageC()
     b = _bench_options(bench)
     if b is not None:
@@ -587,13 +605,13 @@ class Stage:
     def __init__(self, dims, dtype, method, max_levels=0, multiscale=True,
                  storage_order=None, device=0, layer_slots=0,
                  max_batch_frames=0, first_frame=0, z_slab=None,
-                 placement_tries=0, **bench):
+                 placement_tries=0, level0_split_on_host=False, **bench):
         self.dtype = dtype
         d, self._keep = _desc(dims, dtype, method, max_levels, multiscale,
                               storage_order, device)
         zb, ze = z_slab if z_slab else (0, 0)
         o = StageOptionsC(layer_slots, max_batch_frames, first_frame, zb, ze,
-                          placement_tries)
+                          placement_tries, int(bool(level0_split_on_host)))
         h = C.c_void_p()
         b = _bench_options(bench)
         if b is not None:
@@ -709,6 +727,23 @@ class Stage:
 
     def frames_written(self, level):
         return lib().aqz_stage_frames_written(self.h, level)
+
+    def split_level0_host(self, frames_ptr, n_frames, first_frame, dst_ptr, cap, has_ptr,
+                          has_cap, chunk0=0):
+        """aqz_stage_split_level0_host: level-0 frames [first_frame, +n) (host
+        memory at frames_ptr) tile-split by the stage's host threads into the
+        packed chunks [chunk0, ...) of one layer at dst_ptr (host)."""
+        _check(lib().aqz_stage_split_level0_host(self.h, frames_ptr, n_frames, first_frame,
+                                                 chunk0, dst_ptr, cap, has_ptr, has_cap),
+               "split_level0_host")
+
+    def split_level0_rows(self, frame_ptr, frame_id, row_begin, row_end, dst_ptr, cap,
+                          has_ptr, has_cap, chunk0=0, frame_copy_ptr=None):
+        """aqz_stage_split_level0_rows: rows of one level-0 frame, this thread
+        (and, with frame_copy_ptr, the same rows copied there)."""
+        _check(lib().aqz_stage_split_level0_rows(self.h, frame_ptr, frame_id, row_begin,
+                                                 row_end, frame_copy_ptr, chunk0, dst_ptr, cap,
+                                                 has_ptr, has_cap), "split_level0_rows")
 
     def frames_consumed(self):
         """Level-0 frames whose source bytes have been read (reusable)."""

@@ -378,6 +378,25 @@ aqz_dims_dim1_banding(const aqz_dims* d, int32_t* supported, uint32_t* n_bands,
 }
 
 aqz_status
+aqz_dims_split_frame_rows(const aqz_dims* d, const void* frame, uint64_t frame_id,
+                          uint32_t row_begin, uint32_t row_end, uint32_t chunk0, void* dst,
+                          size_t cap, uint8_t* has_data, size_t has_data_cap)
+{
+    if (!d || !frame || !dst || !has_data)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard([&] {
+        const ArrayDimensions& a = *d->ad;
+        const uint64_t n = std::min<uint64_t>(cap / a.bytes_per_chunk(), has_data_cap);
+        if (n == 0 || chunk0 >= a.number_of_chunks_in_memory())
+            throw Error(1, "destination holds no chunk of the layer");
+        split_rows(split_geom(a, frame_id), static_cast<const uint8_t*>(frame), row_begin,
+                   row_end, static_cast<uint8_t*>(dst), chunk0,
+                   uint32_t(std::min<uint64_t>(n, a.number_of_chunks_in_memory() - chunk0)),
+                   has_data);
+    });
+}
+
+aqz_status
 aqz_pyramid_levels(const aqz_dimension* dims, size_t ndims, uint32_t max_levels,
                    uint32_t* n_levels, aqz_dimension* out_dims, size_t out_cap)
 {
@@ -514,7 +533,7 @@ apply_bench(const aqz_stage_bench_options* bench, StageOptions& o)
     if (!bench)
         return;
     o.force_levels = bench->force_levels;
-    o.skip_level0_split = bench->skip_level0_split != 0;
+    o.skip_level0_split = o.skip_level0_split || bench->skip_level0_split != 0;
     if (bench->placement_tries)
         o.placement_tries = bench->placement_tries;
     if (bench->placement_reps)
@@ -550,6 +569,8 @@ apply_options(const aqz_stage_options* opt, StageOptions& o)
     o.z_slab_begin = opt->z_slab_begin;
     o.z_slab_end = opt->z_slab_end;
     o.placement_tries = opt->placement_tries;
+    o.level0_on_host = opt->level0_split_on_host != 0;
+    o.skip_level0_split = o.skip_level0_split || o.level0_on_host;
 }
 
 static aqz_status
@@ -866,6 +887,34 @@ aqz_status
 aqz_stage_finalize(aqz_stage* st)
 {
     return guard_sticky(st, [&] { st->st->finalize(); });
+}
+
+// host work only (no GPU call): not sticky, any thread
+aqz_status
+aqz_stage_split_level0_host(aqz_stage* st, const void* frames, uint64_t n_frames,
+                            uint64_t first_frame, uint32_t chunk0, void* dst, size_t cap,
+                            uint8_t* has_data, size_t has_data_cap)
+{
+    if (!st || !st->st)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard([&] {
+        st->st->split_level0_host(frames, n_frames, first_frame, chunk0, dst, cap, has_data,
+                                  has_data_cap);
+    });
+}
+
+aqz_status
+aqz_stage_split_level0_rows(const aqz_stage* st, const void* frame, uint64_t frame_id,
+                            uint32_t row_begin, uint32_t row_end, void* frame_copy,
+                            uint32_t chunk0, void* dst, size_t cap, uint8_t* has_data,
+                            size_t has_data_cap)
+{
+    if (!st || !st->st)
+        return AQZ_STATUS_INVALID_ARGUMENT;
+    return guard([&] {
+        st->st->split_level0_rows(frame, frame_id, row_begin, row_end, frame_copy, chunk0, dst,
+                                  cap, has_data, has_data_cap);
+    });
 }
 
 aqz_status

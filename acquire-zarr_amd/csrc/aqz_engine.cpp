@@ -291,6 +291,8 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         opt_.layer_slots = 2;
     if (opt_.max_batch_frames == 0)
         opt_.max_batch_frames = 64;
+    if (opt_.level0_on_host)
+        opt_.skip_level0_split = true;
 
     auto base = std::make_unique<ArrayDimensions>(desc.dims, desc.dtype,
                                                   desc.storage_order);
@@ -298,6 +300,9 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         // Array::write_frame_to_chunks_ transposes the acquired frame
         // (array.cpp:525-533) and the downsampler sees the transposed frame
         // (multiscale.array.cpp:66-72): every level works in storage order
+        if (opt_.level0_on_host)
+            throw Error(9, "level0_split_on_host needs storage rows = acquisition rows "
+                           "(no XY-transposed storage order)");
         xy_ = true;
         const size_t nd = desc.dims.size();
         acq_rows_ = desc.dims[nd - 2].array_size_px;
@@ -1634,7 +1639,7 @@ Stage::copy_layer(uint32_t level, uint64_t layer, void* dst, size_t cap,
         throw Error(3, "level out of range");
     StageLevel& L = lv_[level];
     if (!L.ring.p)
-        throw Error(1, "level 0 split disabled for this stage");
+        throw Error(1, "level 0 is not split on the device by this stage");
     const uint32_t slot = uint32_t(layer % L.n_slots);
     if (L.slot_layer[slot] != int64_t(layer))
         throw Error(3, "chunk layer not resident");
@@ -1667,7 +1672,7 @@ Stage::copy_layer_async(uint32_t level, uint64_t layer, void* dst, size_t cap,
         throw Error(3, "level out of range");
     StageLevel& L = lv_[level];
     if (!L.ring.p)
-        throw Error(1, "level 0 split disabled for this stage");
+        throw Error(1, "level 0 is not split on the device by this stage");
     const uint32_t slot = uint32_t(layer % L.n_slots);
     if (L.slot_layer[slot] != int64_t(layer))
         throw Error(3, "chunk layer not resident");
@@ -1725,7 +1730,7 @@ Stage::copy_band_async(uint32_t level, uint64_t layer, uint32_t band, void* dst,
         throw Error(3, "level out of range");
     StageLevel& L = lv_[level];
     if (!L.ring.p)
-        throw Error(1, "level 0 split disabled for this stage");
+        throw Error(1, "level 0 is not split on the device by this stage");
     int32_t ok = 0;
     uint32_t nb = 1, cpb = L.n_chunks;
     uint64_t fpb = L.F;
@@ -2464,7 +2469,7 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
     // workgroups and latency-bound)
     const hipStream_t cs = comp_stream(L);
     if (!L.ring.p)
-        throw Error(1, "level 0 split disabled for this stage");
+        throw Error(1, "level 0 is not split on the device by this stage");
     const uint32_t slot = uint32_t(layer % L.n_slots);
     if (L.slot_layer[slot] != int64_t(layer))
         throw Error(3, "chunk layer not resident");
@@ -2597,7 +2602,7 @@ Stage::import_frames(Stage* src, uint32_t level, uint64_t layer, uint32_t first,
         throw Error(3, "level out of range");
     StageLevel& L = lv_[level];
     if (!L.ring.p)
-        throw Error(1, "level 0 split disabled for this stage");
+        throw Error(1, "level 0 is not split on the device by this stage");
     if (uint64_t(first) + count > L.F)
         throw Error(3, "frames outside the chunk layer");
     StageLevel* S = nullptr;
@@ -2672,6 +2677,58 @@ Stage::finalize()
     }
     finalized_ = true;
     synchronize();
+}
+
+static unsigned
+split_workers()
+{
+    if (const char* s = std::getenv("AQZ_SPLIT_THREADS"))
+        return unsigned(std::max(0, std::atoi(s)));
+    // 16 threads in all: a GPU's share of a node's cores (the reference
+    // splits with OpenMP over all of them, array.cpp:575)
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    return std::min(15u, hw / 2);
+}
+
+void
+Stage::split_level0_rows(const void* frame, uint64_t frame_id, uint32_t row_begin,
+                         uint32_t row_end, void* frame_copy, uint32_t chunk0, void* dst,
+                         size_t cap, uint8_t* has_data, size_t has_data_cap) const
+{
+    const StageLevel& L = lv_[0];
+    if (!frame || !dst || !has_data)
+        throw Error(1, "null frame, destination or has_data");
+    const uint64_t n = std::min<uint64_t>(cap / L.bpc, has_data_cap);
+    if (n == 0 || chunk0 >= L.n_chunks)
+        throw Error(1, "destination holds no chunk of the layer");
+    split_rows(split_geom(*L.ad, frame_id), static_cast<const uint8_t*>(frame), row_begin,
+               row_end, static_cast<uint8_t*>(dst), chunk0,
+               uint32_t(std::min<uint64_t>(n, L.n_chunks - chunk0)), has_data,
+               static_cast<uint8_t*>(frame_copy));
+}
+
+void
+Stage::split_level0_host(const void* frames, uint64_t n, uint64_t first, uint32_t chunk0,
+                         void* dst, size_t cap, uint8_t* has_data, size_t has_data_cap)
+{
+    if (n == 0)
+        return;
+    if (!frames)
+        throw Error(1, "null frames");
+    const StageLevel& L = lv_[0];
+    const uint64_t fbytes = uint64_t(L.W) * L.H * bpp_;
+    // tasks of 64 rows (256 KiB of a 2048-px u16 frame), frame-major
+    constexpr uint32_t kRows = 64;
+    const uint32_t per_frame = parts_along(L.H, kRows);
+    if (!split_pool_)
+        split_pool_ = std::make_unique<SplitPool>(split_workers(), numa_cpus_);
+    const auto* src = static_cast<const uint8_t*>(frames);
+    split_pool_->run(size_t(n) * per_frame, [&](size_t i) {
+        const uint64_t f = i / per_frame;
+        const uint32_t r0 = uint32_t(i % per_frame) * kRows;
+        split_level0_rows(src + f * fbytes, first + f, r0, std::min(L.H, r0 + kRows), nullptr,
+                          chunk0, dst, cap, has_data, has_data_cap);
+    });
 }
 
 void

@@ -11,6 +11,7 @@
 #include "aqz_codec.hh"
 #include "aqz_copy.hh"
 #include "aqz_geometry.hh"
+#include "aqz_hostsplit.hh"
 #include "aqz_hostzstd.hh"
 #include "aqz_params.hh"
 
@@ -228,6 +229,9 @@ struct StageOptions
     uint32_t max_batch_frames = 64;
     uint32_t force_levels = 0;
     bool skip_level0_split = false;
+    // aqz_stage_options.level0_split_on_host: no level-0 split on the device
+    // (implies skip_level0_split); the caller splits level 0 on the host
+    bool level0_on_host = false;
     uint64_t first_frame = 0;
     uint32_t z_slab_begin = 0, z_slab_end = 0; // aqz_stage_options
     // creation-time placement search (aqz_stage_options.placement_tries;
@@ -426,6 +430,15 @@ class Stage
     void shard_geometry(uint32_t level, uint32_t* chunks_per_shard, uint32_t* n_shards,
                         uint32_t* layers_per_shard) const;
     void finalize();
+    // the level-0 tile split on the host (level0_on_host; aqz_hostsplit.hh):
+    // frames [first, first + n) over the stage's host threads, or rows of
+    // one frame on the calling thread, into the packed chunks [chunk0,
+    // chunk0 + cap / bytes_per_chunk) of a layer
+    void split_level0_host(const void* frames, uint64_t n, uint64_t first, uint32_t chunk0,
+                           void* dst, size_t cap, uint8_t* has_data, size_t has_data_cap);
+    void split_level0_rows(const void* frame, uint64_t frame_id, uint32_t row_begin,
+                           uint32_t row_end, void* frame_copy, uint32_t chunk0, void* dst,
+                           size_t cap, uint8_t* has_data, size_t has_data_cap) const;
     // z-slab assembly: frames [first, first + count) of `layer` of `level`
     // (layer-local frame ids) copied from src's resident layer -- or zeroed
     // when src is null -- with their has_data, after the work enqueued so far
@@ -517,6 +530,7 @@ class Stage
     }
     std::unique_ptr<CopyPool> pool_;
     std::unique_ptr<TaskPool> zpool_; // host zstd workers
+    std::unique_ptr<SplitPool> split_pool_; // host level-0 split workers
     // CPUs of the device's NUMA node: the host pools run there (AQZ_NUMA=0
     // turns it off)
     std::vector<int> numa_cpus_;

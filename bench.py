@@ -308,8 +308,16 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
     # keeps 128-frame batches: a 2-batch pinned source ring of 2 GiB)
     dt, bpp = cfg["dtype"], BPP[cfg["dtype"]]
     B = args.batch or min(cfg["batch"], 128)
+    codec = {"none": 0, "lz4": 1, "blosc-zstd": 2, "zstd": 3}[args.codec]
+    # a raw hand-off splits level 0 on the host from the frames it holds
+    # (H2D 1x, D2H 1/3x of the input instead of 4/3x)
+    host0 = args.level0_split == "host" or (args.level0_split == "auto" and not codec)
+    if host0 and codec:
+        sys.exit("--level0-split host needs a raw hand-off (the codecs compress level 0 "
+                 "on the device)")
     st = aqz.Stage(cfg["dims"], dt, cfg["method"], force_levels=cfg["force_levels"],
-                   max_batch_frames=B, layer_slots=2, device=dev.index, **args.tune)
+                   max_batch_frames=B, layer_slots=2, device=dev.index,
+                   level0_split_on_host=host0, **args.tune)
     L = st.n_levels()
     sizes = level_sizes(st)
     fbytes = sizes[0][0] * sizes[0][1] * bpp
@@ -323,7 +331,6 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
         src_arr = np.empty(src_frames * fbytes, dtype=np.uint8)
         src_ptr, mem = src_arr.ctypes.data, aqz.MEM_HOST
     rng = np.random.default_rng(7 + rank)
-    codec = {"none": 0, "lz4": 1, "blosc-zstd": 2, "zstd": 3}[args.codec]
     host_zstd = os.environ.get("AQZ_ZSTD_HOST", "0") not in ("", "0")
     if codec:
         # compressible camera-like frames (smooth background + noise)
@@ -358,10 +365,31 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
     # blosc clevel 5; --clevel overrides
     clevel = args.clevel if args.clevel >= 0 else (1 if codec == 3 else 5)
 
+    appended = [0]
+
+    def split_level0(ptr):
+        """Level 0 of the batch at ptr, split on the host into the layer
+        buffers (the stage's host threads, next to the device)."""
+        F = lay[0]["frames_per_layer"]
+        f, end = appended[0], appended[0] + B
+        while f < end:
+            layer = f // F
+            hi = min(end, (layer + 1) * F)
+            i = layer % 4
+            if f % F == 0:
+                hd[0][i].array[...] = 0
+            st.split_level0_host(ptr + (f - appended[0]) * fbytes, hi - f, f, dst[0][i].ptr,
+                                 lbytes[0], hd[0][i].ptr, hd[0][i].nbytes)
+            if hi % F == 0:
+                out_bytes[0] += lbytes[0]
+                handed[0] += 1
+            f = hi
+        appended[0] = end
+
     def hand_off():
         if codec:
             drain_compressed()  # last step's layers: their kernels are done by now
-        for l in range(L):
+        for l in range(1 if host0 else 0, L):
             done = st.frames_written(l) // lay[l]["frames_per_layer"]
             while handed[l] < done:
                 i = handed[l] % 4
@@ -377,7 +405,10 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
                 handed[l] += 1
 
     def step(s):
-        st.append_ptr(src_ptr + (s % 2) * B * fbytes, B, mem)
+        ptr = src_ptr + (s % 2) * B * fbytes
+        st.append_ptr(ptr, B, mem)
+        if host0:
+            split_level0(ptr)  # overlaps the batch's H2D and kernels
         hand_off()
 
     for s in range(args.warmup):
@@ -414,7 +445,9 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
                       3: ("D2H -> host zstd of every chunk layer" if host_zstd
                           else "device zstd compression -> D2H of every compressed chunk "
                           "layer")}[codec]
-                     if codec else "D2H of every chunk layer"),
+                     if codec else ("level 0 tile-split on the host, D2H of every chunk "
+                                    "layer of levels >= 1" if host0
+                                    else "D2H of every chunk layer")),
         "value": round(world * in_bytes / el / 1e9, 3), "unit": "GB/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el * 1e3 / args.steps, 3), "higher_is_better": True,
@@ -429,6 +462,7 @@ def run_e2e(torch, aqz, dev, cfg, args, world, rank, dist):
         "frames_per_s_per_gpu": round(args.steps * B / el, 1),
         "host_threads": {"numa_node": affinity[0], "pinned_cpus": affinity[1]},
         "d2h_bytes_per_input_byte": round(d2h[0] / in_bytes, 4),
+        "level0_split": "host" if host0 else "device",
         "sink_bytes_per_input_byte": round(out_bytes[0] / in_bytes, 4),
     }
 
@@ -578,6 +612,10 @@ def main():
                     help="end-to-end mode: frames start in host memory (pinned or "
                          "pageable), every completed chunk layer is handed back to "
                          "pinned host buffers (DESIGN.md 'End to end')")
+    ap.add_argument("--level0-split", choices=["auto", "host", "device"], default="auto",
+                    help="e2e: where level 0 is tile-split (auto: on the host for a raw "
+                         "hand-off, aqz_stage_options.level0_split_on_host; on the device "
+                         "when the layers are compressed there)")
     ap.add_argument("--clevel", type=int, default=-1,
                     help="e2e compression level (default: zstd 1, blosc 5)")
     ap.add_argument("--xy", action="store_true",

@@ -268,7 +268,19 @@ typedef struct
                                   batch of random frames and a second ring
                                   set) is in aqz_stage_estimate_memory.
                                   0/1 = none. */
-    uint32_t reserved;
+    uint32_t level0_split_on_host; /* 1: the device does not tile-split level
+                                  0 (no level-0 ring in HBM); the caller
+                                  splits level 0 on the host from the frames
+                                  it holds (aqz_stage_split_level0_host /
+                                  _rows): a raw hand-off
+                                  then moves H2D 1x and D2H 1/3x of the input
+                                  instead of D2H 4/3x.  Level-0 hand-off calls
+                                  (copy_layer*, copy_band_async,
+                                  compress_layer, device_layer,
+                                  import_frames) return
+                                  AQZ_STATUS_INVALID_ARGUMENT.  Not with an
+                                  XY-transposed storage order
+                                  (AQZ_STATUS_INVALID_SETTINGS). */
 } aqz_stage_options;
 
 typedef struct
@@ -551,6 +563,45 @@ uint32_t aqz_compressor_blocksize(const aqz_compressor* c);
  * buffers Array::write_frame_to_chunks_ fills (array.cpp:507-622). */
 aqz_status aqz_stage_import_frames(aqz_stage* dst, aqz_stage* src, uint32_t level,
                                    uint64_t layer, uint32_t first, uint32_t count);
+
+/* ---- level-0 tile split on the host (aqz_stage_options.
+ * level0_split_on_host) ---------------------------------------------------
+ * Array::write_frame_to_chunks_ (array.cpp:537-619) with
+ * Chunk::write_tile_rows (chunk.cpp:17-58), run by the host on frames it
+ * holds: tile t of level-0 frame f goes to chunk t + tile_group_offset(f)
+ * of f's chunk layer, its rows at chunk_internal_offset(f) +
+ * r * tile_cols * bpp (f transposed to storage order first,
+ * array.cpp:557-566); ragged padding is not written; has_data[c] becomes 1
+ * once a copied byte of chunk c is nonzero and is never cleared (zero it
+ * when a layer starts).  dst holds the packed chunks [chunk0, chunk0 +
+ * cap / bytes_per_chunk) of one layer -- the whole layer (chunk0 0), or a
+ * dim-1 band (chunk0 = band * chunks_per_band) -- laid out as
+ * aqz_stage_copy_layer_async / _band_async would write them; has_data has
+ * has_data_cap >= that many bytes.  Every tile of every frame must fall in
+ * that range (else AQZ_STATUS_INVALID_ARGUMENT).  Pure host work: no GPU
+ * call, any thread. */
+/* Frames [first_frame, first_frame + n_frames) (level-0 frame ids, in
+ * acquisition order, frame after frame at `frames`), split by the stage's
+ * host threads (on the NUMA node of its device). */
+aqz_status aqz_stage_split_level0_host(aqz_stage* st, const void* frames, uint64_t n_frames,
+                                       uint64_t first_frame, uint32_t chunk0, void* dst,
+                                       size_t cap, uint8_t* has_data, size_t has_data_cap);
+/* Rows [row_begin, row_end) of one level-0 frame, on the calling thread;
+ * several threads may split disjoint rows of one frame at once.  frame_copy
+ * (NULL: none): the same rows are also copied to this frame-sized buffer in
+ * the same pass -- the hand-off's copy into its pinned batch
+ * (ZarrStream_append's one copy, frame.queue.cpp:37-39). */
+aqz_status aqz_stage_split_level0_rows(const aqz_stage* st, const void* frame,
+                                       uint64_t frame_id, uint32_t row_begin,
+                                       uint32_t row_end, void* frame_copy, uint32_t chunk0,
+                                       void* dst, size_t cap, uint8_t* has_data,
+                                       size_t has_data_cap);
+/* The same split over an aqz_dims (the array's acquisition dims with its
+ * storage order), no stage and no GPU. */
+aqz_status aqz_dims_split_frame_rows(const aqz_dims* d, const void* frame, uint64_t frame_id,
+                                     uint32_t row_begin, uint32_t row_end, uint32_t chunk0,
+                                     void* dst, size_t cap, uint8_t* has_data,
+                                     size_t has_data_cap);
 
 /* Zero the not-yet-written frames of every level's last partial layer so
  * it can be flushed (the reference's lazily zeroed chunks, chunk.cpp:8-15).

@@ -283,7 +283,24 @@ struct HandoffOptions
     uint32_t host_slots = 3;    // host unit buffers per level (>= 1)
     uint32_t copy_threads = 8;  // threads copying frames into the batch
     aqz_compression comp{};     // codec 0: raw chunk units
+    // Raw units only: level 0 is tile-split on the host by the copy threads
+    // in the same pass that copies each frame into the pinned batch (the
+    // stages are created with aqz_stage_options.level0_split_on_host): only
+    // levels >= 1 cross PCIe back.
+    bool level0_on_host = false;
 };
+
+// Whether an array takes the host split of level 0 (HandoffOptions::
+// level0_on_host, aqz_stage_options.level0_split_on_host): a raw hand-off
+// of an array whose storage rows are its acquisition rows.
+inline bool
+level0_on_host_for(const aqz_array_desc& desc, const aqz_compression& comp)
+{
+    const size_t nd = desc.dimension_count;
+    const bool xy = desc.storage_dimension_order && nd >= 2 &&
+                    desc.storage_dimension_order[nd - 1] != nd - 1;
+    return comp.codec == AQZ_CODEC_NONE && !xy;
+}
 
 // AQZ_DEVICE (a deployment setting read where the reference configures an
 // array, zarr.stream.cpp:1231-1279; no ABI change):
@@ -499,6 +516,9 @@ class Handoff
             // a compressed unit is a whole layer (the device compresses
             // layers); raw units follow the reference's dim-1 bands
             L.compressed = opt_.comp.codec != AQZ_CODEC_NONE;
+            L.host = l == 0 && opt_.level0_on_host;
+            if (L.host && L.compressed)
+                status_ = worse(status_, AQZ_STATUS_INVALID_ARGUMENT);
             if (L.compressed || !banded) {
                 L.n_bands = 1;
                 L.frames_per_band = L.lay.frames_per_layer;
@@ -523,8 +543,23 @@ class Handoff
                 status_ = worse(status_, aqz_host_alloc(cap, reinterpret_cast<void**>(&s->buf)));
                 status_ = worse(status_, aqz_host_alloc(L.chunks_per_band,
                                                         reinterpret_cast<void**>(&s->has)));
+                // the host split never writes ragged padding (chunk.cpp:8-15):
+                // it must start zero
+                if (L.host && s->buf)
+                    std::memset(s->buf, 0, cap);
                 s->ent.resize(L.chunks_per_band);
                 L.slots.push_back(std::move(s));
+            }
+            if (L.host) {
+                // a ragged last dim-1 band leaves internal positions that
+                // the other bands fill: its slot is cleared when a full
+                // band used it last
+                L.ragged_last_band =
+                  L.n_bands > 1 &&
+                  L.lay.frames_per_layer - uint64_t(L.n_bands - 1) * L.frames_per_band <
+                    L.frames_per_band;
+                rows_ = L.lay.height;
+                row_bytes_ = L.lay.height ? L.lay.frame_bytes / L.lay.height : 0;
             }
         }
         const uint32_t nt = std::max<uint32_t>(1, opt_.copy_threads);
@@ -601,10 +636,23 @@ class Handoff
             if (s != AQZ_STATUS_SUCCESS)
                 return status_ = s;
         }
-        copy_frame_(in.buf[in.cur] + size_t(in.n) * frame_bytes_, frame);
+        Level* L0 = levels_.empty() || !levels_[0].host ? nullptr : &levels_[0];
+        if (L0) {
+            const aqz_status s = begin_host_unit_();
+            if (s != AQZ_STATUS_SUCCESS)
+                return status_ = s;
+        }
+        copy_frame_(in.buf[in.cur] + size_t(in.n) * frame_bytes_, frame, L0);
+        if (split_err_ != AQZ_STATUS_SUCCESS)
+            return status_ = split_err_;
         ++in.n;
         ++in.appended;
         ++accepted_;
+        if (L0 && accepted_ == host_.hi) {
+            const aqz_status s = deliver_host_unit_(true);
+            if (s != AQZ_STATUS_SUCCESS)
+                return status_ = s;
+        }
         if (in.n == opt_.batch_frames || run_end)
             return append_batch_(r);
         // units whose copies landed meanwhile go to the sink now
@@ -626,6 +674,11 @@ class Handoff
         }
         for (aqz_stage* st : st_) {
             const aqz_status s = aqz_stage_finalize(st);
+            if (s != AQZ_STATUS_SUCCESS)
+                return status_ = s;
+        }
+        if (!levels_.empty() && levels_[0].host) {
+            const aqz_status s = close_host_layer_();
             if (s != AQZ_STATUS_SUCCESS)
                 return status_ = s;
         }
@@ -657,6 +710,7 @@ class Handoff
         std::vector<aqz_chunk_entry> ent;
         std::atomic<int> pins{ 0 };
         bool busy = false; // compressing, or its copy in flight
+        bool padding_clean = true; // host split: ragged padding is zero
     };
     struct Level
     {
@@ -665,6 +719,8 @@ class Handoff
         uint32_t n_bands = 1, chunks_per_band = 0;
         uint64_t frames_per_band = 0;
         uint32_t planes = 0; // z planes of the level (slab mode)
+        bool host = false;   // level 0 split on the host (level0_on_host)
+        bool ragged_last_band = false;
         uint64_t layer = 0;  // next unit to hand off: (layer, band)
         uint32_t band = 0;
         std::vector<std::unique_ptr<Slot>> slots;
@@ -692,11 +748,18 @@ class Handoff
     }
 
     // ---- frame copy into the pinned batch, split over copy_threads ----------
-    void copy_frame_(uint8_t* dst, const void* src)
+    // With the host split of level 0 (split != null) each thread also splits
+    // the rows it copied, from the caller's frame while they are in cache.
+    void copy_frame_(uint8_t* dst, const void* src, Level* split)
     {
         const size_t nt = copiers_.size() + 1;
+        csplit_ = split;
         if (nt == 1 || frame_bytes_ < (size_t(1) << 20)) {
-            std::memcpy(dst, src, frame_bytes_);
+            cdst_ = dst;
+            csrc_ = static_cast<const uint8_t*>(src);
+            copy_rows_(0, split ? rows_ : 0);
+            if (!split)
+                std::memcpy(dst, src, frame_bytes_);
             return;
         }
         {
@@ -714,11 +777,37 @@ class Handoff
     void copy_part_(uint32_t t)
     {
         const size_t nt = copiers_.size() + 1;
+        if (csplit_) {
+            const uint32_t per = uint32_t((rows_ + nt - 1) / nt);
+            const uint32_t a = std::min<uint32_t>(rows_, per * t);
+            copy_rows_(a, std::min<uint32_t>(rows_, a + per));
+            return;
+        }
         const size_t per = (frame_bytes_ / nt + 4095) & ~size_t(4095);
         const size_t a = std::min(frame_bytes_, per * t);
         const size_t b = std::min(frame_bytes_, a + per);
         if (b > a)
             std::memcpy(cdst_ + a, csrc_ + a, b - a);
+    }
+    // rows [a, b) of the frame: copied into the batch and split into the
+    // current level-0 unit in one pass (the library's streaming copy)
+    void copy_rows_(uint32_t a, uint32_t b)
+    {
+        if (b > a)
+            split_host_rows_(csrc_, accepted_, a, b, cdst_);
+    }
+    void split_host_rows_(const uint8_t* frame, uint64_t fid, uint32_t r0, uint32_t r1,
+                          uint8_t* frame_copy = nullptr)
+    {
+        Level& L = levels_[0];
+        Slot& slot = *L.slots[host_.slot];
+        const aqz_status s = aqz_stage_split_level0_rows(
+          st_[0], frame, fid, r0, r1, frame_copy, host_.band * L.chunks_per_band, slot.buf,
+          slot.cap, slot.has, L.chunks_per_band);
+        if (s != AQZ_STATUS_SUCCESS) {
+            std::lock_guard<std::mutex> lk(emu_);
+            split_err_ = s;
+        }
     }
     void copier_(uint32_t t)
     {
@@ -735,6 +824,101 @@ class Handoff
             if (--cleft_ == 0)
                 cdone_cv_.notify_one();
         }
+    }
+
+    // ---- level 0 split on the host ------------------------------------------------
+    // The unit (layer, band) frame accepted_ belongs to gets a host slot when
+    // its first frame arrives; it is handed to the sink as soon as its last
+    // frame is split (no copy to wait for).
+    struct HostUnit
+    {
+        bool open = false;
+        uint32_t slot = 0, band = 0;
+        uint64_t layer = 0, lo = 0, hi = 0;
+    };
+
+    aqz_status begin_host_unit_()
+    {
+        if (host_.open)
+            return AQZ_STATUS_SUCCESS;
+        Level& L = levels_[0];
+        const uint64_t F = L.lay.frames_per_layer;
+        const uint32_t si = L.next;
+        const aqz_status s = take_slot_(*L.slots[si]);
+        if (s != AQZ_STATUS_SUCCESS)
+            return s;
+        Slot& slot = *L.slots[si];
+        host_.open = true;
+        host_.slot = si;
+        host_.layer = L.layer;
+        host_.band = L.band;
+        host_.lo = L.layer * F + uint64_t(L.band) * L.frames_per_band;
+        host_.hi = L.layer * F + std::min<uint64_t>((uint64_t(L.band) + 1) * L.frames_per_band, F);
+        const bool ragged = L.ragged_last_band && L.band + 1 == L.n_bands;
+        if (ragged && !slot.padding_clean)
+            std::memset(slot.buf, 0, slot.cap);
+        slot.padding_clean = ragged || L.n_bands == 1;
+        std::memset(slot.has, 0, L.chunks_per_band);
+        L.next = (L.next + 1) % uint32_t(L.slots.size());
+        return AQZ_STATUS_SUCCESS;
+    }
+
+    // the open unit to the sink: its frames [lo, min(accepted, hi)) are
+    // split; complete = all of them
+    aqz_status deliver_host_unit_(bool complete)
+    {
+        Level& L = levels_[0];
+        Slot& slot = *L.slots[host_.slot];
+        Unit u;
+        u.level = 0;
+        u.layer = host_.layer;
+        u.band = host_.band;
+        u.n_bands = L.n_bands;
+        u.c0 = host_.band * L.chunks_per_band;
+        u.n_chunks = L.chunks_per_band;
+        u.first = host_.lo;
+        u.frames = std::min(accepted_, host_.hi) - std::min(accepted_, host_.lo);
+        u.complete = complete;
+        u.last_in_layer = host_.band + 1 == L.n_bands;
+        u.bytes_per_chunk = L.lay.bytes_per_chunk;
+        u.chunks = slot.buf;
+        u.has_data = slot.has;
+        u.lease = Lease(&slot.pins);
+        host_.open = false;
+        if (++L.band == L.n_bands) {
+            L.band = 0;
+            ++L.layer;
+        }
+        return sink_.unit(u);
+    }
+
+    // close: the rest of level 0's last, partial layer -- its frames not
+    // written are zero (the reference's zeroed chunks, chunk.cpp:8-15) --
+    // unit by unit, as the device side hands off its finalized layer
+    aqz_status close_host_layer_()
+    {
+        Level& L = levels_[0];
+        const uint64_t F = L.lay.frames_per_layer;
+        if (accepted_ <= L.layer * F && !host_.open)
+            return AQZ_STATUS_SUCCESS;
+        const uint64_t layer = L.layer;
+        std::vector<uint8_t> zero;
+        while (L.layer == layer) {
+            aqz_status s = begin_host_unit_();
+            if (s != AQZ_STATUS_SUCCESS)
+                return s;
+            for (uint64_t f = std::max(accepted_, host_.lo); f < host_.hi; ++f) {
+                if (zero.empty())
+                    zero.assign(frame_bytes_, 0);
+                split_host_rows_(zero.data(), f, 0, rows_);
+                if (split_err_ != AQZ_STATUS_SUCCESS)
+                    return split_err_;
+            }
+            s = deliver_host_unit_(false);
+            if (s != AQZ_STATUS_SUCCESS)
+                return s;
+        }
+        return AQZ_STATUS_SUCCESS;
     }
 
     // ---- batches and units ------------------------------------------------------
@@ -830,6 +1014,8 @@ class Handoff
     {
         for (uint32_t l = 0; l < levels_.size(); ++l) {
             Level& L = levels_[l];
+            if (L.host)
+                continue; // split on the host, handed off as its frames arrive
             const uint64_t F = L.lay.frames_per_layer;
             for (;;) {
                 const uint64_t written = written_(l);
@@ -1048,6 +1234,13 @@ class Handoff
     std::vector<Level> levels_;
     std::deque<Pending> compressing_; // compression issued, in issue order
     std::deque<Pending> inflight_;    // copies issued, in issue order
+    // level 0 split on the host
+    HostUnit host_;
+    uint32_t rows_ = 0;     // level-0 rows per frame
+    uint64_t row_bytes_ = 0;
+    Level* csplit_ = nullptr;
+    std::mutex emu_;
+    aqz_status split_err_ = AQZ_STATUS_SUCCESS;
     // frame copy threads
     std::vector<std::thread> copiers_;
     std::mutex cmu_;

@@ -65,6 +65,21 @@ aqz_codec_for(const std::optional<CompressionParams>& params)
     return c;
 }
 
+// ZarrCompressionSettings -> the array's CompressionParams, as the stream
+// builds them (make_compression_params, zarr.stream.cpp:191-208): the
+// compressor field decides, the codec only names blosc's inner codec.
+inline std::optional<CompressionParams>
+compression_params_of(const ZarrCompressionSettings* s)
+{
+    if (!s || s->compressor == ZarrCompressor_None)
+        return std::nullopt;
+    if (s->compressor == ZarrCompressor_Blosc1)
+        return BloscCompressionParams(blosc_codec_to_string(s->codec), s->level, s->shuffle);
+    if (s->compressor == ZarrCompressor_Zstd)
+        return ZstdCompressionParams{ s->level };
+    return std::nullopt;
+}
+
 // The reference's ArrayDimensions as the router's ShardMap.
 class RefShardMap final : public aqz_binding::ShardMap
 {
@@ -259,11 +274,17 @@ class GpuMultiscaleArray final
                              0 };
         EXPECT(!devices.empty() && (devices.size() == 1 || plan.begin.size() == devices.size()),
                "one device per z slab");
+        const aqz_compression comp = aqz_codec_for(config_->compression_params);
+        // a raw hand-off splits level 0 on the host, in the copy threads'
+        // pass over each frame: only levels >= 1 come back over PCIe
+        // 
+        const bool level0_host = aqz_binding::level0_on_host_for(desc, comp);
         for (size_t r = 0; r < devices.size(); ++r) {
             desc.device = devices[r];
             aqz_stage_options opt{};
             opt.max_batch_frames = batch_frames;
             opt.layer_slots = 2;
+            opt.level0_split_on_host = level0_host ? 1u : 0u;
             // the library maps the chunk-layer rings from 2 MiB virtual-
             // memory pieces, where the fused kernels run in the fast band on
             // most boxes; the arena is timed once against a streaming probe
@@ -286,7 +307,8 @@ class GpuMultiscaleArray final
         aqz_binding::HandoffOptions ho;
         ho.batch_frames = batch_frames;
         ho.host_slots = host_slots;
-        ho.comp = aqz_codec_for(config_->compression_params);
+        ho.comp = comp;
+        ho.level0_on_host = level0_host;
         aqz_binding::HandoffSink& sink = *this;
         handoff_ = std::make_unique<aqz_binding::Handoff>(
           stages_, devices.size() > 1 ? plan : aqz_binding::SlabPlan{}, bytes_per_frame_, ho,
@@ -446,7 +468,10 @@ estimate_gpu_array_memory(const ZarrArraySettings& settings,
     aqz_binding::MemoryEstimate m{};
     int32_t n = 0;
     const char* e = std::getenv("AQZ_DEVICE");
-    if (!settings.multiscale || aqz_device_count(&n) != AQZ_STATUS_SUCCESS || n <= 0 ||
+    // make_gpu_multiscale_array's conditions (a multiscale array with a
+    // downsampling method, a visible device, AQZ_DEVICE not off)
+    if (!settings.multiscale || settings.downsampling_method >= ZarrDownsamplingMethodCount ||
+        aqz_device_count(&n) != AQZ_STATUS_SUCCESS || n <= 0 ||
         (e && (std::string(e) == "off" || std::string(e) == "-1")))
         return m;
     std::vector<aqz_dimension> dims(settings.dimension_count);
@@ -463,15 +488,20 @@ estimate_gpu_array_memory(const ZarrArraySettings& settings,
                                settings.max_levels,
                                settings.storage_dimension_order,
                                0 };
+    // the codec the array gets (its CompressionParams, as the stream builds
+    // them) and, from it, the level-0 side -- as GpuMultiscaleArray decides
+    const aqz_compression comp = aqz_codec_for(compression_params_of(settings.compression_settings));
+    const bool level0_host = aqz_binding::level0_on_host_for(desc, comp);
     aqz_stage_options opt{};
     opt.max_batch_frames = batch_frames;
     opt.layer_slots = 2;
     opt.placement_tries = 2; // as GpuMultiscaleArray creates its stages
+    opt.level0_split_on_host = level0_host ? 1u : 0u;
     aqz_binding::HandoffOptions ho;
     ho.batch_frames = batch_frames;
     ho.host_slots = host_slots;
-    if (const ZarrCompressionSettings* c = settings.compression_settings)
-        ho.comp = aqz_compression{ int32_t(c->codec), int32_t(c->level), int32_t(c->shuffle) };
+    ho.comp = comp;
+    ho.level0_on_host = level0_host;
     const auto plan = gpu_slab_plan(settings);
     const uint32_t stages = uint32_t(std::max<size_t>(1, plan.begin.size()));
     if (aqz_binding::estimate_memory(desc, opt, ho, stages, &m) != AQZ_STATUS_SUCCESS)

@@ -59,5 +59,21 @@ main()
     setenv("AQZ_Z_SLABS", "junk", 1);
     expect(aqz_binding::slabs_from_env() == 1, "AQZ_Z_SLABS invalid");
     std::printf("%s\n", fails ? "FAILED" : "OK");
+    // the level-0 side: on the host for a raw hand-off of an array stored in
+    // acquisition row order; on the device with a codec or an XY order
+    {
+        using aqz_binding::level0_on_host_for;
+        aqz_dimension d[3] = { { AQZ_DIM_TIME, 0, 8, 1 }, { AQZ_DIM_SPACE, 64, 16, 1 },
+                               { AQZ_DIM_SPACE, 64, 16, 1 } };
+        const size_t same[3] = { 0, 1, 2 }, xy[3] = { 0, 2, 1 };
+        aqz_array_desc a{ d, 3, AQZ_DTYPE_UINT16, 1, AQZ_METHOD_MEAN, 0, nullptr, 0 };
+        const aqz_compression raw{ AQZ_CODEC_NONE, 0, 0 }, lz4{ AQZ_CODEC_BLOSC_LZ4, 1, 1 };
+        expect(level0_on_host_for(a, raw), "raw, acquisition order: host");
+        expect(!level0_on_host_for(a, lz4), "blosc-lz4: device");
+        a.storage_dimension_order = same;
+        expect(level0_on_host_for(a, raw), "identity storage order: host");
+        a.storage_dimension_order = xy;
+        expect(!level0_on_host_for(a, raw), "XY storage order: device");
+    }
     return fails ? 1 : 0;
 }

@@ -38,6 +38,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -322,10 +323,18 @@ main(int argc, char** argv)
     const bool record = std::strcmp(argv[2], "-") != 0;
 
     aqz_array_desc desc{ dims.data(), dims.size(), dtype, 1, method, 0, nullptr, device };
+    // level 0 split on the host for a raw hand-off, as the binding ships it
+    // (aqz_binding::level0_on_host_for); AQZ_REPLAY_LEVEL0=device|host
+    // forces one side
+    const aqz_compression comp{ codec, clevel, shuffle };
+    bool level0_host = aqz_binding::level0_on_host_for(desc, comp);
+    if (const char* e = std::getenv("AQZ_REPLAY_LEVEL0"))
+        level0_host = std::strcmp(e, "host") == 0;
     aqz_stage_options opt{};
     opt.max_batch_frames = batch;
     opt.layer_slots = 2;
     opt.placement_tries = tries;
+    opt.level0_split_on_host = level0_host ? 1u : 0u;
     aqz_stage* st = nullptr;
     if (aqz_stage_create(&desc, &opt, &st) != AQZ_STATUS_SUCCESS) {
         fprintf(stderr, "aqz_stage_create: %s\n", aqz_last_error());
@@ -393,7 +402,8 @@ main(int argc, char** argv)
         ho.batch_frames = batch;
         ho.host_slots = slots;
         ho.copy_threads = copy_threads;
-        ho.comp = aqz_compression{ codec, clevel, shuffle };
+        ho.comp = comp;
+        ho.level0_on_host = level0_host;
         aqz_binding::Handoff h(stages, plan, fbytes, ho, sink);
         if (h.status() != AQZ_STATUS_SUCCESS) {
             fprintf(stderr, "handoff: %s\n", aqz_last_error());
@@ -445,13 +455,14 @@ main(int argc, char** argv)
            "\"sink_bytes_per_input_byte\": %.4f, \"codec\": %d, \"clevel\": %d, "
            "\"shuffle\": %d, \"device\": %d, \"batch\": %u, \"copy_threads\": %u, "
            "\"pool_threads\": %u, \"host_bytes\": %llu, \"device_bytes\": %llu, "
-           "\"estimate_host_bytes\": %llu, \"estimate_device_bytes\": %llu}\n",
+           "\"estimate_host_bytes\": %llu, \"estimate_device_bytes\": %llu, "
+           "\"level0_split\": \"%s\"}\n",
            rc == 0 ? "true" : "false", (unsigned long long)sink.units.load(),
            (unsigned long long)aqz_stage_last_ticket(stages.back()), (unsigned long long)n_frames,
            seconds, in / seconds / 1e9, double(sink.chunk_bytes.load()) / in, codec, clevel,
            shuffle, device, batch, copy_threads, pool_threads, (unsigned long long)host_bytes,
            (unsigned long long)device_bytes, (unsigned long long)est_host,
-           (unsigned long long)est_device);
+           (unsigned long long)est_device, level0_host ? "host" : "device");
     for (aqz_stage* s : stages)
         aqz_stage_destroy(s);
     for (auto& L : sink.lv)

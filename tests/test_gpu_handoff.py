@@ -176,7 +176,7 @@ class Replay:
 
 def _run_replay(tmp_path, dims, dtype, method, frames, batch, slots, codec=(0, 0, 0),
                 copy_threads=4, pool_threads=4, device=0, synth=0, n_frames=None,
-                placement_tries=0, record=True, z_slabs=1):
+                placement_tries=0, record=True, z_slabs=1, level0=None):
     """tests/native/handoff_replay: the binding's hand-off
     (integration/aqz_handoff.hh, what GpuMultiscaleArray runs) over the C
     ABI; every unit goes through the shipped ShardRouter (what GpuArray
@@ -204,8 +204,11 @@ def _run_replay(tmp_path, dims, dtype, method, frames, batch, slots, codec=(0, 0
                             copy_threads, pool_threads, synth, placement_tries, z_slabs, n, fb))
         if frames is not None:
             f.write(np.ascontiguousarray(frames).tobytes())
+    env = dict(os.environ)
+    if level0:  # force the level-0 side (default: the binding's choice)
+        env["AQZ_REPLAY_LEVEL0"] = level0
     r = subprocess.run([exe, str(job), str(out) if record else "-"], capture_output=True,
-                       text=True, timeout=300)
+                       text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     log = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     summary = log[-1]
@@ -376,6 +379,8 @@ def test_binding_handoff_replay(gpu, tmp_path, case, codec):
         frames[5:9] = 0
     exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
     r = _run_replay(tmp_path, dims, U16, MEAN, frames, batch, 2, codec=CODECS[codec])
+    # a raw hand-off splits level 0 on the host (the binding's choice)
+    assert r.summary["level0_split"] == ("device" if CODECS[codec][0] else "host")
     st = gpu.Stage(dims, U16, MEAN)
     if case.startswith("banded") and not CODECS[codec][0]:
         assert len([e for e in r.log if e["level"] == 0]) > len(
@@ -430,3 +435,40 @@ def test_binding_z_slabs(gpu, tmp_path, codec, slabs, tail):
     st = gpu.Stage(dims, U16, MEAN)
     _check_replay(exp, fw, r, CODECS[codec], st)
     st.close()
+
+
+@pytest.mark.parametrize("case", sorted(REPLAY_CASES))
+def test_binding_handoff_replay_level0_on_device(gpu, tmp_path, case):
+    """The raw hand-off with level 0 split on the device and copied D2H (the
+    path a compressed hand-off keeps for level 0, and the raw one before the
+    host split): the same units, chunks and routing as the host split."""
+    dims, n, batch = REPLAY_CASES[case]
+    frames = synthetic_frames(U16, n, dims[-2][1], dims[-1][1], 83 + n)
+    frames[5:9] = 0
+    exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
+    r = _run_replay(tmp_path, dims, U16, MEAN, frames, batch, 2, level0="device")
+    assert r.summary["level0_split"] == "device"
+    st = gpu.Stage(dims, U16, MEAN)
+    _check_replay(exp, fw, r, CODECS["raw"], st)
+    st.close()
+
+
+@pytest.mark.parametrize("copy_threads", [1, 3])
+def test_binding_handoff_replay_host_split_frames_small_and_large(gpu, tmp_path, copy_threads):
+    """The host split in the copy pass: frames under 1 MiB are copied and
+    split by the consumer thread alone, larger ones by row ranges over the
+    copy threads (each thread's rows into the same unit buffer); a ragged
+    dim-1 band clears the slot a full band left (padding positions), and
+    close zero-fills the unwritten frames of level 0's last layer."""
+    dims = [(TIME, 0, 1, 1), (SPACE, 20, 8, 1)]
+    n = 2 * 20 + 11  # two layers and a partial third; bands of 8, 8, 4 planes
+    frames = synthetic_frames(U16, n, 1000, 640, 97 + copy_threads)  # 1.28 MB frames
+    frames[30:33] = 0
+    for fr, batch in ((frames, 6), (np.ascontiguousarray(frames[:, :300, :256]), 5)):
+        d = dims[:2] + [(SPACE, fr.shape[1], 128, 2), (SPACE, fr.shape[2], 128, 2)]
+        e, f, _ = expected_stage_layers(d, U16, MEAN, fr)
+        r = _run_replay(tmp_path, d, U16, MEAN, fr, batch, 2, copy_threads=copy_threads)
+        assert r.summary["level0_split"] == "host"
+        st = gpu.Stage(d, U16, MEAN)
+        _check_replay(e, f, r, CODECS["raw"], st)
+        st.close()

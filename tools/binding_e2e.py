@@ -32,7 +32,12 @@ def main():
     ap.add_argument("--pool-threads", type=int, default=16)
     ap.add_argument("--host-slots", type=int, default=3)
     ap.add_argument("--placement-tries", type=int, default=0)
+    ap.add_argument("--level0", default="", choices=["", "host", "device"],
+                    help="force the level-0 side (default: the binding's choice)")
     args = ap.parse_args()
+    env = dict(os.environ)
+    if args.level0:
+        env["AQZ_REPLAY_LEVEL0"] = args.level0
     dims = [(2, 0, 64, 1), (0, 2048, 256, 1), (0, 2048, 256, 1)]
     for name in args.codecs.split(","):
         with tempfile.TemporaryDirectory() as d:
@@ -44,7 +49,8 @@ def main():
                 f.write(struct.pack("<iiIIiiiiIIIIIQQ", 1, 1, args.batch, args.host_slots, 0,
                                     *CODECS[name], args.copy_threads, args.pool_threads, 1,
                                     args.placement_tries, 1, args.frames, 2048 * 2048 * 2))
-            r = subprocess.run([EXE, job, "-"], capture_output=True, text=True, timeout=600)
+            r = subprocess.run([EXE, job, "-"], capture_output=True, text=True, timeout=600,
+                               env=env)
             if r.returncode != 0:
                 sys.exit(r.stdout[-2000:] + r.stderr[-2000:])
             s = json.loads(r.stdout.strip().splitlines()[-1])

@@ -58,4 +58,40 @@ python3 -c "import json; d=json.load(open('$O/pyr$i.json')); r=d['roofline']; p=
 done
 }
 
+# host split of level 0: parity tests, then the e2e A/B (bench.py --e2e
+# pinned / pageable, host vs device level 0; the binding's raw row both ways)
+step_p2() {
+O=gpurun_out/r6p2
+mkdir -p $O
+timeout -k 10 900 python3 -u -m pytest tests/test_gpu_hostsplit.py tests/test_gpu_handoff.py -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -3 $O/pytest.log
+e2e_ab $O
+}
+
+e2e_ab() {
+O=$1
+for a in "--e2e pinned" "--e2e pinned --level0-split device" "--e2e pageable" "--e2e pageable --level0-split device"; do
+timeout -k 10 200 python3 -u bench.py --steps 16 --warmup 4 $a --no-cpu-baseline > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+cat $O/tmp.json >> $O/bench_e2e.jsonl
+python3 -c "import json; d=json.load(open('$O/tmp.json')); print('$a', d['value'], d['ms_per_step'], d.get('d2h_bytes_per_input_byte'), d.get('level0_split'))"
+done
+timeout -k 10 400 python3 -u tools/binding_e2e.py --frames 2048 --placement-tries 2 --codecs raw > $O/binding.jsonl 2> $O/binding.err || { tail $O/binding.err; exit 1; }
+timeout -k 10 400 python3 -u tools/binding_e2e.py --frames 2048 --placement-tries 2 --codecs raw --level0 device >> $O/binding.jsonl 2>> $O/binding.err || { tail $O/binding.err; exit 1; }
+timeout -k 10 400 python3 -u tools/binding_e2e.py --frames 2048 --placement-tries 2 --codecs raw --copy-threads 15 >> $O/binding.jsonl 2>> $O/binding.err || { tail $O/binding.err; exit 1; }
+python3 -c "
+import json
+for l in open('$O/binding.jsonl'):
+    d = json.loads(l); print('binding', d['codec_name'], d['level0_split'], d['copy_threads'], d['input_gbs'])"
+}
+
+# host split throughput on the box's cores (tools/split_probe.cpp, CPU only)
+step_p3() {
+O=gpurun_out/r6p3
+mkdir -p $O
+g++ -O3 -std=c++20 -pthread tools/split_probe.cpp -o $O/split_probe || exit 1
+timeout -k 10 300 $O/split_probe 256 > $O/split_probe.jsonl 2>&1 || { tail $O/split_probe.jsonl; exit 1; }
+cat $O/split_probe.jsonl
+nproc; grep -m1 "model name" /proc/cpuinfo; taskset -p $$ || true
+}
+
 "step_$@"
