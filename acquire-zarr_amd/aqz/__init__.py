@@ -255,6 +255,7 @@ def lib():
         "aqz_stage_timing_mark": ([vp, i32], i32),
         "aqz_stage_timing_elapsed": ([vp, C.POINTER(C.c_double)], i32),
         "aqz_stage_dominant_kernel": ([vp], C.c_char_p),
+        "aqz_stage_zstd_far_ranges": ([vp, u32], u32),
         "aqz_probe_hbm": ([i32, i32, u64, u32, C.POINTER(C.c_double), C.POINTER(u64)], i32),
         "aqz_stage_placement": ([vp, C.POINTER(C.c_double), sz, C.POINTER(sz),
                                  C.POINTER(u32)], i32),
@@ -808,6 +809,11 @@ class Stage:
 
     def dominant_kernel(self):
         return lib().aqz_stage_dominant_kernel(self.h).decode()
+
+    def zstd_far_ranges(self, level):
+        """Ranges of the device zstd far pass over level's last compressed
+        layer (aqz_stage_zstd_far_ranges; 0 = none ran)."""
+        return lib().aqz_stage_zstd_far_ranges(self.h, level)
 
     def host_affinity(self):
         """(NUMA node of the device, CPUs the host pools are pinned to)."""

@@ -951,6 +951,16 @@ aqz_stage_dominant_kernel(const aqz_stage* st)
     return st ? st->st->dominant_kernel() : "";
 }
 
+uint32_t
+aqz_stage_zstd_far_ranges(const aqz_stage* st, uint32_t level)
+{
+    try {
+        return st && st->st ? st->st->zstd_far_ranges(level) : 0;
+    } catch (...) {
+        return 0;
+    }
+}
+
 aqz_status
 aqz_stage_host_affinity(const aqz_stage* st, int32_t* numa_node, uint32_t* n_cpus)
 {

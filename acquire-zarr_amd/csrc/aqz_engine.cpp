@@ -2067,17 +2067,12 @@ Compressor::Compressor(uint64_t chunk_bytes, uint32_t typesize, const Compressio
 //                1.983, c-blosc clevel 5 1.974); byte shuffle: none (its
 //                planes lose from longer matches: camera 1.891 -> 1.845)
 // (tools/zstd_lab.cpp far=..., farbatch=4096)
-// compute units of the current device (the far pass's range split)
-static uint64_t
-device_cus()
-{
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        n <= 0)
-        return 256;
-    return uint64_t(n);
-}
+// The far pass's range split is sized for the MI355X's 256 CUs as a
+// constant, not read from the device: the ranges (and so a chunk's frame
+// bytes) then follow from the layer geometry alone, the same for a stage
+// and a standalone compressor on any device.  Every choice decodes to the
+// same chunk.
+constexpr uint64_t kFarRangeCus = 256;
 
 uint32_t
 zstd_far_slices(const Compression& c, uint32_t typesize)
@@ -2256,7 +2251,7 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
             // size).  Layers that fill the device keep one range.
             const uint64_t wgs = nseg * p.far_slices;
             const uint64_t steps = (uint64_t(p.seg_bytes) + kZSub - 1) / kZSub;
-            const uint64_t cus = device_cus();
+            const uint64_t cus = kFarRangeCus;
             const uint64_t warm = std::max<uint64_t>(kFarWarm, (2 * plane_bytes_ + kZSub - 1) / kZSub);
             p.far_warm = uint32_t(std::min<uint64_t>(warm, steps));
             p.far_ranges = 1;
@@ -2264,6 +2259,7 @@ Compressor::run_zstd(const uint8_t* chunks, uint64_t pitch, uint32_t n_chunks,
                    steps / (2u * p.far_ranges) >= warm)
                 p.far_ranges *= 2;
         }
+        far_ranges_ = far ? p.far_ranges : 0;
         if (p.match) {
             const uint64_t nu = nblk * kZSubBlocks;
             alloc_large(lits_, nu * kZSub, tune_.vmm);

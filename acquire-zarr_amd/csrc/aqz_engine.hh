@@ -166,6 +166,8 @@ class Compressor
     // walk warms up over at least two of them (0: unknown)
     void set_plane_bytes(uint64_t b) { plane_bytes_ = b; }
     uint64_t chunk_bytes() const { return nbytes_; }
+    // ranges of the last run's far pass (0: none ran)
+    uint32_t far_ranges() const { return far_ranges_; }
     // the blosc block size recorded in the frames (0: plain zstd)
     uint32_t blocksize() const
     {
@@ -199,6 +201,7 @@ class Compressor
     CodecTuning tune_;
     uint64_t nbytes_ = 0;
     uint64_t plane_bytes_ = 0;
+    uint32_t far_ranges_ = 0;
     uint32_t typesize_ = 1;
     BloscGeom g_{};
     bool store_only_;
@@ -452,6 +455,12 @@ class Stage
     void mark(int which);
     double marked_ms();
     const char* dominant_kernel() const;
+    uint32_t zstd_far_ranges(uint32_t level) const
+    {
+        if (level >= lv_.size())
+            throw Error(3, "level out of range");
+        return lv_[level].comp ? lv_[level].comp->far_ranges() : 0;
+    }
     int numa_node() const { return numa_node_; }
     size_t numa_cpus() const { return numa_cpus_.size(); }
     // pin the calling thread to the CPUs of the device's NUMA node

@@ -4,6 +4,7 @@
 #include <immintrin.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 
 namespace aqz {
@@ -87,12 +88,14 @@ stream_copy_avx2(uint8_t* d, const uint8_t* s, size_t n)
     std::memcpy(d + i, s + i, n - i);
 }
 
-const bool kHaveAvx2 = __builtin_cpu_supports("avx2");
+// AQZ_SPLIT_NT=0: plain memcpy stores (A/B)
+const bool kStream = __builtin_cpu_supports("avx2") &&
+                     !(std::getenv("AQZ_SPLIT_NT") && std::atoi(std::getenv("AQZ_SPLIT_NT")) == 0);
 
 inline void
 stream_copy(uint8_t* d, const uint8_t* s, size_t n)
 {
-    if (kHaveAvx2 && n >= 128)
+    if (kStream && n >= 128)
         stream_copy_avx2(d, s, n);
     else
         std::memcpy(d, s, n);

@@ -147,6 +147,10 @@ aqz_status aqz_stage_timing_mark(aqz_stage* st, int32_t which);
 aqz_status aqz_stage_timing_elapsed(aqz_stage* st, double* ms);
 /* Name of the dominant kernel symbol (for matching rocprof output). */
 const char* aqz_stage_dominant_kernel(const aqz_stage* st);
+/* Ranges the device zstd far pass walked each segment of `level`'s last
+ * compressed layer in (1 = one sequential walk; 0 = no far pass or no
+ * compression yet): the ranges follow from the layer geometry alone. */
+uint32_t aqz_stage_zstd_far_ranges(const aqz_stage* st, uint32_t level);
 
 /* Placement calibration done at creation (the chunk-layer rings were
  * allocated up to n times and the fastest placement kept): the ms per

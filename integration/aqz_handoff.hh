@@ -172,12 +172,21 @@ class ShardRouter
     // test, array.cpp:713-720).  On a layer's last unit the ragged padding
     // of every shard is skipped so each shard's countdown completes
     // (array.cpp:771-790, 852-862).  A compressed unit's entries carry the
-    // device's (shard, internal) of each chunk: they must agree with the
-    // map, else INTERNAL_ERROR and nothing more of the unit is routed.
+    // device's (shard, internal) of each chunk: they must all agree with the
+    // map -- checked before any chunk is dispatched -- else INTERNAL_ERROR
+    // and nothing of the unit is routed.
     aqz_status route(const Unit& u, ShardWriter& w) const
     {
         const uint32_t n_mem = map_.chunks_in_memory();
         const uint32_t offset = current_layer_ * n_mem;
+        for (uint32_t i = 0; i < u.n_chunks; ++i) {
+            const uint32_t local = u.entries ? u.entries[i].chunk : u.c0 + i;
+            if (local >= n_mem)
+                return AQZ_STATUS_INTERNAL_ERROR;
+            if (u.entries && (u.entries[i].shard != map_.shard_index_for_chunk(offset + local) ||
+                              u.entries[i].internal != map_.shard_internal_index(offset + local)))
+                return AQZ_STATUS_INTERNAL_ERROR;
+        }
         for (uint32_t i = 0; i < u.n_chunks; ++i) {
             uint32_t local;
             const uint8_t* p;
@@ -192,13 +201,9 @@ class ShardRouter
                 p = u.chunks + size_t(i) * u.bytes_per_chunk;
                 n = u.has_data[i] ? u.bytes_per_chunk : 0;
             }
-            if (local >= n_mem)
-                return AQZ_STATUS_INTERNAL_ERROR;
             const uint32_t chunk = offset + local;
             const uint32_t shard = map_.shard_index_for_chunk(chunk);
             const uint32_t internal = map_.shard_internal_index(chunk);
-            if (u.entries && (u.entries[i].shard != shard || u.entries[i].internal != internal))
-                return AQZ_STATUS_INTERNAL_ERROR;
             if (n == 0)
                 w.skip_chunk(shard, internal, chunk);
             else

@@ -377,7 +377,7 @@ def test_plain_zstd_far_ranges_keep_the_bytes(gpu, monkeypatch):
     frames = np.stack([base + rng.integers(0, 2, hw * hw).astype(np.uint16) * (t % 2)
                        for t in range(T)]).reshape(T, hw, hw)
     dims = [(TIME, 0, T, 1), (SPACE, hw, hw, 1), (SPACE, hw, hw, 1)]
-    sizes = {}
+    sizes, ranges = {}, {}
     for name, flags in (("ranges", 0), ("one", gpu.ZSTD_FAR_ONE_RANGE)):
         st = gpu.Stage(dims, U16, MEAN, multiscale=False, layer_slots=2, max_batch_frames=T,
                        zstd_flags=flags)
@@ -390,8 +390,11 @@ def test_plain_zstd_far_ranges_keep_the_bytes(gpu, monkeypatch):
             assert zstd_decode(data[o:o + nb].tobytes(), bpc) == \
                 layer[c * bpc:(c + 1) * bpc].tobytes(), (name, c)
         sizes[name] = int(off[-1])
+        ranges[name] = st.zstd_far_ranges(0)
         st.close()
-    print(f"16 MiB chunk at level 3: bytes {sizes}")
+    print(f"16 MiB chunk at level 3: bytes {sizes}, far ranges {ranges}")
+    # the ranged walk ran, the A/B switch kept one range
+    assert ranges["one"] == 1 and ranges["ranges"] > 1, ranges
     assert sizes["ranges"] <= 1.005 * sizes["one"], sizes
 
 

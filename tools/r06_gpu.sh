@@ -63,7 +63,7 @@ done
 step_p2() {
 O=gpurun_out/r6p2
 mkdir -p $O
-timeout -k 10 900 python3 -u -m pytest tests/test_gpu_hostsplit.py tests/test_gpu_handoff.py -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+timeout -k 10 900 python3 -u -m pytest tests/test_gpu_hostsplit.py tests/test_gpu_handoff.py tests/test_gpu_zstd.py -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -3 $O/pytest.log
 e2e_ab $O
 }
@@ -92,6 +92,49 @@ g++ -O3 -std=c++20 -pthread tools/split_probe.cpp -o $O/split_probe || exit 1
 timeout -k 10 300 $O/split_probe 256 > $O/split_probe.jsonl 2>&1 || { tail $O/split_probe.jsonl; exit 1; }
 cat $O/split_probe.jsonl
 nproc; grep -m1 "model name" /proc/cpuinfo; taskset -p $$ || true
+}
+
+# host split A/B on one box: streaming vs plain stores (AQZ_SPLIT_NT), split
+# threads (AQZ_SPLIT_THREADS) for bench.py --e2e, copy threads for the binding
+step_p4() {
+O=gpurun_out/r6p4
+mkdir -p $O
+for nt in 1 0 1 0; do
+for a in "--e2e pinned" "--e2e pageable"; do
+AQZ_SPLIT_NT=$nt timeout -k 10 200 python3 -u bench.py --steps 16 --warmup 4 $a --no-cpu-baseline > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+cat $O/tmp.json >> $O/bench_e2e.jsonl
+python3 -c "import json; d=json.load(open('$O/tmp.json')); print('nt=$nt $a', d['value'])"
+done
+done
+for th in 7 11; do
+AQZ_SPLIT_THREADS=$th timeout -k 10 200 python3 -u bench.py --steps 16 --warmup 4 --e2e pinned --no-cpu-baseline > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/tmp.json')); print('split threads $th+1 pinned', d['value'])"
+done
+for nt in 1 0; do
+for ct in 8 15; do
+AQZ_SPLIT_NT=$nt timeout -k 10 400 python3 -u tools/binding_e2e.py --frames 2048 --placement-tries 2 --codecs raw --copy-threads $ct > $O/b.json 2>> $O/binding.err || { tail $O/binding.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/b.json')); print('binding nt=$nt copy $ct', d['input_gbs'])"
+done
+done
+}
+
+# e2e rows, 3 interleaved rounds on one box (medians for DESIGN): bench.py
+# --e2e pinned / pageable with level 0 on the host and on the device, the
+# binding's raw row both ways
+step_p5() {
+O=gpurun_out/r6p5
+mkdir -p $O
+for rnd in 1 2 3; do
+for a in "--e2e pinned" "--e2e pinned --level0-split device" "--e2e pageable" "--e2e pageable --level0-split device"; do
+timeout -k 10 200 python3 -u bench.py --steps 48 --warmup 4 $a --no-cpu-baseline > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+cat $O/tmp.json >> $O/bench_e2e.jsonl
+python3 -c "import json; d=json.load(open('$O/tmp.json')); print('r$rnd $a', d['value'], d.get('level0_split'))"
+done
+for l0 in host device; do
+timeout -k 10 400 python3 -u tools/binding_e2e.py --frames 2048 --placement-tries 2 --codecs raw --level0 $l0 >> $O/binding.jsonl 2>> $O/binding.err || { tail $O/binding.err; exit 1; }
+python3 -c "import json; d=[json.loads(l) for l in open('$O/binding.jsonl')][-1]; print('r$rnd binding raw', d['level0_split'], d['input_gbs'])"
+done
+done
 }
 
 "step_$@"
