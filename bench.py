@@ -645,12 +645,18 @@ def main():
     if world != args.gpus:
         sys.exit(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU required")
     if args.launch_probe:
-        # CPU test hook: report the rank layout and stop before any GPU work
-        # one write() per line: ranks share the pipe
-        sys.stdout.write(json.dumps({"rank": int(os.environ.get("RANK", "0")),
-                                     "world": world,
-                                     "local_rank": int(os.environ.get("LOCAL_RANK", "0"))})
-                         + "\n")
+        # CPU test hook: report the rank layout -- and for C4 the rank's z
+        # slab -- and stop before any GPU work; one write() per line: ranks
+        # share the pipe
+        probe = {"rank": int(os.environ.get("RANK", "0")), "world": world,
+                 "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}
+        if args.config == "c4" and world > 1:
+            import aqz
+            from aqz.dist import z_levels, z_slab
+            planes = [lv[1][1] for lv in aqz.pyramid_levels(CONFIGS["c4"]["dims"])]
+            probe["z_slab"] = list(z_slab(planes[0], world, probe["rank"],
+                                          1 << z_levels(planes)))
+        sys.stdout.write(json.dumps(probe) + "\n")
         sys.stdout.flush()
         return
 
@@ -744,6 +750,7 @@ def main():
         if args.no_kernel_events:
             kms = elapsed * 1e3
         kernel = st.dominant_kernel()
+        numa = st.host_affinity()  # (NUMA node of the device, CPUs there)
         placement = st.placement()
         placement["estimate_device_bytes"] = est["device_bytes"]
         placement["stage_create_s"] = round(create_s, 3)
@@ -764,7 +771,7 @@ def main():
         alg = (emitted[0] * fbytes * (1 if pyramid_only else 2) + out_bytes) // max(1, steps)
         avg_ms = kms / max(1, launches)
         return dict(elapsed=elapsed, elapsed_local=elapsed_local, sizes=sizes, fbytes=fbytes,
-                    kernel=kernel,
+                    kernel=kernel, numa=numa,
                     avg_ms=avg_ms, alg=alg, placement=placement,
                     achieved=alg / (avg_ms * 1e-3) / 1e9 if launches else 0.0,
                     value=world * steps * B * fbytes / elapsed / 1e9)
@@ -788,7 +795,9 @@ def main():
         # after the timed region (a few numbers per rank) so a multi-GPU line
         # shows which rank set the max
         mp = main_run["placement"]
-        mine = {"rank": rank, "device": dev.index,
+        numa = main_run.get("numa")
+        mine = {"rank": rank, "device": dev.index, "numa_node": numa[0] if numa else None,
+                "host_cpus": numa[1] if numa else None,
                 "kernel_avg_ms": round(main_run["avg_ms"], 5),
                 "frac": round(main_run["achieved"] / HBM_PEAK_GBS, 4),
                 "elapsed_s": round(main_run["elapsed_local"], 5),
