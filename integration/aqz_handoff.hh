@@ -240,6 +240,47 @@ class ShardRouter
     uint32_t current_layer_ = 0;
 };
 
+// The per-array counters zarr::Array keeps frame by frame (the tail of
+// Array::write_frame, array.cpp:196-219; flush_completed_bands_, :873-908),
+// advanced a whole unit of frames at a time.  GpuArray mirrors them into
+// the reference's members (frames_written_() = total_bytes_written_ /
+// bytes_per_frame_ is what should_rollover_ reads, array.cpp:924-937,
+// 974-977); the GPU replay runs the same code and checks it, unit by unit,
+// against the reference's per-frame rules.
+struct ArrayLedger
+{
+    uint64_t total_bytes_written = 0;
+    uint64_t last_successful_frame_id = 0;
+    // bytes of frames not yet handed to their shards: 0 after every unit
+    // (the reference zeroes it at each layer flush; its only reader,
+    // Array::close_, array.cpp:380-383, must find nothing left to flush)
+    uint64_t bytes_to_flush = 0;
+    uint32_t flushed_band_count = 0; // bands of the current layer flushed
+
+    uint64_t frames_written(uint64_t bytes_per_frame) const
+    {
+        return bytes_per_frame ? total_bytes_written / bytes_per_frame : 0;
+    }
+
+    // The unit's frames are written: false (nothing changes) when they would
+    // pass max_bytes (Array::write_frame's bounds check, array.cpp:174-177;
+    // 0 = unbounded).
+    bool commit(const Unit& u, uint64_t bytes_per_frame, uint64_t max_bytes)
+    {
+        const uint64_t nbytes = u.frames * bytes_per_frame;
+        if (max_bytes > 0 && total_bytes_written + nbytes > max_bytes)
+            return false;
+        if (u.frames)
+            last_successful_frame_id = frames_written(bytes_per_frame) + u.frames - 1;
+        total_bytes_written += nbytes;
+        bytes_to_flush = 0;
+        // a layer's last band resets the count (array.cpp:884-896), an
+        // interior band leaves band + 1 flushed (:897-905)
+        flushed_band_count = u.last_in_layer ? 0 : u.band + 1;
+        return true;
+    }
+};
+
 // aqz_dims as the router's ShardMap (the replay; any caller without the
 // reference's ArrayDimensions).  Does not own d.
 class DimsShardMap final : public ShardMap

@@ -141,16 +141,17 @@ class GpuArray final
     // (ShardRouter::commit: compress_and_flush_data_ :799-803,
     // flush_completed_bands_ :880-898).  The last, partial layer at close
     // is already written, so close_ has nothing to flush.
+    // The counters are aqz_binding::ArrayLedger's (the code the GPU replay
+    // runs and checks against the reference's per-frame rules), mirrored
+    // into the reference's members before should_rollover_ reads them.
     WriteResult commit_unit(const aqz_binding::Unit& u)
     {
-        const uint64_t nbytes = u.frames * bytes_per_frame_;
-        if (max_bytes_ > 0 && total_bytes_written_ + nbytes > max_bytes_)
+        if (!ledger_.commit(u, bytes_per_frame_, max_bytes_))
             return WriteResult::OutOfBounds;
-        if (u.frames)
-            last_successful_frame_id_ = frames_written_() + u.frames - 1;
-        total_bytes_written_ += nbytes;
-        bytes_to_flush_ = 0;
-        flushed_band_count_ = u.last_in_layer ? 0 : u.band + 1;
+        total_bytes_written_ = ledger_.total_bytes_written;
+        last_successful_frame_id_ = ledger_.last_successful_frame_id;
+        bytes_to_flush_ = ledger_.bytes_to_flush;
+        flushed_band_count_ = ledger_.flushed_band_count;
         router_.commit(u, *this);
         current_layer_ = router_.current_layer();
         return WriteResult::Ok;
@@ -176,6 +177,7 @@ class GpuArray final
 
     RefShardMap map_;
     aqz_binding::ShardRouter router_;
+    aqz_binding::ArrayLedger ledger_;
 
     void dispatch_bytes_job_(std::shared_ptr<Shard> shard,
                              uint32_t chunk_idx,
@@ -257,6 +259,12 @@ class GpuMultiscaleArray final
             gpu_arrays_[lod] = a.get();
             arrays_[lod] = std::move(a);
         }
+        // every level's CPU Array was replaced (create_arrays_ made one per
+        // writer configuration, multiscale.array.cpp:137-159)
+        EXPECT(gpu_arrays_.size() == arrays_.size(), "a level without a GpuArray");
+        for (size_t l = 0; l < arrays_.size(); ++l)
+            EXPECT(gpu_arrays_[l] != nullptr && arrays_[l].get() == gpu_arrays_[l],
+                   "level ", l, " still has a CPU Array");
 
         dims_.resize(settings.dimension_count);
         for (size_t i = 0; i < settings.dimension_count; ++i) {

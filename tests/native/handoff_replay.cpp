@@ -34,6 +34,7 @@
 #include "aqz_gpu.h"
 #include "aqz_handoff.hh"
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -126,9 +127,35 @@ struct Record
 
 // One level: the shipped router (aqz_binding::ShardRouter, what GpuArray
 // runs) over aqz_dims, writing into a recorder in place of the shards.
+// zarr::Array's counters as the reference advances them, frame by frame:
+// the tail of Array::write_frame (array.cpp:196-199) and, for an array with
+// dim-1 banding, flush_completed_bands_ (:882-905).  The replay checks the
+// binding's ArrayLedger against it after every complete unit.
+struct RefCounters
+{
+    uint64_t total = 0, last_id = 0;
+    uint32_t flushed = 0;
+    void frame(uint64_t bpf, uint64_t F, bool banded, uint64_t fpb)
+    {
+        last_id = total / bpf; // frame_id == frames_written_() (checked above it)
+        total += bpf;
+        if (!banded)
+            return;
+        const uint64_t in_layer = (total / bpf) % F;
+        if (in_layer == 0)
+            flushed = 0;
+        else if (in_layer % fpb == 0)
+            flushed = std::max<uint32_t>(flushed, uint32_t(in_layer / fpb));
+    }
+};
+
 struct LevelState final : aqz_binding::ShardWriter
 {
     uint64_t F = 0, bpc = 0, committed = 0;
+    uint64_t frame_bytes = 0, fpb = 0;
+    bool banded = false;
+    aqz_binding::ArrayLedger ledger; // what GpuArray::commit_unit runs
+    RefCounters ref;
     uint32_t n_chunks = 0;
     bool incomplete_seen = false;
     uint64_t incomplete_layer = 0;
@@ -220,9 +247,27 @@ struct RecordingSink final : aqz_binding::HandoffSink
             ok = false;
             return s;
         }
-        // GpuArray::commit_unit: the frames are counted, then the layer
-        // advance or rollover
-        L.committed += u.frames;
+        // GpuArray::commit_unit: the frames are counted (the shipped
+        // ArrayLedger), then the layer advance or rollover
+        if (!L.ledger.commit(u, L.frame_bytes, 0))
+            ok = false;
+        L.committed = L.ledger.frames_written(L.frame_bytes);
+        for (uint64_t i = 0; i < u.frames; ++i)
+            L.ref.frame(L.frame_bytes, L.F, L.banded, L.fpb);
+        if (u.complete && (L.ledger.total_bytes_written != L.ref.total ||
+                           (u.frames && L.ledger.last_successful_frame_id != L.ref.last_id) ||
+                           L.ledger.flushed_band_count != L.ref.flushed ||
+                           L.ledger.bytes_to_flush != 0)) {
+            fprintf(stderr, "level %u layer %llu band %u: counters differ from Array's: total "
+                            "%llu/%llu last %llu/%llu bands %u/%u\n",
+                    u.level, (unsigned long long)u.layer, u.band,
+                    (unsigned long long)L.ledger.total_bytes_written,
+                    (unsigned long long)L.ref.total,
+                    (unsigned long long)L.ledger.last_successful_frame_id,
+                    (unsigned long long)L.ref.last_id, L.ledger.flushed_band_count,
+                    L.ref.flushed);
+            ok = false;
+        }
         L.router->commit(u, L);
         return AQZ_STATUS_SUCCESS;
     }
@@ -382,6 +427,15 @@ main(int argc, char** argv)
         L->F = lay.frames_per_layer;
         L->bpc = lay.bytes_per_chunk;
         L->n_chunks = lay.chunks_per_layer;
+        L->frame_bytes = lay.frame_bytes;
+        {
+            int32_t banded = 0;
+            uint32_t nb = 1, cpb = 0;
+            uint64_t fpb = 0;
+            aqz_stage_band_geometry(st, l, &banded, &nb, &fpb, &cpb);
+            L->banded = banded != 0;
+            L->fpb = fpb ? fpb : L->F;
+        }
         std::vector<aqz_dimension> ld(16);
         size_t n = 0;
         aqz_stage_level_dims(st, l, ld.data(), ld.size(), &n);

@@ -88,8 +88,9 @@ for l in open('$O/binding.jsonl'):
 step_p3() {
 O=gpurun_out/r6p3
 mkdir -p $O
-g++ -O3 -std=c++20 -pthread tools/split_probe.cpp -o $O/split_probe || exit 1
+g++ -O3 -std=c++20 -pthread -DWITH_HIP -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include tools/split_probe.cpp -o $O/split_probe -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib || exit 1
 timeout -k 10 300 $O/split_probe 256 > $O/split_probe.jsonl 2>&1 || { tail $O/split_probe.jsonl; exit 1; }
+timeout -k 10 300 $O/split_probe 256 pinned >> $O/split_probe.jsonl 2>&1 || { tail $O/split_probe.jsonl; exit 1; }
 cat $O/split_probe.jsonl
 nproc; grep -m1 "model name" /proc/cpuinfo; taskset -p $$ || true
 }
@@ -135,6 +136,32 @@ timeout -k 10 400 python3 -u tools/binding_e2e.py --frames 2048 --placement-trie
 python3 -c "import json; d=[json.loads(l) for l in open('$O/binding.jsonl')][-1]; print('r$rnd binding raw', d['level0_split'], d['input_gbs'])"
 done
 done
+}
+
+# pinned e2e with the host split: split before the append, producer thread
+# on the device's NUMA node (A/B, interleaved)
+step_p6() {
+O=gpurun_out/r6p6
+mkdir -p $O
+for rnd in 1 2; do
+for a in "" "--split-first" "--e2e-numa" "--e2e-numa --split-first"; do
+timeout -k 10 200 python3 -u bench.py --steps 48 --warmup 4 --e2e pinned $a --no-cpu-baseline > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+cat $O/tmp.json >> $O/bench_e2e.jsonl
+python3 -c "import json; d=json.load(open('$O/tmp.json')); print('r$rnd pinned $a', d['value'], d['host_threads'])"
+done
+timeout -k 10 200 python3 -u bench.py --steps 48 --warmup 4 --e2e pageable --e2e-numa --no-cpu-baseline > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/tmp.json')); print('r$rnd pageable numa', d['value'])"
+done
+}
+
+# hand-off replays (the shared ArrayLedger checked against Array's rules),
+# then the split probe (pageable vs pinned sources)
+step_p7() {
+O=gpurun_out/r6p7
+mkdir -p $O
+timeout -k 10 900 python3 -u -m pytest tests/test_gpu_handoff.py tests/test_gpu_hostsplit.py -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -3 $O/pytest.log
+step_p3
 }
 
 "step_$@"

@@ -8,8 +8,15 @@
 //   both-nt   the same with nontemporal (streaming) stores for both writes
 //   split-nt  the split alone, nontemporal stores
 // Prints GB/s of input per variant and thread count.
+// Argument 2 "pinned": the source frames (and the batch) in hipHostMalloc'd
+// memory, as a camera's DMA ring (-DWITH_HIP, linked with libamdhip64).
 //   g++ -O3 -std=c++20 -pthread tools/split_probe.cpp -o tools/split_probe
+//   g++ -O3 -std=c++20 -pthread -DWITH_HIP -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include \
+//     tools/split_probe.cpp -o split_probe -L/opt/rocm/lib -lamdhip64
 #include <immintrin.h>
+#ifdef WITH_HIP
+#include <hip/hip_runtime_api.h>
+#endif
 
 #include <atomic>
 #include <barrier>
@@ -73,14 +80,32 @@ int
 main(int argc, char** argv)
 {
     const uint32_t frames = argc > 1 ? uint32_t(std::atoi(argv[1])) : 256;
+    const bool pinned = argc > 2 && std::string(argv[2]) == "pinned";
     std::vector<uint32_t> tcounts = { 4, 8, 12, 16 };
-    const uint32_t R = 16; // distinct source frames (128 MiB, past the L3)
-    std::vector<uint8_t> src(R * FRAME);
-    for (size_t i = 0; i < src.size(); i += 8) {
-        const uint64_t x = i * 0x9e3779b97f4a7c15ull;
-        std::memcpy(&src[i], &x, 8);
+    const uint32_t R = 64; // distinct source frames (512 MiB, past the L3)
+    std::vector<uint8_t> src_v;
+    uint8_t* srcp = nullptr;
+    uint8_t* batch = nullptr;
+#ifdef WITH_HIP
+    if (pinned) {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, R * FRAME, hipHostMallocDefault) != hipSuccess)
+            return 1;
+        srcp = static_cast<uint8_t*>(p);
+        if (hipHostMalloc(&p, 64 * FRAME, hipHostMallocDefault) != hipSuccess)
+            return 1;
+        batch = static_cast<uint8_t*>(p);
     }
-    uint8_t* batch = static_cast<uint8_t*>(std::aligned_alloc(4096, 64 * FRAME));
+#endif
+    if (!srcp) {
+        src_v.resize(R * FRAME);
+        srcp = src_v.data();
+        batch = static_cast<uint8_t*>(std::aligned_alloc(4096, 64 * FRAME));
+    }
+    for (size_t i = 0; i < size_t(R) * FRAME; i += 8) {
+        const uint64_t x = i * 0x9e3779b97f4a7c15ull;
+        std::memcpy(&srcp[i], &x, 8);
+    }
     uint8_t* layer = static_cast<uint8_t*>(std::aligned_alloc(4096, NTX * NTX * BPC));
     std::memset(batch, 0, 64 * FRAME);
     std::memset(layer, 0, NTX * NTX * BPC);
@@ -95,7 +120,7 @@ main(int argc, char** argv)
                 sync.arrive_and_wait();
                 const auto t0 = std::chrono::steady_clock::now();
                 for (uint32_t f = 0; f < frames; ++f) {
-                    const uint8_t* fr = src.data() + size_t(f % R) * FRAME;
+                    const uint8_t* fr = srcp + size_t(f % R) * FRAME;
                     uint8_t* bt = batch + size_t(f % 64) * FRAME;
                     for (uint32_t r = a; r < b; r += 16) {
                         const uint32_t e = std::min(b, r + 16);
@@ -122,11 +147,20 @@ main(int argc, char** argv)
                 th.emplace_back(work, t);
             for (auto& x : th)
                 x.join();
-            std::printf("{\"variant\": \"%s\", \"threads\": %u, \"input_gbs\": %.2f}\n",
-                        names[v], T, double(frames) * FRAME / secs / 1e9);
+            std::printf("{\"variant\": \"%s\", \"source\": \"%s\", \"threads\": %u, "
+                        "\"input_gbs\": %.2f}\n",
+                        names[v], pinned ? "pinned" : "pageable", T,
+                        double(frames) * FRAME / secs / 1e9);
             std::fflush(stdout);
         }
-    std::free(batch);
+    if (src_v.empty()) {
+#ifdef WITH_HIP
+        (void)hipHostFree(srcp);
+        (void)hipHostFree(batch);
+#endif
+    } else {
+        std::free(batch);
+    }
     std::free(layer);
     return 0;
 }
