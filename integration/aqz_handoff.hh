@@ -34,6 +34,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -651,6 +652,19 @@ class Handoff
     aqz_status status() const { return status_; }
     uint64_t frames_accepted() const { return accepted_; }
 
+    // Where the consumer thread's time went, in nanoseconds (for a caller
+    // that traces the hand-off; tests/native/handoff_replay prints it):
+    // write_frame in all, and inside it the wait for a batch buffer the stage
+    // has not read yet, the frame copy (+ level-0 split), the waits for a free
+    // host unit buffer and the appends.  sink: the units handed to the sink
+    // (HandoffSink::unit), wherever they were delivered from.
+    struct Stats
+    {
+        uint64_t write_frame_ns = 0, wait_consumed_ns = 0, copy_ns = 0, slot_wait_ns = 0;
+        uint64_t append_ns = 0, sink_ns = 0, units = 0;
+    };
+    const Stats& stats() const { return stats_; }
+
     // pinned host bytes held (batch buffers + unit buffers)
     size_t host_bytes() const
     {
@@ -667,6 +681,7 @@ class Handoff
     {
         if (status_ != AQZ_STATUS_SUCCESS)
             return status_;
+        Timed tw(stats_.write_frame_ns);
         uint32_t r = 0;
         bool run_end = false;
         if (st_.size() > 1) {
@@ -678,6 +693,7 @@ class Handoff
         Input& in = in_[r];
         if (in.n == 0) {
             // refill only once the stage has read this buffer's last batch
+            Timed t(stats_.wait_consumed_ns);
             const aqz_status s = aqz_stage_wait_consumed(st_[r], in.end[in.cur]);
             if (s != AQZ_STATUS_SUCCESS)
                 return status_ = s;
@@ -688,7 +704,10 @@ class Handoff
             if (s != AQZ_STATUS_SUCCESS)
                 return status_ = s;
         }
-        copy_frame_(in.buf[in.cur] + size_t(in.n) * frame_bytes_, frame, L0);
+        {
+            Timed t(stats_.copy_ns);
+            copy_frame_(in.buf[in.cur] + size_t(in.n) * frame_bytes_, frame, L0);
+        }
         if (split_err_ != AQZ_STATUS_SUCCESS)
             return status_ = split_err_;
         ++in.n;
@@ -785,6 +804,29 @@ class Handoff
     static aqz_status worse(aqz_status a, aqz_status b)
     {
         return a != AQZ_STATUS_SUCCESS ? a : b;
+    }
+
+    // adds the scope's duration to a Stats counter
+    struct Timed
+    {
+        uint64_t& acc;
+        std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+        explicit Timed(uint64_t& a)
+          : acc(a)
+        {
+        }
+        ~Timed()
+        {
+            acc += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                              std::chrono::steady_clock::now() - t0)
+                              .count());
+        }
+    };
+    aqz_status to_sink_(Unit& u)
+    {
+        Timed t(stats_.sink_ns);
+        ++stats_.units;
+        return sink_.unit(u);
     }
 
     static void wait_pins_(Slot& s)
@@ -935,7 +977,7 @@ class Handoff
             L.band = 0;
             ++L.layer;
         }
-        return sink_.unit(u);
+        return to_sink_(u);
     }
 
     // close: the rest of level 0's last, partial layer -- its frames not
@@ -973,7 +1015,11 @@ class Handoff
         Input& in = in_[r];
         if (in.n == 0)
             return AQZ_STATUS_SUCCESS;
-        const aqz_status s = aqz_stage_append(st_[r], in.buf[in.cur], in.n, AQZ_MEM_HOST_PINNED);
+        aqz_status s;
+        {
+            Timed t(stats_.append_ns);
+            s = aqz_stage_append(st_[r], in.buf[in.cur], in.n, AQZ_MEM_HOST_PINNED);
+        }
         if (s != AQZ_STATUS_SUCCESS)
             return status_ = s;
         in.end[in.cur] = in.appended;
@@ -1122,6 +1168,7 @@ class Handoff
     // no lease on it.
     aqz_status take_slot_(Slot& slot)
     {
+        Timed t(stats_.slot_wait_ns);
         while (slot.busy) {
             const aqz_status s = progress_(true);
             if (s != AQZ_STATUS_SUCCESS)
@@ -1241,7 +1288,7 @@ class Handoff
         }
         u.lease = Lease(&slot.pins);
         slot.busy = false;
-        return sink_.unit(u);
+        return to_sink_(u);
     }
 
     aqz_status retire_(bool wait_all)
@@ -1280,6 +1327,7 @@ class Handoff
     std::vector<Level> levels_;
     std::deque<Pending> compressing_; // compression issued, in issue order
     std::deque<Pending> inflight_;    // copies issued, in issue order
+    Stats stats_;
     // level 0 split on the host
     HostUnit host_;
     uint32_t rows_ = 0;     // level-0 rows per frame

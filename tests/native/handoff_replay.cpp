@@ -451,6 +451,7 @@ main(int argc, char** argv)
     int rc = 0;
     double seconds = 0;
     uint64_t host_bytes = 0, device_bytes = 0, est_host = 0, est_device = 0;
+    aqz_binding::Handoff::Stats hs{};
     {
         aqz_binding::HandoffOptions ho;
         ho.batch_frames = batch;
@@ -476,6 +477,7 @@ main(int argc, char** argv)
         }
         pool.drain(); // the writer jobs (Array::close_ waits on write_counter_)
         seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        hs = h.stats();
         // what the drop-in holds now (every compressed slot in use) against
         // its estimate (aqz_binding::estimate_memory)
         host_bytes = h.host_bytes();
@@ -510,13 +512,17 @@ main(int argc, char** argv)
            "\"shuffle\": %d, \"device\": %d, \"batch\": %u, \"copy_threads\": %u, "
            "\"pool_threads\": %u, \"host_bytes\": %llu, \"device_bytes\": %llu, "
            "\"estimate_host_bytes\": %llu, \"estimate_device_bytes\": %llu, "
-           "\"level0_split\": \"%s\"}\n",
+           "\"level0_split\": \"%s\", \"consumer_s\": {\"write_frame\": %.4f, "
+           "\"wait_consumed\": %.4f, \"copy\": %.4f, \"slot_wait\": %.4f, \"append\": %.4f, "
+           "\"sink\": %.4f}}\n",
            rc == 0 ? "true" : "false", (unsigned long long)sink.units.load(),
            (unsigned long long)aqz_stage_last_ticket(stages.back()), (unsigned long long)n_frames,
            seconds, in / seconds / 1e9, double(sink.chunk_bytes.load()) / in, codec, clevel,
            shuffle, device, batch, copy_threads, pool_threads, (unsigned long long)host_bytes,
            (unsigned long long)device_bytes, (unsigned long long)est_host,
-           (unsigned long long)est_device, level0_host ? "host" : "device");
+           (unsigned long long)est_device, level0_host ? "host" : "device",
+           hs.write_frame_ns * 1e-9, hs.wait_consumed_ns * 1e-9, hs.copy_ns * 1e-9,
+           hs.slot_wait_ns * 1e-9, hs.append_ns * 1e-9, hs.sink_ns * 1e-9);
     for (aqz_stage* s : stages)
         aqz_stage_destroy(s);
     for (auto& L : sink.lv)

@@ -91,6 +91,8 @@ mkdir -p $O
 g++ -O3 -std=c++20 -pthread -DWITH_HIP -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include tools/split_probe.cpp -o $O/split_probe -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib || exit 1
 timeout -k 10 300 $O/split_probe 256 > $O/split_probe.jsonl 2>&1 || { tail $O/split_probe.jsonl; exit 1; }
 timeout -k 10 300 $O/split_probe 256 pinned >> $O/split_probe.jsonl 2>&1 || { tail $O/split_probe.jsonl; exit 1; }
+timeout -k 10 300 $O/split_probe 256 pinned-thp >> $O/split_probe.jsonl 2>&1 || { tail $O/split_probe.jsonl; exit 1; }
+grep -i -E "AnonHugePages|Hugepagesize" /proc/meminfo; cat /sys/kernel/mm/transparent_hugepage/enabled || true
 cat $O/split_probe.jsonl
 nproc; grep -m1 "model name" /proc/cpuinfo; taskset -p $$ || true
 }
@@ -162,6 +164,25 @@ mkdir -p $O
 timeout -k 10 900 python3 -u -m pytest tests/test_gpu_handoff.py tests/test_gpu_hostsplit.py -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -3 $O/pytest.log
 step_p3
+}
+
+# binding e2e (every codec) next to bench.py --e2e pinned / pageable of the
+# same codecs on one box, with the hand-off's consumer-time breakdown
+step_p8() {
+O=gpurun_out/r6p8
+mkdir -p $O
+timeout -k 10 600 python3 -u tools/binding_e2e.py --frames 2048 --placement-tries 2 --codecs raw,lz4,lz4-bit,blosc-zstd,zstd-1,zstd-3 > $O/binding.jsonl 2> $O/binding.err || { tail $O/binding.err; exit 1; }
+python3 -c "
+import json
+for l in open('$O/binding.jsonl'):
+    d = json.loads(l); print('binding', d['codec_name'], d['level0_split'], d['input_gbs'], d['seconds'], d['consumer_s'])"
+for src in pinned pageable; do
+for a in "" "--compress 1" "--compress 2" "--codec blosc-zstd --compress 1" "--codec zstd" "--codec zstd --clevel 3"; do
+timeout -k 10 200 python3 -u bench.py --steps 16 --warmup 4 --e2e $src $a --no-cpu-baseline > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+cat $O/tmp.json >> $O/bench_e2e.jsonl
+python3 -c "import json; d=json.load(open('$O/tmp.json')); print('bench $src $a', d['value'], d.get('level0_split'))"
+done
+done
 }
 
 "step_$@"

@@ -16,6 +16,7 @@
 #include <immintrin.h>
 #ifdef WITH_HIP
 #include <hip/hip_runtime_api.h>
+#include <sys/mman.h>
 #endif
 
 #include <atomic>
@@ -80,14 +81,15 @@ int
 main(int argc, char** argv)
 {
     const uint32_t frames = argc > 1 ? uint32_t(std::atoi(argv[1])) : 256;
-    const bool pinned = argc > 2 && std::string(argv[2]) == "pinned";
+    const std::string kind = argc > 2 ? argv[2] : "pageable";
+    const bool pinned = kind == "pinned" || kind == "pinned-thp";
     std::vector<uint32_t> tcounts = { 4, 8, 12, 16 };
     const uint32_t R = 64; // distinct source frames (512 MiB, past the L3)
     std::vector<uint8_t> src_v;
     uint8_t* srcp = nullptr;
     uint8_t* batch = nullptr;
 #ifdef WITH_HIP
-    if (pinned) {
+    if (kind == "pinned") {
         void* p = nullptr;
         if (hipHostMalloc(&p, R * FRAME, hipHostMallocDefault) != hipSuccess)
             return 1;
@@ -95,6 +97,26 @@ main(int argc, char** argv)
         if (hipHostMalloc(&p, 64 * FRAME, hipHostMallocDefault) != hipSuccess)
             return 1;
         batch = static_cast<uint8_t*>(p);
+    } else if (kind == "pinned-thp") {
+        // 2 MiB-aligned anonymous memory with transparent huge pages,
+        // touched, then page-locked for DMA (hipHostRegister)
+        auto thp = [](size_t n) -> uint8_t* {
+            const size_t a = size_t(2) << 20;
+            void* p = mmap(nullptr, n + a, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS,
+                           -1, 0);
+            if (p == MAP_FAILED)
+                return nullptr;
+            uint8_t* q = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(p) + a - 1) & ~(a - 1));
+            madvise(q, n, MADV_HUGEPAGE);
+            std::memset(q, 0, n);
+            if (hipHostRegister(q, n, hipHostRegisterDefault) != hipSuccess)
+                return nullptr;
+            return q;
+        };
+        srcp = thp(R * FRAME);
+        batch = thp(64 * FRAME);
+        if (!srcp || !batch)
+            return 1;
     }
 #endif
     if (!srcp) {
@@ -149,14 +171,16 @@ main(int argc, char** argv)
                 x.join();
             std::printf("{\"variant\": \"%s\", \"source\": \"%s\", \"threads\": %u, "
                         "\"input_gbs\": %.2f}\n",
-                        names[v], pinned ? "pinned" : "pageable", T,
+                        names[v], kind.c_str(), T,
                         double(frames) * FRAME / secs / 1e9);
             std::fflush(stdout);
         }
     if (src_v.empty()) {
 #ifdef WITH_HIP
-        (void)hipHostFree(srcp);
-        (void)hipHostFree(batch);
+        if (kind == "pinned") {
+            (void)hipHostFree(srcp);
+            (void)hipHostFree(batch);
+        }
 #endif
     } else {
         std::free(batch);
