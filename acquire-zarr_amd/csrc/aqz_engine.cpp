@@ -2,6 +2,8 @@
 // aqz_engine.cpp -- see aqz_engine.hh.  Citations are to
 // /root/reference/src/streaming/.
 #include "aqz_engine.hh"
+
+#include <hsa/hsa_ext_amd.h>
 #include "aqz_zstd.hh"
 
 #include <algorithm>
@@ -280,6 +282,55 @@ method_valid(int32_t m)
 // ===========================================================================
 // Stage
 // ===========================================================================
+// page-locked host memory (hipHostMalloc / hipHostRegister)?
+static bool
+pinned_host(const void* p)
+{
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// The HSA agents of HIP device `device` and of the host, for DMA-engine
+// copies (hsa_amd_memory_async_copy).  false when either is not found.
+static bool
+find_hsa_agents(int device, hsa_agent_t* gpu, hsa_agent_t* cpu)
+{
+    hipDeviceProp_t prop{};
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess || hsa_init() != HSA_STATUS_SUCCESS)
+        return false;
+    struct Find
+    {
+        uint32_t bdf, domain;
+        hsa_agent_t gpu{ 0 }, cpu{ 0 };
+    } f{ (uint32_t(prop.pciBusID) << 8) | (uint32_t(prop.pciDeviceID) << 3),
+         uint32_t(prop.pciDomainID) };
+    auto cb = [](hsa_agent_t a, void* data) -> hsa_status_t {
+        auto* f = static_cast<Find*>(data);
+        hsa_device_type_t t;
+        if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS)
+            return HSA_STATUS_SUCCESS;
+        if (t == HSA_DEVICE_TYPE_CPU && !f->cpu.handle)
+            f->cpu = a;
+        if (t == HSA_DEVICE_TYPE_GPU) {
+            uint32_t bdf = 0, dom = 0;
+            hsa_agent_get_info(a, hsa_agent_info_t(HSA_AMD_AGENT_INFO_BDFID), &bdf);
+            hsa_agent_get_info(a, hsa_agent_info_t(HSA_AMD_AGENT_INFO_DOMAIN), &dom);
+            if ((bdf & ~7u) == f->bdf && dom == f->domain)
+                f->gpu = a;
+        }
+        return HSA_STATUS_SUCCESS;
+    };
+    if (hsa_iterate_agents(cb, &f) != HSA_STATUS_SUCCESS || !f.gpu.handle || !f.cpu.handle)
+        return false;
+    *gpu = f.gpu;
+    *cpu = f.cpu;
+    return true;
+}
+
 Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
   : desc_(desc)
   , opt_(opt)
@@ -561,6 +612,10 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
         hip_check(hipStreamCreateWithPriority(&comp_lo2_, hipStreamNonBlocking, least),
                   "hipStreamCreate");
     }
+    // AQZ_D2H_SDMA=1: the compressed frames' D2H on a DMA engine, with the
+    // HSA agents of this device (matched by PCI location) and of the host
+    if (const char* e = std::getenv("AQZ_D2H_SDMA"); e && std::atoi(e) != 0)
+        sdma_d2h_ = find_hsa_agents(desc.device, &hsa_gpu_, &hsa_cpu_);
     for (auto& L : lv_) {
         hip_check(hipEventCreateWithFlags(&L.ops_ev, hipEventDisableTiming),
                   "hipEventCreate");
@@ -917,10 +972,22 @@ Stage::~Stage()
     for (size_t i = inflight_head_; i < inflight_.size(); ++i)
         if (inflight_[i].first)
             free_ev_.push_back(inflight_[i].first);
-    for (hipEvent_t e : tickets_)
-        free_ev_.push_back(e);
+    for (const Ticket& t : tickets_) {
+        if (t.ev)
+            free_ev_.push_back(t.ev);
+        if (t.sig.handle) {
+            // a DMA-engine copy still in flight must land before its
+            // buffers go
+            while (hsa_signal_wait_scacquire(t.sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                             HSA_WAIT_STATE_BLOCKED) > 0) {
+            }
+            free_sig_.push_back(t.sig);
+        }
+    }
     for (hipEvent_t e : free_ev_)
         (void)hipEventDestroy(e);
+    for (hsa_signal_t g : free_sig_)
+        (void)hsa_signal_destroy(g);
     for (auto& L : lv_) {
         if (L.ops_ev)
             (void)hipEventDestroy(L.ops_ev);
@@ -1091,10 +1158,20 @@ Stage::issue_ticket()
         free_ev_.pop_back();
     }
     hip_check(hipEventRecord(e, d2h_), "hipEventRecord");
-    tickets_.push_back(e);
+    tickets_.push_back(Ticket{ e, hsa_signal_t{ 0 } });
     ++tickets_issued_;
     // retire what has landed, so a caller that never asks does not hold one
     // live event per copy for the stage's lifetime
+    (void)copies_completed();
+    return tickets_issued_;
+}
+
+// a DMA-engine copy's ticket: complete when its signal reaches 0
+uint64_t
+Stage::issue_ticket(hsa_signal_t sig)
+{
+    tickets_.push_back(Ticket{ nullptr, sig });
+    ++tickets_issued_;
     (void)copies_completed();
     return tickets_issued_;
 }
@@ -1103,16 +1180,28 @@ uint64_t
 Stage::copies_completed(bool wait_all, uint64_t until)
 {
     while (!tickets_.empty() && tickets_done_ < tickets_issued_) {
-        hipEvent_t e = tickets_.front();
-        if (wait_all || tickets_done_ < until) {
-            hip_check(hipEventSynchronize(e), "hipEventSynchronize");
-        } else {
-            const hipError_t q = hipEventQuery(e);
-            if (q == hipErrorNotReady)
+        const Ticket t = tickets_.front();
+        const bool wait = wait_all || tickets_done_ < until;
+        if (t.sig.handle) {
+            if (wait) {
+                while (hsa_signal_wait_scacquire(t.sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                                 HSA_WAIT_STATE_BLOCKED) > 0) {
+                }
+            } else if (hsa_signal_load_scacquire(t.sig) > 0) {
                 break;
-            hip_check(q, "hipEventQuery");
+            }
+            free_sig_.push_back(t.sig);
+        } else {
+            if (wait) {
+                hip_check(hipEventSynchronize(t.ev), "hipEventSynchronize");
+            } else {
+                const hipError_t q = hipEventQuery(t.ev);
+                if (q == hipErrorNotReady)
+                    break;
+                hip_check(q, "hipEventQuery");
+            }
+            free_ev_.push_back(t.ev);
         }
-        free_ev_.push_back(e);
         tickets_.pop_front();
         ++tickets_done_;
     }
@@ -2335,6 +2424,7 @@ Stage::ensure_comp_slots(StageLevel& L)
     L.comp_ev.assign(L.n_slots, nullptr);
     L.cdone_ev.assign(L.n_slots, nullptr);
     L.cdone_pending.assign(L.n_slots, 0);
+    L.cdone_ticket.assign(L.n_slots, 0);
     L.comp_layer.assign(L.n_slots, -1);
     L.h_zin.resize(L.n_slots);
     L.h_zhas.resize(L.n_slots);
@@ -2400,6 +2490,11 @@ Stage::compress_layer_host(StageLevel& L, uint32_t slot, uint64_t layer,
         L.zjob[slot] = std::make_shared<HostLayerJob>();
     // device frames of an earlier blosc-lz4 use of the slot may still be
     // on their way out
+    if (L.cdone_ticket[slot]) {
+        // the slot's frames left on a DMA engine: the host waits for them
+        (void)copies_completed(false, L.cdone_ticket[slot]);
+        L.cdone_ticket[slot] = 0;
+    }
     if (L.cdone_pending[slot]) {
         hip_check(hipStreamWaitEvent(cs, L.cdone_ev[slot], 0), "hipStreamWaitEvent");
         L.cdone_pending[slot] = 0;
@@ -2486,6 +2581,11 @@ Stage::compress_layer(uint32_t level, uint64_t layer, const Compression& c)
         L.zjob[slot]->wait();
     L.comp_host[slot] = 0;
     // the slot's previous frames may still be on their way to the host
+    if (L.cdone_ticket[slot]) {
+        // the slot's frames left on a DMA engine: the host waits for them
+        (void)copies_completed(false, L.cdone_ticket[slot]);
+        L.cdone_ticket[slot] = 0;
+    }
     if (L.cdone_pending[slot]) {
         hip_check(hipStreamWaitEvent(cs, L.cdone_ev[slot], 0), "hipStreamWaitEvent");
         L.cdone_pending[slot] = 0;
@@ -2582,6 +2682,32 @@ Stage::copy_compressed_async(uint32_t level, uint64_t layer, void* dst, size_t c
       reinterpret_cast<const uint64_t*>(L.h_coffsets[slot].p)[L.n_chunks];
     if (cap < total)
         throw Error(2, "destination too small for the compressed layer");
+    if (sdma_d2h_ && pinned_host(dst)) {
+        // one copy on a DMA engine (the compression has finished: the event
+        // above), no blit kernel beside the codec kernels; the next
+        // compression into this slot waits for its ticket (compress_layer).
+        // A DMA engine reads or writes page-locked memory only: pageable or
+        // device destinations take the HIP copy below.
+        hsa_signal_t sig{ 0 };
+        if (free_sig_.empty()) {
+            if (hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS)
+                throw Error(5, "hsa_signal_create failed");
+        } else {
+            sig = free_sig_.back();
+            free_sig_.pop_back();
+            hsa_signal_store_screlease(sig, 1);
+        }
+        if (total == 0) {
+            hsa_signal_store_screlease(sig, 0);
+        } else if (hsa_amd_memory_async_copy(dst, hsa_cpu_, L.cframes[slot].p, hsa_gpu_, total,
+                                             0, nullptr, sig) != HSA_STATUS_SUCCESS) {
+            free_sig_.push_back(sig);
+            throw Error(5, "hsa_amd_memory_async_copy failed");
+        }
+        last_ticket_ = issue_ticket(sig);
+        L.cdone_ticket[slot] = last_ticket_;
+        return;
+    }
     memcpy_pieces(dst, L.cframes[slot].p, total, hipMemcpyDefault, d2h_);
     hip_check(hipEventRecord(L.copy_ev[slot], d2h_), "hipEventRecord");
     hip_check(hipEventRecord(L.cdone_ev[slot], d2h_), "hipEventRecord");

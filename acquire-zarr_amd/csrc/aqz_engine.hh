@@ -16,6 +16,7 @@
 #include "aqz_params.hh"
 
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
 
 #include <deque>
 #include <memory>
@@ -338,6 +339,7 @@ struct StageLevel
     std::vector<hipEvent_t> comp_ev;
     std::vector<hipEvent_t> cdone_ev;      // the slot's frames were copied out
     std::vector<uint8_t> cdone_pending;
+    std::vector<uint64_t> cdone_ticket;    // ... by this DMA-engine ticket (0: none)
     std::vector<int64_t> comp_layer;       // layer compressed in each slot
     // host-side zstd codecs (aqz_hostzstd.hh): per slot the pinned inputs
     // (shuffled or raw chunks, has_data bytes), their D2H event and the
@@ -556,9 +558,22 @@ class Stage
     size_t inflight_head_ = 0;
     std::vector<hipEvent_t> free_ev_;
     uint64_t appended_ = 0, consumed_ = 0;
-    std::deque<hipEvent_t> tickets_;  // hand-off copies not yet retired
+    // a hand-off copy not yet retired: a HIP event on d2h_, or the signal
+    // of a copy on a DMA engine (sdma_d2h_)
+    struct Ticket
+    {
+        hipEvent_t ev = nullptr;
+        hsa_signal_t sig{ 0 };
+    };
+    std::deque<Ticket> tickets_;
     uint64_t tickets_issued_ = 0, tickets_done_ = 0, last_ticket_ = 0;
     uint64_t issue_ticket();
+    uint64_t issue_ticket(hsa_signal_t sig);
+    // compressed frames D2H on an SDMA engine (hsa_amd_memory_async_copy)
+    // instead of HIP's blit kernels (AQZ_D2H_SDMA=1, A/B)
+    bool sdma_d2h_ = false;
+    hsa_agent_t hsa_gpu_{ 0 }, hsa_cpu_{ 0 };
+    std::vector<hsa_signal_t> free_sig_;
     void note_consumed(hipStream_t s, uint64_t frames);
     void retire_consumed(bool wait);
     uint32_t nt_mode_ = 7;           // nontemporal policy: input loads (1), level-0 (2) and level-1/2 (4) stores

@@ -185,4 +185,22 @@ done
 done
 }
 
+# SDMA D2H of compressed frames (AQZ_D2H_SDMA=1) vs the blit kernels: codec
+# tests under SDMA, then the e2e codec rows interleaved
+step_p9() {
+O=gpurun_out/r6p9
+mkdir -p $O
+AQZ_D2H_SDMA=1 timeout -k 10 900 python3 -u -m pytest tests/test_gpu_codec.py tests/test_gpu_handoff.py -m gpu -v -x --timeout 100 --timeout-method thread -p no:cacheprovider -k "codec or compress or lz4 or zstd" > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -3 $O/pytest.log
+for rnd in 1 2; do
+for sd in 0 1; do
+for a in "--compress 1" "--codec blosc-zstd --compress 2" "--codec zstd --clevel 3" "--codec zstd"; do
+AQZ_D2H_SDMA=$sd timeout -k 10 200 python3 -u bench.py --steps 16 --warmup 4 --e2e pinned $a --no-cpu-baseline > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+cat $O/tmp.json >> $O/bench_e2e.jsonl
+python3 -c "import json; d=json.load(open('$O/tmp.json')); print('r$rnd sdma=$sd $a', d['value'], d.get('sink_bytes_per_input_byte'))"
+done
+done
+done
+}
+
 "step_$@"
