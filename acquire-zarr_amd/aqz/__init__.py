@@ -815,6 +815,11 @@ class Stage:
         layer (aqz_stage_zstd_far_ranges; 0 = none ran)."""
         return lib().aqz_stage_zstd_far_ranges(self.h, level)
 
+    def bind_host_thread(self):
+        """aqz_stage_bind_host_thread: pin the calling thread to the CPUs of
+        the device's NUMA node (memory it first touches lands there)."""
+        _check(lib().aqz_stage_bind_host_thread(self.h), "bind_host_thread")
+
     def host_affinity(self):
         """(NUMA node of the device, CPUs the host pools are pinned to)."""
         node, n = C.c_int32(-1), C.c_uint32(0)
