@@ -203,4 +203,29 @@ done
 done
 }
 
+# bench lines of every config with the current build (device-resident)
+step_lines() {
+O=gpurun_out/r6lines${1:-}
+mkdir -p $O
+for c in c2 c3 c4 c5 c1 c2-ref4; do
+timeout -k 10 200 python3 -u bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline > $O/$c.json 2> $O/$c.err || { tail $O/$c.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/$c.json')); r=d['roofline']; p=r['placement']; py=d.get('pyramid_only') or {}; print(json.dumps({'cfg': '$c', 'value': d['value'], 'frac': r['frac'], 'ms': r['kernel_avg_ms'], 'kernel': r['kernel'], 'cand': p.get('candidates_ms'), 'acc': p.get('accepted'), 'stop': p.get('stop'), 'probe': r.get('probe_same_shape_gbs'), 'fop': r.get('frac_of_probe_same_shape'), 'traffic': r.get('traffic'), 'pyr': py.get('input_rate_frac_of_peak'), 'pyr_fop_same_mem': py.get('kernel_frac_of_probe_same_memory'), 'est_gb': round(p['estimate_device_bytes']/1e9, 2), 'peak_gb': round(p['peak_device_bytes']/1e9, 2)}))" | tee -a $O/lines.jsonl
+done
+}
+
+# the final library: suite + smoke, the default line, every config's line
+step_finala() {
+step_full || exit 1
+step_default final || exit 1
+step_lines final || exit 1
+}
+
+# the final library: rocprof trace + PMC of every config (and C2 pyramid-only)
+step_finalb() {
+for c in c2 c3 c4 c5 c1; do
+NO_SQ=1 STEPS=200 bash tools/profile.sh $c r06 || exit 1
+done
+NO_SQ=1 STEPS=200 bash tools/profile.sh c2 r06 pyr || exit 1
+}
+
 "step_$@"
