@@ -2,14 +2,16 @@
 // Built with -fsanitize=address,undefined by tests/test_sanitize_cpu.py
 // together with the product's pure-host sources (aqz_geometry.cpp: the
 // ArrayDimensions / level-rule restatement that drives kernel addressing;
-// aqz_copy.cpp: the staging copy pool; aqz_hostzstd.cpp: the host zstd pool
-// and frame writer) and the CPU oracle (oracle/aqz_oracle.c,
+// aqz_copy.cpp: the staging copy pool; aqz_hostsplit.cpp: the host split of
+// level 0 and its pool; aqz_hostzstd.cpp: the host zstd pool and frame
+// writer) and the CPU oracle (oracle/aqz_oracle.c,
 // aqz_codec_oracle.c).  It drives them hard -- random geometries, a copy pool
 // under concurrent use, host zstd jobs from several threads -- and
 // cross-checks product against oracle, so ASan/UBSan see every path.  Exit
 // status 0 = clean (the sanitizers abort on the first report).
 #include "aqz_copy.hh"
 #include "aqz_geometry.hh"
+#include "aqz_hostsplit.hh"
 #include "aqz_hostzstd.hh"
 
 extern "C" {
@@ -137,6 +139,64 @@ copy_pool()
     }
 }
 
+// the host split of level 0 (aqz_hostsplit.cpp): random geometries, every
+// frame of a layer split in row ranges by a SplitPool (threads sharing a
+// frame's chunks and has_data flags), with the batch copy in the same pass;
+// the layer and flags equal the oracle's, the copy equals the frames
+static void
+host_split(std::mt19937& rng)
+{
+    SplitPool pool(5);
+    for (int it = 0; it < 60; ++it) {
+        const uint32_t h = 1 + rng() % 90, w = 1 + rng() % 90;
+        const int dtype = int(rng() % 10);
+        const std::vector<Dim> dims = { Dim{ kTime, 0, 1 + rng() % 3, 1 },
+                                        Dim{ kSpace, 1 + rng() % 5, 1 + rng() % 3, 1 },
+                                        Dim{ kSpace, h, 1 + rng() % 17, 1 },
+                                        Dim{ kSpace, w, 1 + rng() % 17, 1 } };
+        std::vector<or_dim> od;
+        for (const Dim& x : dims)
+            od.push_back(or_dim{ x.type, x.array_size_px, x.chunk_size_px, x.shard_size_chunks });
+        ArrayDimensions a(dims, dtype);
+        const uint64_t F = a.frames_per_chunk_layer(), bpc = a.bytes_per_chunk();
+        const uint32_t nch = a.number_of_chunks_in_memory();
+        const size_t fb = size_t(h) * w * or_bytes_of_type(dtype);
+        std::vector<uint8_t> frames(F * fb), copy(F * fb, 0), layer(bpc * nch, 0),
+          has(nch, 0), olayer(bpc * nch, 0), ohas(nch, 0);
+        or_fill_splitmix(frames.data(), frames.size(), rng());
+        if (F > 1)
+            std::memset(frames.data(), 0, fb); // a frame without data
+        const uint32_t rows = 1 + rng() % 7;
+        const uint32_t per_frame = (h + rows - 1) / rows;
+        pool.run(size_t(F) * per_frame, [&](size_t i) {
+            const uint64_t f = i / per_frame;
+            const uint32_t r0 = uint32_t(i % per_frame) * rows;
+            split_rows(split_geom(a, f), frames.data() + f * fb, r0, std::min(h, r0 + rows),
+                       layer.data(), 0, nch, has.data(), copy.data() + f * fb);
+        });
+        for (uint64_t f = 0; f < F; ++f)
+            or_write_frame_to_chunks(od.data(), int(od.size()), dtype, f, frames.data() + f * fb,
+                                     olayer.data(), ohas.data());
+        CHECK(layer == olayer);
+        CHECK(has == ohas);
+        CHECK(copy == frames);
+    }
+    // a task that throws reaches the caller, and the pool stays usable
+    bool threw = false;
+    try {
+        pool.run(8, [](size_t i) {
+            if (i == 3)
+                throw Error(1, "task 3");
+        });
+    } catch (const Error&) {
+        threw = true;
+    }
+    CHECK(threw);
+    std::atomic<int> n{ 0 };
+    pool.run(100, [&](size_t) { ++n; });
+    CHECK(n == 100);
+}
+
 using zdec_t = size_t (*)(void*, size_t, const void*, size_t);
 using ziserr_t = unsigned (*)(size_t);
 
@@ -236,6 +296,7 @@ main()
     geometry(rng);
     oracle_cascade(rng);
     copy_pool();
+    host_split(rng);
     host_zstd();
     std::printf("host sanitizer driver: clean\n");
     return 0;

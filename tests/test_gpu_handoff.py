@@ -347,6 +347,9 @@ REPLAY_CASES = {
     # 2-D, ragged tiles and a partial last layer; shards of 2 x 2 chunks
     "layers-2d-ragged": ([(TIME, 0, 4, 2), (SPACE, 300, 64, 2), (SPACE, 260, 64, 2)],
                          4 * 9 + 3, 5),
+    # a bounded append dimension (10 frames in 4-frame chunks): the array is
+    # full at close, its last layer holds 2 frames and padding
+    "bounded-append": ([(TIME, 10, 4, 2), (SPACE, 300, 64, 2), (SPACE, 260, 64, 2)], 10, 3),
 }
 CODECS = {"raw": (0, 0, 0), "lz4-shuffle": (1, 5, 1), "blosc-zstd-bitshuffle": (2, 5, 2),
           "zstd-1": (3, 1, 0), "zstd-3": (3, 3, 0)}

@@ -35,7 +35,8 @@ def test_host_code_clean_under_asan_ubsan(tmp_path):
         assert r.returncode == 0, r.stderr
         objs.append(o)
     srcs = [os.path.join(REPO, "tests", "sanitize", "host_sanitize.cpp")] + [
-        os.path.join(CSRC, f) for f in ("aqz_geometry.cpp", "aqz_copy.cpp", "aqz_hostzstd.cpp")]
+        os.path.join(CSRC, f) for f in ("aqz_geometry.cpp", "aqz_copy.cpp", "aqz_hostsplit.cpp",
+                                        "aqz_hostzstd.cpp")]
     r = subprocess.run(["g++", "-std=c++20", *flags, "-I", CSRC, "-I",
                         os.path.join(REPO, "oracle"), *srcs, *objs, "-ldl", "-o", exe],
                        capture_output=True, text=True)
