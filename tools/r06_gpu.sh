@@ -228,4 +228,26 @@ done
 NO_SQ=1 STEPS=200 bash tools/profile.sh c2 r06 pyr || exit 1
 }
 
+# split probe on the GPU's NUMA node: pageable, pinned (runtime placement)
+# and pinned with the thread's NUMA policy (hipHostMallocNumaUser), 3 rounds
+step_p10() {
+O=gpurun_out/r6p10
+mkdir -p $O
+g++ -O3 -std=c++20 -pthread -DWITH_HIP -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include tools/split_probe.cpp -o $O/split_probe -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib || exit 1
+NODE=$(timeout -k 10 120 python3 -c "
+import torch
+p = torch.cuda.get_device_properties(0)
+a = '%04x:%02x:%02x.0' % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+print(open('/sys/bus/pci/devices/%s/numa_node' % a).read().strip())" 2>/dev/null)
+[ -z "$NODE" ] || [ "$NODE" = "-1" ] && NODE=0
+CPUS=$(cat /sys/devices/system/node/node$NODE/cpulist)
+echo "node $NODE cpus $CPUS"
+for rnd in 1 2 3; do
+for k in pageable pinned pinned-numauser; do
+timeout -k 10 120 taskset -c $CPUS $O/split_probe 128 $k split-nt,both-nt >> $O/split_probe.jsonl 2>&1 || { tail $O/split_probe.jsonl; exit 1; }
+done
+done
+cat $O/split_probe.jsonl
+}
+
 "step_$@"

@@ -82,19 +82,22 @@ main(int argc, char** argv)
 {
     const uint32_t frames = argc > 1 ? uint32_t(std::atoi(argv[1])) : 256;
     const std::string kind = argc > 2 ? argv[2] : "pageable";
-    const bool pinned = kind == "pinned" || kind == "pinned-thp";
+    const bool pinned = kind == "pinned" || kind == "pinned-thp" || kind == "pinned-numauser";
     std::vector<uint32_t> tcounts = { 4, 8, 12, 16 };
     const uint32_t R = 64; // distinct source frames (512 MiB, past the L3)
     std::vector<uint8_t> src_v;
     uint8_t* srcp = nullptr;
     uint8_t* batch = nullptr;
 #ifdef WITH_HIP
-    if (kind == "pinned") {
+    if (kind == "pinned" || kind == "pinned-numauser") {
+        // pinned-numauser: pages placed by this thread's NUMA policy (run
+        // under taskset on the GPU's node: local) instead of the runtime's
+        const unsigned fl = kind == "pinned" ? hipHostMallocDefault : hipHostMallocNumaUser;
         void* p = nullptr;
-        if (hipHostMalloc(&p, R * FRAME, hipHostMallocDefault) != hipSuccess)
+        if (hipHostMalloc(&p, R * FRAME, fl) != hipSuccess)
             return 1;
         srcp = static_cast<uint8_t*>(p);
-        if (hipHostMalloc(&p, 64 * FRAME, hipHostMallocDefault) != hipSuccess)
+        if (hipHostMalloc(&p, 64 * FRAME, fl) != hipSuccess)
             return 1;
         batch = static_cast<uint8_t*>(p);
     } else if (kind == "pinned-thp") {
@@ -132,8 +135,12 @@ main(int argc, char** argv)
     std::memset(batch, 0, 64 * FRAME);
     std::memset(layer, 0, NTX * NTX * BPC);
     const char* names[] = { "copy", "split", "both", "both-nt", "split-nt" };
+    const std::string only = argc > 3 ? argv[3] : "";
     for (int v = 0; v < 5; ++v)
         for (uint32_t T : tcounts) {
+            if (!only.empty() && ("," + only + ",").find("," + std::string(names[v]) + ",") ==
+                                   std::string::npos)
+                continue;
             std::barrier sync(T);
             std::atomic<double> secs{ 0 };
             auto work = [&](uint32_t t) {
@@ -177,7 +184,7 @@ main(int argc, char** argv)
         }
     if (src_v.empty()) {
 #ifdef WITH_HIP
-        if (kind == "pinned") {
+        if (kind == "pinned" || kind == "pinned-numauser") {
             (void)hipHostFree(srcp);
             (void)hipHostFree(batch);
         }
