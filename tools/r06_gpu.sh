@@ -223,9 +223,9 @@ step_lines final || exit 1
 # the final library: rocprof trace + PMC of every config (and C2 pyramid-only)
 step_finalb() {
 for c in c2 c3 c4 c5 c1; do
-NO_SQ=1 STEPS=200 bash tools/profile.sh $c r06 || exit 1
+NO_SQ=1 STEPS=200 bash tools/profile.sh $c ${1:-r06} || exit 1
 done
-NO_SQ=1 STEPS=200 bash tools/profile.sh c2 r06 pyr || exit 1
+NO_SQ=1 STEPS=200 bash tools/profile.sh c2 ${1:-r06} pyr || exit 1
 }
 
 # split probe on the GPU's NUMA node: pageable, pinned (runtime placement)
