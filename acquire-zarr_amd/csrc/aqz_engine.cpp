@@ -2838,6 +2838,9 @@ Stage::split_level0_host(const void* frames, uint64_t n, uint64_t first, uint32_
     if (!frames)
         throw Error(1, "null frames");
     const StageLevel& L = lv_[0];
+    // one layer's frames: another layer's would land on the same chunks
+    if (first / L.F != (first + n - 1) / L.F)
+        throw Error(1, "the frames span two chunk layers");
     const uint64_t fbytes = uint64_t(L.W) * L.H * bpp_;
     // tasks of 64 rows (256 KiB of a 2048-px u16 frame), frame-major
     constexpr uint32_t kRows = 64;

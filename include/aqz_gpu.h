@@ -581,8 +581,9 @@ aqz_status aqz_stage_import_frames(aqz_stage* dst, aqz_stage* src, uint32_t leve
  * that range (else AQZ_STATUS_INVALID_ARGUMENT).  Pure host work: no GPU
  * call, any thread. */
 /* Frames [first_frame, first_frame + n_frames) (level-0 frame ids, in
- * acquisition order, frame after frame at `frames`), split by the stage's
- * host threads (on the NUMA node of its device). */
+ * acquisition order, frame after frame at `frames`; all in one chunk layer,
+ * else AQZ_STATUS_INVALID_ARGUMENT), split by the stage's host threads (on
+ * the NUMA node of its device). */
 aqz_status aqz_stage_split_level0_host(aqz_stage* st, const void* frames, uint64_t n_frames,
                                        uint64_t first_frame, uint32_t chunk0, void* dst,
                                        size_t cap, uint8_t* has_data, size_t has_data_cap);

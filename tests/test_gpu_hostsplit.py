@@ -101,6 +101,15 @@ def test_host_split_stage_memory_and_refusals(gpu):
     da, db = a.memory_usage()["device_bytes"], b.memory_usage()["device_bytes"]
     assert da - db >= ring0
     assert db <= est[1]["device_bytes"]
+    # frames of two chunk layers in one call are refused (they would land on
+    # the same chunks)
+    fr = gpu.HostBuffer(16 * 512 * 512 * 2)
+    lb = b.layout(0)["bytes_per_chunk"] * b.layout(0)["chunks_per_layer"]
+    dst, hd = gpu.HostBuffer(lb), gpu.HostBuffer(b.layout(0)["chunks_per_layer"])
+    with pytest.raises(gpu.AqzError) as e:
+        b.split_level0_host(fr.ptr, 2, 7, dst.ptr, lb, hd.ptr, hd.nbytes)
+    assert e.value.status == 1
+    b.split_level0_host(fr.ptr, 8, 8, dst.ptr, lb, hd.ptr, hd.nbytes)
     a.close()
     b.close()
     with pytest.raises(gpu.AqzError) as e:
