@@ -445,7 +445,7 @@ Stage::Stage(const ArrayDesc& desc, const StageOptions& opt)
     // hipMemMap), when the rings reach 256 MiB.  The fused kernels ran in the
     // fast placement band on such memory in every configuration, box and
     // process tried, and in the slow one on hipMalloc'd rings, on pieces of
-    // the rings' own sizes and on 1 GiB pieces (profiles/r04_vmm_rings.txt;
+    // the rings' own sizes and on 1 GiB pieces (profiles/archive/r04_vmm_rings.txt;
     // DESIGN.md section 3).
     bool per_level = true;
     if (opt_.ring_arena || (opt_.ring_malloc_flags == 0 && arena_rings_ >= kArenaMinRings)) {

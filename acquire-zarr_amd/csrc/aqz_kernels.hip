@@ -2336,7 +2336,7 @@ launch_fused_pyramid_3d(int dtype, int method, const FusedParams& p,
     const bool strip = p.rh_log2 == 6 && p.n_fused <= 4 && !(p.knobs & 256u);
     // two planes at a time (fused_pyramid_strip3d_pair) when level 1 halves
     // z and the group holds whole pairs: 0.8-1.3% faster than one plane at a
-    // time on C4, same stage (profiles/r04_c4_pair_ab.txt); knob 2 keeps
+    // time on C4, same stage (profiles/archive/r04_c4_pair_ab.txt); knob 2 keeps
     // fused_pyramid_strip3d
     // knob 65536: the round-4 pair kernels (6 waves per SIMD, spilling; the
     // pair for XY stages too)
