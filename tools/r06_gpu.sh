@@ -250,4 +250,13 @@ done
 cat $O/split_probe.jsonl
 }
 
+# kernel + copy timelines of the e2e codec rows (tools/e2e_trace.sh,
+# tools/timeline.py over the last 300 ms: the timed steps)
+step_p11() {
+bash tools/e2e_trace.sh r6z3 --steps 16 --warmup 4 --e2e pinned --codec zstd --clevel 3 || exit 1
+python3 tools/timeline.py gpurun_out/e2e_r6z3/trace 300
+bash tools/e2e_trace.sh r6bz2 --steps 16 --warmup 4 --e2e pinned --codec blosc-zstd --compress 2 || exit 1
+python3 tools/timeline.py gpurun_out/e2e_r6bz2/trace 300
+}
+
 "step_$@"

@@ -62,3 +62,17 @@ for k, iv in cg.items():
         k, len(iv), 100 * u / win, cb[k] / 1e9, cb[k] / u if u else 0))
 both = union(kiv + [x for v in cg.values() for x in v])
 print("anything busy: %.1f%%" % (100 * both / win))
+# per stream: busy fraction of the window and its heaviest kernels
+ps = defaultdict(list)
+pk = defaultdict(lambda: defaultdict(float))
+for r in ks:
+    c = clip(r)
+    if not c:
+        continue
+    sid = r.get("Stream_Id", r.get("Queue_Id", "?"))
+    ps[sid].append(c)
+    pk[sid][r["Kernel_Name"][:40]] += (c[1] - c[0]) / 1e6
+for sid, iv in sorted(ps.items(), key=lambda x: -union(x[1])):
+    top = sorted(pk[sid].items(), key=lambda x: -x[1])[:4]
+    print("stream %-4s busy %5.1f%%  " % (sid, 100 * union(iv) / win) +
+          ", ".join("%s %.2f ms" % (k, t) for k, t in top))
