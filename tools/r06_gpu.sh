@@ -259,4 +259,22 @@ bash tools/e2e_trace.sh r6bz2 --steps 16 --warmup 4 --e2e pinned --codec blosc-z
 python3 tools/timeline.py gpurun_out/e2e_r6bz2/trace 300
 }
 
+# compression streams: one per small level (default) vs the round-5 map
+# (AQZ_COMP_STREAMS=2); codec tests first
+step_p12() {
+O=gpurun_out/r6p12
+mkdir -p $O
+timeout -k 10 900 python3 -u -m pytest tests/test_gpu_codec.py tests/test_gpu_zstd.py -m gpu -q -x --timeout 100 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+for rnd in 1 2; do
+for cs in 1 2; do
+for a in "--codec zstd --clevel 3" "--codec blosc-zstd --compress 2" "--compress 1" "--codec zstd"; do
+AQZ_COMP_STREAMS=$cs timeout -k 10 200 python3 -u bench.py --steps 16 --warmup 4 --e2e pinned $a --no-cpu-baseline > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+cat $O/tmp.json >> $O/bench_e2e.jsonl
+python3 -c "import json; d=json.load(open('$O/tmp.json')); print('r$rnd streams=$cs $a', d['value'], d.get('sink_bytes_per_input_byte'))"
+done
+done
+done
+}
+
 "step_$@"
