@@ -46,6 +46,17 @@
 
 namespace zarr {
 
+// The reference classes the binding derives from.  tests/native/
+// binding_exec.cpp defines AQZ_BINDING_TEST_BASES and test doubles under
+// these two names (their members restated from array.cpp / shard.cpp /
+// multiscale.array.cpp, whose definitions do not build in that harness), so
+// that this file's code -- every line of it, unchanged -- runs on the GPU
+// against them.
+#ifndef AQZ_BINDING_TEST_BASES
+using GpuArrayBase = Array;
+using GpuMultiscaleArrayBase = MultiscaleArray;
+#endif
+
 // ZarrCompressionSettings as the reference applies them (compression_params,
 // zarr.stream.cpp:191-208; chunk.cpp:78-106) -> the device codec.
 inline aqz_compression
@@ -109,7 +120,7 @@ class RefShardMap final : public aqz_binding::ShardMap
 };
 
 class GpuArray final
-  : public Array
+  : public GpuArrayBase
   , private aqz_binding::ShardWriter
 {
   public:
@@ -117,7 +128,7 @@ class GpuArray final
              std::shared_ptr<ThreadPool> thread_pool,
              std::shared_ptr<FileHandlePool> file_handle_pool,
              std::shared_ptr<S3ConnectionPool> s3_connection_pool)
-      : Array(config, thread_pool, file_handle_pool, s3_connection_pool)
+      : GpuArrayBase(config, thread_pool, file_handle_pool, s3_connection_pool)
       , map_(config_->dimensions)
       , router_(map_)
     {
@@ -179,7 +190,10 @@ class GpuArray final
     aqz_binding::ShardRouter router_;
     aqz_binding::ArrayLedger ledger_;
 
-    void dispatch_bytes_job_(std::shared_ptr<Shard> shard,
+    // std::shared_ptr<Shard> (array.hh:43)
+    using ShardPtr = decltype(shards_)::value_type;
+
+    void dispatch_bytes_job_(ShardPtr shard,
                              uint32_t chunk_idx,
                              uint32_t internal_idx,
                              uint32_t shard_idx,
@@ -228,7 +242,7 @@ class GpuArray final
 };
 
 class GpuMultiscaleArray final
-  : public MultiscaleArray
+  : public GpuMultiscaleArrayBase
   , private aqz_binding::HandoffSink
 {
   public:
@@ -245,7 +259,7 @@ class GpuMultiscaleArray final
                        const aqz_binding::SlabPlan& plan = {},
                        uint32_t batch_frames = 64,
                        uint32_t host_slots = 3)
-      : MultiscaleArray(config, thread_pool, file_handle_pool, s3_connection_pool)
+      : GpuMultiscaleArrayBase(config, thread_pool, file_handle_pool, s3_connection_pool)
     {
         EXPECT(downsampler_ != nullptr, "GpuMultiscaleArray needs a downsampling method");
         // per-level writers that take GPU-made chunks (create_arrays_,
@@ -344,7 +358,7 @@ class GpuMultiscaleArray final
             (void)aqz_stage_memory_usage(st, &m);
             pinned += m.pinned_bytes;
         }
-        return MultiscaleArray::memory_usage() + pinned + handoff_->host_bytes();
+        return GpuMultiscaleArrayBase::memory_usage() + pinned + handoff_->host_bytes();
     }
 
     // Sidecar (not part of the reference's interface): HBM the stages hold
@@ -397,7 +411,7 @@ class GpuMultiscaleArray final
             LOG_ERROR("Failed to finalize the GPU stage: ", exc.what());
             return false;
         }
-        return MultiscaleArray::close_();
+        return GpuMultiscaleArrayBase::close_();
     }
 
   private:
@@ -532,7 +546,7 @@ estimate_gpu_array_memory(const ZarrArraySettings& settings,
 // keeps the reference's CPU path.  AQZ_Z_SLABS=N splits a volume stream
 // (a z Space dimension before y, acquisition storage order) into N z slabs
 // on the next N selected devices (BASELINE configs[3]: 4 GPUs).
-inline std::unique_ptr<ArrayBase>
+inline std::unique_ptr<GpuMultiscaleArrayBase>
 make_gpu_multiscale_array(std::shared_ptr<ArrayConfig> config,
                           std::shared_ptr<ThreadPool> thread_pool,
                           std::shared_ptr<FileHandlePool> file_handle_pool,
