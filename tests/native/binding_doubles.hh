@@ -50,7 +50,8 @@ struct BindingLog
     {
         uint32_t level, append, shard, internal;
         bool skipped;
-        std::vector<uint8_t> bytes;
+        std::vector<uint8_t> bytes; // empty unless keep_bytes
+        uint64_t nbytes;
     };
     struct ShardEnd
     {
@@ -72,6 +73,7 @@ struct BindingLog
     std::vector<ShardEnd> shard_ends;
     std::map<uint32_t, LevelEnd> levels;
     std::vector<std::string> errors;
+    bool keep_bytes = true; // false: a timing run, sizes only
 
     void error(const std::string& e)
     {
@@ -146,8 +148,10 @@ class ShardDouble
         }
         {
             std::lock_guard lk(binding_log().mu);
-            binding_log().chunks.push_back(
-              BindingLog::Chunk{ cfg_.level, cfg_.append, cfg_.shard, internal, false, buffer });
+            BindingLog& log = binding_log();
+            log.chunks.push_back(BindingLog::Chunk{
+              cfg_.level, cfg_.append, cfg_.shard, internal, false,
+              log.keep_bytes ? buffer : std::vector<uint8_t>{}, buffer.size() });
         }
         return count_down_();
     }
@@ -172,7 +176,7 @@ class ShardDouble
         {
             std::lock_guard lk(binding_log().mu);
             binding_log().chunks.push_back(
-              BindingLog::Chunk{ cfg_.level, cfg_.append, cfg_.shard, internal, true, {} });
+              BindingLog::Chunk{ cfg_.level, cfg_.append, cfg_.shard, internal, true, {}, 0 });
         }
         return count_down_();
     }

@@ -20,16 +20,19 @@
 //   batch 0 = the hook (make_gpu_multiscale_array: its defaults) instead of
 //   the constructor with (batch, host_slots); z_slabs >= 2 sets AQZ_Z_SLABS
 //   (every slab on the visible device(s), as select_device hands them out);
-//   frames follow (synth 0 only).
+//   frames follow (synth 0), or synth 1 / 2: camera-like / random frames
+//   made here (synth_frames.hh, 8 distinct frames round robin).
 // OUT: the AQZ4 records of handoff_replay, made from what the shard doubles
 //   received: per level, every (append-shard row, shard, internal index)
 //   written or skipped, mapped back to (layer, chunk) through the level's
 //   ArrayDimensions (chunk 0xffffffff: a shard's ragged padding), and the
 //   frame counts at each Array::rollover_.
+//   OUT "-": a timing run -- nothing written, chunk sizes only.
 // stdout: one JSON summary line; exit 0 only if the binding's calls all
 //   returned what the reference's interface promises and no double
 //   recorded an error.
 #include "binding_doubles.hh"
+#include "synth_frames.hh"
 
 // the binding itself, unchanged
 #include "multiscale.array.gpu.cpp"
@@ -86,12 +89,24 @@ main(int argc, char** argv)
     if (!rd(f, &dtype) || !rd(f, &method) || !rd(f, &batch) || !rd(f, &slots) ||
         !rd(f, &device) || !rd(f, &codec) || !rd(f, &clevel) || !rd(f, &shuffle) ||
         !rd(f, &copy_threads) || !rd(f, &pool_threads) || !rd(f, &synth) || !rd(f, &tries) ||
-        !rd(f, &n_slabs) || !rd(f, &n_frames) || !rd(f, &fbytes) || synth != 0)
+        !rd(f, &n_slabs) || !rd(f, &n_frames) || !rd(f, &fbytes) || n_frames == 0)
         return 2;
-    std::vector<uint8_t> frames(n_frames * fbytes);
-    if (!rd(f, frames.data(), frames.size()))
-        return 2;
+    // the caller's frame vectors (ZarrStream_s hands write_frame its own)
+    std::vector<std::vector<uint8_t>> frames;
+    if (synth == 0) {
+        frames.assign(n_frames, std::vector<uint8_t>(fbytes));
+        for (auto& fr : frames)
+            if (!rd(f, fr.data(), fbytes))
+                return 2;
+    } else {
+        const uint32_t R = uint32_t(std::min<uint64_t>(n_frames, 8));
+        const std::vector<uint8_t> v = aqz_test::synth_frames(synth, dtype, fbytes, R);
+        for (uint32_t i = 0; i < R; ++i)
+            frames.emplace_back(v.begin() + i * fbytes, v.begin() + (i + 1) * fbytes);
+    }
     fclose(f);
+    const bool record = std::strcmp(argv[2], "-") != 0;
+    binding_log().keep_bytes = record;
     (void)copy_threads;
     (void)tries;
     if (n_slabs > 1)
@@ -178,15 +193,14 @@ main(int argc, char** argv)
         std::vector<uint8_t> short_frame(fbytes - 1);
         if (gpu->write_frame(short_frame, bw, 0) != WriteResult::FrameSizeMismatch || bw != 0)
             fail("a short frame was not refused with FrameSizeMismatch");
-        std::vector<uint8_t> fr(frames.begin(), frames.begin() + fbytes);
         bw = 7;
-        if (gpu->write_frame(fr, bw, 1) != WriteResult::FrameOutOfOrder || bw != 0)
+        if (gpu->write_frame(frames[0], bw, 1) != WriteResult::FrameOutOfOrder || bw != 0)
             fail("frame id 1 first was not refused with FrameOutOfOrder");
     }
     size_t mem_during = 0;
+    const auto t_frames = std::chrono::steady_clock::now();
     for (uint64_t i = 0; i < n_frames; ++i) {
-        std::vector<uint8_t> fr(frames.begin() + i * fbytes, frames.begin() + (i + 1) * fbytes);
-        const WriteResult r = gpu->write_frame(fr, bw, i);
+        const WriteResult r = gpu->write_frame(frames[i % frames.size()], bw, i);
         if (r != WriteResult::Ok || bw != fbytes) {
             fail("write_frame " + std::to_string(i) + " returned " + std::to_string(int(r)));
             break;
@@ -199,10 +213,9 @@ main(int argc, char** argv)
     const size_t max = gpu->max_bytes();
     bool oob_probed = false;
     if (max > 0 && n_frames * fbytes == max) {
-        std::vector<uint8_t> fr(frames.begin(), frames.begin() + fbytes);
         bw = 7;
         oob_probed = true;
-        if (gpu->write_frame(fr, bw, n_frames) != WriteResult::OutOfBounds || bw != 0)
+        if (gpu->write_frame(frames[0], bw, n_frames) != WriteResult::OutOfBounds || bw != 0)
             fail("a frame past the bounded append dimension was not refused");
     }
     const size_t mem_end = gpu->memory_usage();
@@ -230,11 +243,18 @@ main(int argc, char** argv)
     }
     if (!closed)
         fail("close_ returned false");
+    // close_ has drained every chunk job (Array::close_ waits on
+    // write_counter_): the stream's data is in the shards
+    const auto t_closed = std::chrono::steady_clock::now();
     const uint64_t group_md = array->group_metadata_writes();
     array.reset();
     pool->await_stop();
-    const double seconds =
-      std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    // first write_frame to close_ done: the stream's rate; the one-off
+    // costs (stage creation and placement, teardown) apart
+    const auto t_end = std::chrono::steady_clock::now();
+    const double seconds = std::chrono::duration<double>(t_closed - t_frames).count();
+    const double construct_seconds = std::chrono::duration<double>(t_frames - t0).count();
+    const double destroy_seconds = std::chrono::duration<double>(t_end - t_closed).count();
 
     BindingLog& log = binding_log();
     const uint32_t nl = uint32_t(level_dims.size());
@@ -287,7 +307,7 @@ main(int argc, char** argv)
     for (const auto& c : log.chunks)
         if (c.level < nl)
             per_level[c.level].push_back(&c);
-    FILE* o = fopen(argv[2], "wb");
+    FILE* o = fopen(record ? argv[2] : "/dev/null", "wb");
     if (!o)
         return 2;
     fwrite("AQZ4", 1, 4, o);
@@ -344,7 +364,7 @@ main(int argc, char** argv)
         fail(e);
     uint64_t chunk_bytes = 0;
     for (const auto& c : log.chunks)
-        chunk_bytes += c.bytes.size();
+        chunk_bytes += c.nbytes;
     std::string lv = "[";
     for (uint32_t l = 0; l < nl; ++l) {
         const auto& e = log.levels[l];
@@ -371,6 +391,7 @@ main(int argc, char** argv)
     errs += "]";
     printf("{\"summary\": true, \"ok\": %s, \"failures\": %zu, \"errors\": %s, "
            "\"factory\": %s, \"n_levels\": %u, \"frames\": %llu, \"seconds\": %.4f, "
+           "\"construct_seconds\": %.4f, \"destroy_seconds\": %.4f, "
            "\"input_gbs\": %.3f, \"sink_bytes_per_input_byte\": %.4f, \"codec\": %d, "
            "\"chunks_recorded\": %zu, \"shards_by_countdown\": %llu, \"shards_at_close\": %llu, "
            "\"shards_incomplete\": %llu, \"group_metadata_writes\": %llu, "
@@ -378,7 +399,7 @@ main(int argc, char** argv)
            "\"estimate_host_bytes\": %llu, \"estimate_device_bytes\": %llu, "
            "\"max_bytes\": %zu, \"oob_probed\": %s, \"levels\": %s}\n",
            failures.empty() ? "true" : "false", failures.size(), errs.c_str(),
-           factory ? "true" : "false", nl, (unsigned long long)n_frames, seconds,
+           factory ? "true" : "false", nl, (unsigned long long)n_frames, seconds, construct_seconds, destroy_seconds,
            double(n_frames) * double(fbytes) / seconds / 1e9,
            double(chunk_bytes) / (double(n_frames) * double(fbytes)), codec, log.chunks.size(),
            (unsigned long long)by_countdown, (unsigned long long)at_close,

@@ -7,6 +7,11 @@ hand-off buffers by a pool of writer threads (GpuArray::write_unit without
 the shard I/O).  One JSON line per run.
 
   python3 tools/binding_e2e.py [--frames 512] [--codecs raw,lz4,...]
+  python3 tools/binding_e2e.py --exec ...   the binding itself
+      (oracle/_ref/binding_exec: GpuMultiscaleArray / GpuArray over the test
+      doubles of Array / MultiscaleArray / Shard, as ZarrStream_s drives it --
+      write_frame per frame, the chunk jobs on the reference's ThreadPool,
+      finalize; the shard doubles keep sizes only)
 """
 import argparse
 import json
@@ -18,6 +23,7 @@ import tempfile
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(REPO, "tests", "native", "handoff_replay")
+EXEC = os.path.join(REPO, "oracle", "_ref", "binding_exec")
 CODECS = {"raw": (0, 0, 0), "lz4": (1, 5, 1), "lz4-bit": (1, 5, 2),
           "blosc-zstd": (2, 5, 1), "blosc-zstd-bit": (2, 5, 2), "zstd-1": (3, 1, 0),
           "zstd-3": (3, 3, 0)}
@@ -34,6 +40,8 @@ def main():
     ap.add_argument("--placement-tries", type=int, default=0)
     ap.add_argument("--level0", default="", choices=["", "host", "device"],
                     help="force the level-0 side (default: the binding's choice)")
+    ap.add_argument("--exec", action="store_true",
+                    help="run the binding itself (binding_exec) instead of the replay")
     args = ap.parse_args()
     env = dict(os.environ)
     if args.level0:
@@ -49,12 +57,13 @@ def main():
                 f.write(struct.pack("<iiIIiiiiIIIIIQQ", 1, 1, args.batch, args.host_slots, 0,
                                     *CODECS[name], args.copy_threads, args.pool_threads, 1,
                                     args.placement_tries, 1, args.frames, 2048 * 2048 * 2))
-            r = subprocess.run([EXE, job, "-"], capture_output=True, text=True, timeout=600,
+            r = subprocess.run([EXEC if args.exec else EXE, job, "-"], capture_output=True, text=True, timeout=600,
                                env=env)
             if r.returncode != 0:
                 sys.exit(r.stdout[-2000:] + r.stderr[-2000:])
             s = json.loads(r.stdout.strip().splitlines()[-1])
             s["codec_name"] = name
+            s["harness"] = "binding_exec" if args.exec else "handoff_replay"
             s["workload"] = ("C2 frames u16 2048x2048, 256x256 chunks (t-chunk 64), 4 levels "
                              "(reference rule), camera-like, pageable frame per write_frame "
                              "-> binding hand-off -> sink pool copy")

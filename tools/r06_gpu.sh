@@ -185,6 +185,30 @@ done
 done
 }
 
+# the binding itself (oracle/_ref/binding_exec) end to end, every codec,
+# interleaved with the replay of its hand-off and bench.py --e2e pageable of
+# the same codec on one box (profiles/r06_binding_exec_e2e.jsonl)
+step_p13() {
+O=gpurun_out/r6p13
+mkdir -p $O
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_binding_exec.py -m gpu -q -x --timeout 150 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+declare -A BA=([raw]="" [lz4]="--compress 1" [blosc-zstd]="--codec blosc-zstd --compress 1" [zstd-1]="--codec zstd" [zstd-3]="--codec zstd --clevel 3")
+for rnd in 1 2; do
+for c in raw lz4 blosc-zstd zstd-1 zstd-3; do
+for h in exec replay; do
+x=""; [ $h = exec ] && x="--exec"
+timeout -k 10 400 python3 -u tools/binding_e2e.py --frames 2048 --placement-tries 2 --codecs $c $x > $O/b.json 2>> $O/binding.err || { tail $O/binding.err; exit 1; }
+cat $O/b.json >> $O/binding.jsonl
+python3 -c "import json; d=json.loads(open('$O/b.json').read().splitlines()[-1]); print('r$rnd', d['harness'], d['codec_name'], round(d['input_gbs'], 2))"
+done
+timeout -k 10 200 python3 -u bench.py --steps 16 --warmup 4 --e2e pageable ${BA[$c]} --no-cpu-baseline > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+cat $O/tmp.json >> $O/bench_e2e.jsonl
+python3 -c "import json; d=json.load(open('$O/tmp.json')); print('r$rnd bench-pageable $c', d['value'])"
+done
+done
+}
+
 # SDMA D2H of compressed frames (AQZ_D2H_SDMA=1) vs the blit kernels: codec
 # tests under SDMA, then the e2e codec rows interleaved
 step_p9() {
