@@ -101,3 +101,29 @@ def expected_stage_layers(dims, dtype, method, frames, max_levels=0,
 
 def layer_pixels(buf: np.ndarray, dtype: int) -> np.ndarray:
     return buf.view(NP_DTYPES[dtype])
+
+
+def assemble_layers(layers, dims, dtype) -> np.ndarray:
+    """The stored array a zarr reader sees, from chunk layers {layer: bytes}
+    of storage-order `dims` [(type, size, chunk, shard)]: the regular chunk
+    grid in C order (zarr v3), chunk layer k = append indices
+    [k*c0, (k+1)*c0), chunks of a layer in C order over dims 1..n-1, each
+    chunk a C-order block of the chunk shape (ragged edges padded)."""
+    npdt = NP_DTYPES[dtype]
+    sizes = [d[1] for d in dims]
+    chunks = [d[2] for d in dims]
+    n_layers = max(layers) + 1
+    if sizes[0] == 0:
+        sizes[0] = n_layers * chunks[0]
+    grid = [-(-s // c) for s, c in zip(sizes[1:], chunks[1:])]
+    padded = [n_layers * chunks[0]] + [g * c for g, c in zip(grid, chunks[1:])]
+    out = np.zeros(padded, dtype=npdt)
+    per_chunk = int(np.prod(chunks))
+    for k, buf in layers.items():
+        px = np.frombuffer(bytes(buf), dtype=npdt)
+        for ci, idx in enumerate(np.ndindex(*grid)):
+            block = px[ci * per_chunk:(ci + 1) * per_chunk].reshape(chunks)
+            sl = [slice(k * chunks[0], (k + 1) * chunks[0])]
+            sl += [slice(j * c, (j + 1) * c) for j, c in zip(idx, chunks[1:])]
+            out[tuple(sl)] = block
+    return out[tuple(slice(0, s) for s in sizes)]
