@@ -30,7 +30,7 @@ import subprocess
 import pytest
 
 from helpers import expected_stage_layers
-from oracle_bindings import MEAN, SPACE, TIME, U16, synthetic_frames
+from oracle_bindings import F32, I16, MAX, MEAN, MIN, SPACE, TIME, U8, U16, synthetic_frames
 from test_gpu_handoff import CODECS, REPLAY_CASES, Replay, _check_routing, _decode
 
 pytestmark = pytest.mark.gpu
@@ -42,7 +42,7 @@ EXE = os.environ.get("BINDING_EXEC") or os.path.join(
 
 
 def _run_exec(tmp_path, dims, frames, batch, slots, codec=(0, 0, 0), pool_threads=4,
-              z_slabs=1):
+              z_slabs=1, dtype=U16, method=MEAN):
     """Run the binding on `frames`; batch 0 = through make_gpu_multiscale_array."""
     assert os.path.exists(EXE), "make -C oracle binding (built by __graft_entry__.build)"
     job, out = tmp_path / "job.bin", tmp_path / "out.bin"
@@ -51,7 +51,7 @@ def _run_exec(tmp_path, dims, frames, batch, slots, codec=(0, 0, 0), pool_thread
         f.write(b"AQZ2" + struct.pack("<I", len(dims)))
         for d in dims:
             f.write(struct.pack("<iIII", *d))
-        f.write(struct.pack("<iiIIiiiiIIIIIQQ", U16, MEAN, batch, slots, 0, *codec, 0,
+        f.write(struct.pack("<iiIIiiiiIIIIIQQ", dtype, method, batch, slots, 0, *codec, 0,
                             pool_threads, 0, 0, z_slabs, len(frames), fb))
         f.write(frames.tobytes())
     r = subprocess.run([EXE, str(job), str(out)], capture_output=True, text=True, timeout=300)
@@ -83,7 +83,7 @@ def _run_exec(tmp_path, dims, frames, batch, slots, codec=(0, 0, 0), pool_thread
     return Replay([], summary, got, padding, rollovers)
 
 
-def _check_exec(exp, fw, r, codec, st):
+def _check_exec(exp, fw, r, codec, st, dtype=U16):
     got = r.got
     seen = set()
     for (l, layer), (buf, flags) in exp.items():
@@ -105,6 +105,7 @@ def _check_exec(exp, fw, r, codec, st):
     for e in sm["levels"]:
         l = e["level"]
         fbl = st.layout(l)["frame_bytes"]
+        assert fbl % {U8: 1, U16: 2, I16: 2, F32: 4}[dtype] == 0
         assert e["frames_written"] == fw[l], e
         assert e["total_bytes_written"] == fw[l] * fbl, e
         assert e["last_frame_id"] == max(fw[l] - 1, 0), e
@@ -172,4 +173,41 @@ def test_binding_executes_z_slabs(gpu, tmp_path, slabs):
     r = _run_exec(tmp_path, dims, frames, 8, 3, codec=CODECS["lz4-shuffle"], z_slabs=slabs)
     st = gpu.Stage(dims, U16, MEAN)
     _check_exec(exp, fw, r, CODECS["lz4-shuffle"], st)
+    st.close()
+
+
+@pytest.mark.parametrize("codec", ["raw", "lz4-shuffle"])
+@pytest.mark.parametrize("dtype,method", [(U8, MAX), (I16, MIN), (F32, MEAN)],
+                         ids=["u8-max", "i16-min", "f32-mean"])
+def test_binding_executes_dtypes_and_methods(gpu, tmp_path, dtype, method, codec):
+    """The settings' data type and downsampling method through the binding
+    (ZarrArraySettings -> ArrayConfig -> aqz_array_desc)."""
+    dims, n, batch = REPLAY_CASES["layers-2d-ragged"]
+    frames = synthetic_frames(dtype, n, dims[-2][1], dims[-1][1], 29 + dtype)
+    frames[5:9] = 0
+    exp, fw, _ = expected_stage_layers(dims, dtype, method, frames)
+    r = _run_exec(tmp_path, dims, frames, batch, 2, codec=CODECS[codec], dtype=dtype,
+                  method=method)
+    st = gpu.Stage(dims, dtype, method)
+    _check_exec(exp, fw, r, CODECS[codec], st, dtype)
+    st.close()
+
+
+@pytest.mark.parametrize("codec", ["raw", "zstd-1"])
+def test_binding_executes_c2_frames(gpu, tmp_path, codec):
+    """C2's frames (u16 2048 x 2048, 256-px chunks) through the hook, with
+    16-frame chunk layers in append shards of 2 layers: five full layers
+    (two rollovers) and a partial sixth; 8 MiB frames, so the copy threads
+    split each frame's rows between them."""
+    from codec_helpers import libzstd
+    if CODECS[codec][0] in (2, 3) and libzstd() is None:
+        pytest.skip("no libzstd to decode with")
+    dims = [(TIME, 0, 16, 2), (SPACE, 2048, 256, 1), (SPACE, 2048, 256, 1)]
+    frames = synthetic_frames(U16, 5 * 16 + 7, 2048, 2048, 2) & 0x0fff
+    frames[20:23] = 0
+    exp, fw, _ = expected_stage_layers(dims, U16, MEAN, frames)
+    r = _run_exec(tmp_path, dims, frames, 0, 0, codec=CODECS[codec], pool_threads=8)
+    assert r.summary["factory"] and [len(x) for x in r.rollovers][0] == 2
+    st = gpu.Stage(dims, U16, MEAN)
+    _check_exec(exp, fw, r, CODECS[codec], st)
     st.close()
