@@ -958,6 +958,11 @@ Stage::~Stage()
     // host compression jobs read pinned inputs and wait on events: finish
     // them before anything is freed (the pool drains its queue)
     zpool_.reset();
+    // other stages' imports still reading this stage's rings
+    for (auto& L : lv_)
+        for (auto& v : L.peer_ev)
+            for (const auto& e : v)
+                (void)hipEventSynchronize(e.get());
     if (stream_)
         (void)hipStreamSynchronize(stream_);
     for (hipStream_t s : { h2d_, comp_, comp_lo_, comp_lo2_, d2h_ })
@@ -1381,6 +1386,13 @@ Stage::enter_layer(StageLevel& L, uint64_t layer)
     if (!L.copy_pending.empty() && L.copy_pending[slot]) {
         hip_check(hipStreamWaitEvent(stream_, L.copy_ev[slot], 0), "hipStreamWaitEvent");
         L.copy_pending[slot] = 0;
+    }
+    if (!L.peer_ev.empty()) {
+        // another stage's import of the slot, on any device
+        std::lock_guard<std::mutex> lk(access_mu_);
+        for (const auto& e : L.peer_ev[slot])
+            hip_check(hipStreamWaitEvent(stream_, e.get(), 0), "hipStreamWaitEvent");
+        L.peer_ev[slot].clear();
     }
     L.slot_layer[slot] = int64_t(layer);
 }
@@ -2768,9 +2780,18 @@ Stage::import_frames(Stage* src, uint32_t level, uint64_t layer, uint32_t first,
                 uint32_t(layer / L.n_slots + 1), stream_),
               "import launch");
     if (src) {
-        // src's slot holds the layer until the copy has read it
-        hip_check(hipEventRecord(S->copy_ev[slot], stream_), "hipEventRecord");
-        S->copy_pending[slot] = 1;
+        // src's slot holds the layer until the copy has read it: an event of
+        // this stage's device on this stream, for src's stream to wait on
+        // before it reuses the slot (src->copy_ev is src's device's event
+        // and may not be recorded here)
+        hipEvent_t e = nullptr;
+        hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        std::shared_ptr<ihipEvent_t> ev(e, [](hipEvent_t x) { (void)hipEventDestroy(x); });
+        hip_check(hipEventRecord(e, stream_), "hipEventRecord");
+        std::lock_guard<std::mutex> lk(src->access_mu_);
+        if (S->peer_ev.empty())
+            S->peer_ev.resize(S->n_slots);
+        S->peer_ev[slot].push_back(std::move(ev));
     }
 }
 

@@ -329,6 +329,11 @@ struct StageLevel
     // ring slot in flight; the slot's next layer waits for it
     std::vector<hipEvent_t> ready_ev, copy_ev;
     std::vector<uint8_t> copy_pending;
+    // per slot: other stages' imports of the slot (import_frames), each an
+    // event of the reading stage's device recorded on its stream (an event
+    // is recorded only on a stream of its own device); the slot's next
+    // layer waits for them
+    std::vector<std::vector<std::shared_ptr<ihipEvent_t>>> peer_ev;
     DevBuf flag_bytes;                     // per slot: has_data as 0/1 bytes
     // device compression of resident layers (compress_layer): per slot the
     // frames, their offsets (device and pinned host copy) and an event
@@ -593,7 +598,7 @@ class Stage
     DevBuf arena_;                      // every level's ring (the shipped arena)
     uint64_t arena_rings_ = 0;          // bytes of the rings inside it
     bool arena_fallback_ = false;       // the VMM arena failed: per-level rings
-    std::mutex access_mu_;              // grant_access
+    std::mutex access_mu_;              // grant_access, StageLevel::peer_ev
     std::vector<int> granted_;          // devices mapped into a VMM arena
     // import_frames from another device reads this stage's rings: a
     // virtual-memory arena must be mapped for that device too
