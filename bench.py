@@ -143,6 +143,36 @@ def fill_ring(torch, ring, dtype, seed):
         ring.view(torch.float32).uniform_(0.0, 65535.0, generator=g)
 
 
+def device_code_sha256(path):
+    """sha256 of a shared library's device code (its .hip_fatbin section:
+    every gfx950 kernel code object), read from the ELF section table.  Two
+    builds that differ only in host code have the same value, so a kernel
+    profile of one describes the other's kernels."""
+    import hashlib
+    import struct
+    try:
+        with open(path, "rb") as fh:
+            data = fh.read()
+    except OSError:
+        return None
+    if data[:4] != b"\x7fELF" or data[4] != 2:  # ELF64 only
+        return None
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+
+    def sec(i):
+        name, _, _, _, off, size = struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize)
+        return name, off, size
+
+    _, stroff, _ = sec(shstrndx)
+    for i in range(shnum):
+        name, off, size = sec(i)
+        end = data.index(b"\0", stroff + name)
+        if data[stroff + name:end] == b".hip_fatbin":
+            return hashlib.sha256(data[off:off + size]).hexdigest()
+    return None
+
+
 def lib_sha256():
     """sha256 of the libaqz_gpu.so this process loaded (aqz.lib())."""
     import hashlib
@@ -154,8 +184,17 @@ def lib_sha256():
         return None
 
 
+def lib_device_code_sha256():
+    """device_code_sha256 of the libaqz_gpu.so this process loaded."""
+    import aqz
+    try:
+        return device_code_sha256(aqz.lib()._name)
+    except AttributeError:
+        return None
+
+
 def pmc_traffic(config, pyramid_only, kernel, frames, ring_allocation, run_ms=None,
-                lib_sha=None):
+                lib_sha=None, dev_sha=None):
     """Per-launch HBM bytes of the dominant kernel from the newest committed
     rocprofv3 PMC summary for this configuration whose rings were allocated
     the same way as this run's (tools/profile.sh -> tools/pmc_summary.py ->
@@ -175,8 +214,11 @@ def pmc_traffic(config, pyramid_only, kernel, frames, ring_allocation, run_ms=No
             found.append((f, d))
     if not found:
         return None, None, None
-    # a profile of the library build this run loaded, when there is one
+    # a profile of the library build this run loaded, when there is one,
+    # else of a build with the same device code (host-only changes)
     same = [fd for fd in found if lib_sha and fd[1].get("lib_sha256") == lib_sha]
+    if not same and dev_sha:
+        same = [fd for fd in found if fd[1].get("device_code_sha256") == dev_sha]
     found = same or found
     # MI355X boxes run the same kernel at different speeds (DESIGN.md
     # section 5); the bytes do not change with the box.  Of the profiles of
@@ -822,7 +864,8 @@ def main():
     # how the chunk-layer rings were allocated (aqz_placement_report.mode)
     pl["ring_allocation"] = ring_allocation(pl)
     traffic, traffic_src, prof = pmc_traffic(args.config, args.pyramid_only, kernel, B,
-                                             pl["ring_allocation"], avg_ms, lib_sha256())
+                                             pl["ring_allocation"], avg_ms, lib_sha256(),
+                                             lib_device_code_sha256())
 
     result = {
         "metric": f"input GB/s, device-resident multiscale downsample, {DTYPE_WORDS[dt]} "
@@ -865,6 +908,9 @@ def main():
     if prof:
         result["roofline"]["traffic_profile_same_build"] = bool(
             prof.get("lib_sha256") and prof.get("lib_sha256") == lib_sha256())
+        result["roofline"]["traffic_profile_same_device_code"] = bool(
+            prof.get("device_code_sha256")
+            and prof.get("device_code_sha256") == lib_device_code_sha256())
         # the profiled run of this command: its rocprof kernel average and
         # the frac it gives, next to this run's
         pa = prof.get("steady_avg_duration_ns") or prof.get("avg_duration_ns")

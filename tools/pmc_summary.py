@@ -59,6 +59,16 @@ def main():
     shaf = os.path.join(d, "lib.sha256")
     if os.path.exists(shaf):
         res["lib_sha256"] = open(shaf).read().strip()
+    # its device code (the .hip_fatbin section): builds that differ only in
+    # host code share it (bench.py falls back to a summary of the same
+    # device code); recorded when the profiled library is the one in-tree
+    sys.path.insert(0, REPO)
+    from bench import device_code_sha256, REPO as _r  # noqa: F401
+    lib = os.path.join(REPO, "acquire-zarr_amd", "libaqz_gpu.so")
+    import hashlib
+    if res.get("lib_sha256") and os.path.exists(lib) and \
+            hashlib.sha256(open(lib, "rb").read()).hexdigest() == res["lib_sha256"]:
+        res["device_code_sha256"] = device_code_sha256(lib)
     # the traced bench line: how its rings were allocated (bench.py matches
     # a summary to a run by it) and its own event-timed kernel average
     try:
