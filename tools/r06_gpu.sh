@@ -209,6 +209,23 @@ done
 done
 }
 
+# the binding's copy threads (HandoffOptions::copy_threads) for the raw
+# hand-off: 8 / 12 / 16, interleaved, with bench.py --e2e pageable beside
+step_p14() {
+O=gpurun_out/r6p14
+mkdir -p $O
+for rnd in 1 2 3; do
+for ct in 8 12 16; do
+timeout -k 10 400 python3 -u tools/binding_e2e.py --frames 2048 --placement-tries 2 --codecs raw --copy-threads $ct > $O/b.json 2>> $O/binding.err || { tail $O/binding.err; exit 1; }
+cat $O/b.json >> $O/binding.jsonl
+python3 -c "import json; d=json.loads(open('$O/b.json').read().splitlines()[-1]); print('r$rnd copy $ct', round(d['input_gbs'], 2), d['consumer_s'])"
+done
+timeout -k 10 200 python3 -u bench.py --steps 16 --warmup 4 --e2e pageable --no-cpu-baseline > $O/tmp.json 2> $O/tmp.err || { tail $O/tmp.err; exit 1; }
+cat $O/tmp.json >> $O/bench_e2e.jsonl
+python3 -c "import json; d=json.load(open('$O/tmp.json')); print('r$rnd bench-pageable raw', d['value'])"
+done
+}
+
 # SDMA D2H of compressed frames (AQZ_D2H_SDMA=1) vs the blit kernels: codec
 # tests under SDMA, then the e2e codec rows interleaved
 step_p9() {
