@@ -54,7 +54,11 @@ def _run_exec(tmp_path, dims, frames, batch, slots, codec=(0, 0, 0), pool_thread
         f.write(struct.pack("<iiIIiiiiIIIIIQQ", dtype, method, batch, slots, 0, *codec, 0,
                             pool_threads, 0, 0, z_slabs, len(frames), fb))
         f.write(frames.tobytes())
-    r = subprocess.run([EXE, str(job), str(out)], capture_output=True, text=True, timeout=300)
+    # BINDING_EXEC_PREFIX: a launcher that execs the harness before it
+    # touches the GPU (tools/binding_sanitize.sh: setarch -R for TSan)
+    pre = os.environ.get("BINDING_EXEC_PREFIX", "").split()
+    r = subprocess.run(pre + [EXE, str(job), str(out)], capture_output=True, text=True,
+                       timeout=300)
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert r.returncode == 0 and lines, r.stdout[-3000:] + r.stderr[-3000:]
     summary = lines[-1]
