@@ -31,7 +31,7 @@ else
   san=${2:-thread}
   export TSAN_OPTIONS="halt_on_error=1 exitcode=66 second_deadlock_stack=1 suppressions=$PWD/tools/tsan.supp"
   export ASAN_OPTIONS="halt_on_error=1 exitcode=66 detect_leaks=1 protect_shadow_gap=0"
-  export LSAN_OPTIONS="exitcode=66"
+  export LSAN_OPTIONS="exitcode=66 suppressions=$PWD/tools/lsan.supp"
   # ASLR off for the harness (setarch -R execs it before it touches the
   # GPU): gcc's TSan rejects libraries mapped below its high-memory range
   BINDING_EXEC_PREFIX="setarch $(uname -m) -R" BINDING_EXEC="$OUT/binding_exec_$san" timeout -k 10 900 python3 -u -m pytest -x -v \
