@@ -41,7 +41,9 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <atomic>
 #include <set>
+#include <thread>
 
 namespace {
 
@@ -157,6 +159,46 @@ main(int argc, char** argv)
 
     std::vector<std::string> failures;
     auto fail = [&](const std::string& s) { failures.push_back(s); };
+    // BINDING_EXEC_PROGRESS=file: a line every 10 s (phase, frames written,
+    // chunks the shard doubles received), so a stalled run says where it is
+    std::atomic<int> phase{ 0 };
+    std::atomic<uint64_t> frames_done{ 0 };
+    std::atomic<bool> stop_watch{ false };
+    std::thread watch;
+    if (const char* pf = std::getenv("BINDING_EXEC_PROGRESS")) {
+        watch = std::thread([&, path = std::string(pf)] {
+            const char* names[] = { "construct", "write_frame", "close", "teardown" };
+            for (int k = 1; !stop_watch.load(); ++k) {
+                for (int i = 0; i < 100 && !stop_watch.load(); ++i)
+                    std::this_thread::sleep_for(std::chrono::milliseconds(100));
+                if (stop_watch.load())
+                    break;
+                size_t chunks = 0;
+                {
+                    std::lock_guard lk(binding_log().mu);
+                    chunks = binding_log().chunks.size();
+                }
+                if (FILE* w = fopen(path.c_str(), "a")) {
+                    fprintf(w, "%s t=%ds phase=%s frames=%llu/%llu chunks=%zu\n", argv[1], 10 * k,
+                            names[phase.load()], (unsigned long long)frames_done.load(),
+                            (unsigned long long)n_frames, chunks);
+                    fclose(w);
+                }
+            }
+        });
+    }
+    // every return below stops and joins the watchdog first
+    struct WatchGuard
+    {
+        std::atomic<bool>& stop;
+        std::thread& t;
+        ~WatchGuard()
+        {
+            stop = true;
+            if (t.joinable())
+                t.join();
+        }
+    } watch_guard{ stop_watch, watch };
     const auto t0 = std::chrono::steady_clock::now();
     std::unique_ptr<GpuMultiscaleArrayBase> array;
     bool factory = batch == 0;
@@ -199,7 +241,8 @@ main(int argc, char** argv)
     }
     size_t mem_during = 0;
     const auto t_frames = std::chrono::steady_clock::now();
-    for (uint64_t i = 0; i < n_frames; ++i) {
+    phase = 1;
+    for (uint64_t i = 0; i < n_frames; ++i, frames_done = i) {
         const WriteResult r = gpu->write_frame(frames[i % frames.size()], bw, i);
         if (r != WriteResult::Ok || bw != fbytes) {
             fail("write_frame " + std::to_string(i) + " returned " + std::to_string(int(r)));
@@ -237,6 +280,7 @@ main(int argc, char** argv)
     }
     bool closed = false;
     try {
+        phase = 2;
         closed = array->finalize(); // finalize_array -> GpuMultiscaleArray::close_
     } catch (const std::exception& e) {
         fail(std::string("close: ") + e.what());
@@ -247,8 +291,10 @@ main(int argc, char** argv)
     // write_counter_): the stream's data is in the shards
     const auto t_closed = std::chrono::steady_clock::now();
     const uint64_t group_md = array->group_metadata_writes();
+    phase = 3;
     array.reset();
     pool->await_stop();
+    stop_watch = true;
     // first write_frame to close_ done: the stream's rate; the one-off
     // costs (stage creation and placement, teardown) apart
     const auto t_end = std::chrono::steady_clock::now();

@@ -34,6 +34,9 @@ else
   export LSAN_OPTIONS="exitcode=66 suppressions=$PWD/tools/lsan.supp"
   # ASLR off for the harness (setarch -R execs it before it touches the
   # GPU): gcc's TSan rejects libraries mapped below its high-memory range
+  # a stalled harness writes where it is every 10 s (and so keeps the run
+  # from looking silent until pytest's own limit ends it)
+  export BINDING_EXEC_PROGRESS="$PWD/gpurun_out/binding_progress_$san.txt"
   BINDING_EXEC_PREFIX="setarch $(uname -m) -R" BINDING_EXEC="$OUT/binding_exec_$san" timeout -k 10 900 python3 -u -m pytest -x -v \
     --timeout 300 --timeout-method thread tests/test_gpu_binding_exec.py ${3:+-k "$3"} \
     > "gpurun_out/binding_$san.log" 2>&1
