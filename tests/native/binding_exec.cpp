@@ -141,14 +141,25 @@ main(int argc, char** argv)
     settings.multiscale = true;
     settings.downsampling_method = ZarrDownsamplingMethod(method);
     settings.max_levels = 0;
-    settings.storage_dimension_order = nullptr;
+    // BINDING_EXEC_ORDER="0,2,1": the array's storage_dimension_order
+    std::vector<size_t> order;
+    if (const char* o = std::getenv("BINDING_EXEC_ORDER")) {
+        for (const char* c = o; *c;) {
+            order.push_back(size_t(std::strtoul(c, const_cast<char**>(&c), 10)));
+            if (*c == ',')
+                ++c;
+        }
+        if (order.size() != nd)
+            return 2;
+    }
+    settings.storage_dimension_order = order.empty() ? nullptr : order.data();
 
     // make_array_config (zarr.stream.cpp:330-375)
     std::vector<ZarrDimension> zd;
     for (const auto& p : props)
         zd.emplace_back(p.name, p.type, p.array_size_px, p.chunk_size_px, p.shard_size_chunks,
                         "", 1.0);
-    auto dims = std::make_shared<ArrayDimensions>(std::move(zd), settings.data_type);
+    auto dims = std::make_shared<ArrayDimensions>(std::move(zd), settings.data_type, order);
     auto config = std::make_shared<ArrayConfig>(
       "/binding_exec", "", std::nullopt, compression_params_of(settings.compression_settings),
       dims, settings.data_type, std::optional(settings.downsampling_method), 0,

@@ -215,3 +215,30 @@ def test_binding_executes_c2_frames(gpu, tmp_path, codec):
     st = gpu.Stage(dims, U16, MEAN)
     _check_exec(exp, fw, r, CODECS[codec], st)
     st.close()
+
+
+@pytest.mark.parametrize("codec", ["raw", "lz4-shuffle"])
+def test_binding_executes_xy_storage_order(gpu, tmp_path, codec, monkeypatch):
+    """storage_dimension_order with X and Y swapped (ZarrArraySettings ->
+    ArrayDimensions' target order and aqz_array_desc): a raw hand-off then
+    keeps level 0 on the device (level0_on_host_for), and every stored frame
+    is the acquired one transposed (array.cpp:488-504, 525-533).  The append
+    dimension is bounded, as in the reference's own test_swap_xy: with an
+    unbounded one and only X/Y permuted the reference's ArrayDimensions
+    cannot be built (compute_transposition, array.dimensions.cpp:96-102:
+    lookup_dims is 0 and `lookup_dims - 1` wraps; it faults), so no stream
+    reaches the binding with that array."""
+    import numpy as np
+    acq = [(TIME, 16, 4, 2), (SPACE, 300, 64, 2), (SPACE, 260, 64, 2)]
+    frames = synthetic_frames(U16, 16, 300, 260, 45)
+    if CODECS[codec][0]:
+        frames &= 0x00ff
+    frames[5:9] = 0
+    perm = [0, 2, 1]
+    stored = np.ascontiguousarray(frames.transpose(0, 2, 1))
+    exp, fw, _ = expected_stage_layers([acq[i] for i in perm], U16, MEAN, stored)
+    monkeypatch.setenv("BINDING_EXEC_ORDER", "0,2,1")
+    r = _run_exec(tmp_path, acq, frames, 5, 2, codec=CODECS[codec])
+    st = gpu.Stage(acq, U16, MEAN, storage_order=perm)
+    _check_exec(exp, fw, r, CODECS[codec], st)
+    st.close()
