@@ -42,8 +42,8 @@
 #include <cstring>
 #include <map>
 #include <atomic>
-#include <set>
 #include <thread>
+#include <tuple>
 
 namespace {
 
