@@ -177,7 +177,7 @@ class GpuArray final
     }
     void skip_chunk(uint32_t shard, uint32_t internal, uint32_t) override
     {
-        dispatch_skip_job_(shards_[shard], internal, shard);
+        dispatch_skip_(shards_[shard], internal, shard);
     }
     bool should_rollover() override { return should_rollover_(); }
     void rollover() override
@@ -193,6 +193,48 @@ class GpuArray final
     // std::shared_ptr<Shard> (array.hh:43)
     using ShardPtr = decltype(shards_)::value_type;
 
+    // A writer job ends: write_counter_ drops under write_counter_mutex_, the
+    // mutex Array::close_ checks its predicate under (array.cpp:390-392), so
+    // close_ cannot miss the last notification.  The reference's own jobs
+    // decrement without it (array.cpp:649-650, 743-744): a job that ends
+    // between close_'s predicate check and its wait is a lost wake-up, and
+    // close_ then waits forever -- seen here as an occasional stalled close
+    // of the binding harness, which is why the binding runs its skips with
+    // its own jobs too instead of Array::dispatch_skip_job_.
+    void job_done_()
+    {
+        {
+            std::lock_guard<std::mutex> lk(write_counter_mutex_);
+            write_counter_.fetch_sub(1);
+        }
+        write_counter_cv_.notify_all();
+    }
+
+    // Array::dispatch_skip_job_ (array.cpp:625-662) with job_done_
+    void dispatch_skip_(ShardPtr shard, uint32_t internal_idx, uint32_t shard_idx)
+    {
+        write_counter_.fetch_add(1);
+        auto job = [this, shard, internal_idx, shard_idx](std::string& err) {
+            ThreadPool::TaskResult result = ThreadPool::TaskResult::Success;
+            try {
+                if (!shard->skip_chunk(internal_idx)) {
+                    err = "Failed to skip chunk " + std::to_string(internal_idx) + " of shard " +
+                          std::to_string(shard_idx);
+                    result = ThreadPool::TaskResult::Fatal;
+                }
+            } catch (const std::exception& exc) {
+                err = std::string("Failed skipping chunk: ") + exc.what();
+                result = ThreadPool::TaskResult::Fatal;
+            }
+            job_done_();
+            return result;
+        };
+        if (thread_pool_->n_threads() == 1 || !thread_pool_->push_job(job)) {
+            if (!thread_pool_->execute_job(std::move(job)))
+                LOG_ERROR("Failed to skip chunk ", internal_idx, " of shard ", shard_idx);
+        }
+    }
+
     void dispatch_bytes_job_(ShardPtr shard,
                              uint32_t chunk_idx,
                              uint32_t internal_idx,
@@ -202,7 +244,6 @@ class GpuArray final
                              aqz_binding::Lease lease)
     {
         write_counter_.fetch_add(1);
-        write_counter_cv_.notify_all();
         auto job = [this, shard, chunk_idx, internal_idx, shard_idx, bytes, nbytes,
                     lease = std::move(lease)](std::string& err) mutable {
             ThreadPool::TaskResult result = ThreadPool::TaskResult::Success;
@@ -229,8 +270,7 @@ class GpuArray final
                 err = std::string("Failed to write chunk: ") + exc.what();
                 result = ThreadPool::TaskResult::Fatal;
             }
-            write_counter_.fetch_sub(1);
-            write_counter_cv_.notify_all();
+            job_done_();
             return result;
         };
         if (thread_pool_->n_threads() == 1 || !thread_pool_->push_job(job)) {

@@ -57,8 +57,17 @@ def _run_exec(tmp_path, dims, frames, batch, slots, codec=(0, 0, 0), pool_thread
     # BINDING_EXEC_PREFIX: a launcher that execs the harness before it
     # touches the GPU (tools/binding_sanitize.sh: setarch -R for TSan)
     pre = os.environ.get("BINDING_EXEC_PREFIX", "").split()
-    r = subprocess.run(pre + [EXE, str(job), str(out)], capture_output=True, text=True,
-                       timeout=300)
+    env = dict(os.environ)
+    # where a stalled run is (phase, frames, chunks), every 10 s
+    prog = tmp_path / "progress.txt"
+    env.setdefault("BINDING_EXEC_PROGRESS", str(prog))
+    try:
+        r = subprocess.run(pre + [EXE, str(job), str(out)], capture_output=True, text=True,
+                           timeout=float(os.environ.get("BINDING_EXEC_TIMEOUT", "240")),
+                           env=env)
+    except subprocess.TimeoutExpired as e:
+        where = prog.read_text() if prog.exists() else "(no progress file)"
+        raise AssertionError(f"binding_exec stalled: {where}\nstderr: {e.stderr}") from None
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert r.returncode == 0 and lines, r.stdout[-3000:] + r.stderr[-3000:]
     summary = lines[-1]
