@@ -32,6 +32,7 @@
 #include "zarr.common.hh"
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <map>
@@ -437,8 +438,20 @@ class ArrayDouble
                                 std::to_string(bytes_to_flush_) +
                                 " bytes to flush from CPU chunk buffers");
         {
+            // the reference waits with the predicate (array.cpp:390-392) and
+            // would block forever on a lost wake-up (a job that decremented
+            // without the mutex between the check and the wait); here a
+            // timed wait that then finds the counter at 0 records that
+            // instead of hanging
             std::unique_lock lock(write_counter_mutex_);
-            write_counter_cv_.wait(lock, [this]() { return write_counter_.load() == 0; });
+            while (write_counter_.load() != 0) {
+                if (write_counter_cv_.wait_for(lock, std::chrono::seconds(5)) ==
+                      std::cv_status::timeout &&
+                    write_counter_.load() == 0)
+                    binding_log().error("level " + std::to_string(level_()) +
+                                        ": close_ missed the writer jobs' last "
+                                        "notification (a lost wake-up)");
+            }
         }
         bool ok = finalize_shards_();
         close_sinks_();
